@@ -1,0 +1,136 @@
+/*
+ * spittle_hip.h -- C ABI of the MI355X-native Whisper transcription backend.
+ *
+ * This is the drop-in boundary for Spittle's transcription hot path.  In the
+ * reference, TranscriptionManager owns a transcribe_rs::engines::whisper::WhisperEngine
+ * through `LoadedEngine::Whisper` (/root/reference/src-tauri/src/managers/transcription.rs:29-34)
+ * and calls, from different OS threads but serialised by one Mutex
+ * (transcription.rs:36-47, 437):
+ *
+ *   WhisperEngine::new() + load_model(&path)     transcription.rs:261-276  -> spt_ctx_create
+ *   transcribe_samples(Vec<f32>, Some(params))   transcription.rs:494-503  -> spt_transcribe
+ *   unload_model() / Drop                         transcription.rs:175-208  -> spt_ctx_destroy
+ *
+ * with WhisperInferenceParams { language, translate, initial_prompt, ..Default }
+ * (transcription.rs:445-499) -> spt_infer_params, and TranscriptionResult.text
+ * (transcription.rs:537-546) -> spt_result.text.  The Rust binding a maintainer
+ * adds (spittle-hip-sys / HipWhisperEngine) is shown in INTEGRATION.md.
+ *
+ * Conventions (same as the in-tree Swift bridge,
+ * src-tauri/swift/apple_intelligence_bridge.h:10-24): plain pointers and sizes,
+ * status codes plus a message, library-owned results released by
+ * spt_result_free.  Input PCM is borrowed for the duration of the call (16 kHz
+ * mono f32 in [-1, 1]).  A context is not thread-affine (every entry point
+ * selects its device) but is not re-entrant: callers serialise, as the app does.
+ */
+#ifndef SPITTLE_HIP_H
+#define SPITTLE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPT_ABI_VERSION 1
+
+typedef enum {
+    SPT_OK = 0,
+    SPT_ERR_INVALID_ARG = 1,   /* bad pointer / size / parameter */
+    SPT_ERR_LOAD = 2,          /* model spec or file could not be loaded */
+    SPT_ERR_DEVICE = 3,        /* HIP runtime / device failure */
+    SPT_ERR_OOM = 4,           /* device allocation failed */
+    SPT_ERR_UNSUPPORTED = 5,   /* feature not implemented (e.g. beam search) */
+    SPT_ERR_INTERNAL = 6
+} spt_status;
+
+typedef enum { SPT_DTYPE_F32 = 0, SPT_DTYPE_BF16 = 1 } spt_dtype;
+
+/* decode flags (spt_infer_params.flags) */
+#define SPT_SUPPRESS_BLANK  1u  /* whisper_full_params.suppress_blank (default on) */
+#define SPT_NO_TIMESTAMPS   2u  /* whisper_full_params.no_timestamps */
+#define SPT_IGNORE_EOT      4u  /* benchmark protocol: keep decoding past <|endoftext|> */
+
+typedef struct {
+    int32_t dtype;        /* spt_dtype: weights + activations (accumulation is always f32) */
+    int32_t device;       /* HIP device ordinal */
+    int32_t max_batch;    /* utterance (30 s window) capacity per call */
+    int32_t reserved;
+    uint64_t seed;        /* synthetic weights: PRNG seed */
+} spt_model_params;
+
+typedef struct {
+    const char* language;        /* ISO-639-1 ("en", "zh", ...); NULL = auto-detect */
+    int32_t translate;           /* task <|translate|> instead of <|transcribe|> */
+    const char* initial_prompt;  /* jargon prompt (src-tauri/src/jargon.rs:594); needs a vocab */
+    uint32_t flags;              /* SPT_SUPPRESS_BLANK | SPT_NO_TIMESTAMPS | SPT_IGNORE_EOT */
+    int32_t max_new_tokens;      /* generated tokens per 30 s window (<= 220 like whisper.cpp) */
+    float temperature;           /* only 0 (greedy) is implemented */
+    int32_t beam_size;           /* only 1 (greedy) is implemented */
+    const int32_t* forced_tokens;/* test hook (teacher forcing): [batch][n_forced] or NULL */
+    int32_t n_forced;
+} spt_infer_params;
+
+typedef struct {
+    char* text;             /* UTF-8; for synthetic models the token ids as "[id]" */
+    int32_t* tokens;        /* generated token ids (EOT included, stops after it) */
+    float* top1;            /* suppressed logit of the chosen token, per step */
+    float* top2;            /* runner-up suppressed logit, per step */
+    int32_t n_tokens;
+    int32_t n_windows;      /* 30 s windows the input was split into */
+} spt_result;
+
+typedef struct {
+    int32_t n_mels, d, n_head, n_enc, n_dec, n_vocab, n_audio_ctx, n_text_ctx;
+    int32_t dtype, max_batch;
+    int64_t weight_bytes;
+    int64_t workspace_bytes;
+} spt_model_info;
+
+/* per-phase device time of the last call, from HIP events on the engine stream */
+typedef struct {
+    double mel_ms, encoder_ms, cross_kv_ms, decode_ms, total_ms, h2d_ms;
+    int32_t n_decode_passes;
+    int32_t batch;
+} spt_timings;
+
+typedef struct spt_ctx spt_ctx;
+
+const char* spt_version(void);
+void spt_default_model_params(spt_model_params* p);
+void spt_default_infer_params(spt_infer_params* p);
+
+/* model_spec: "synthetic:<tiny.en|tiny|base|small|medium|large-v3>[:enc=N][:dec=N][:seed=S]"
+ * or a filesystem path (ggml .bin loading is not implemented yet -> SPT_ERR_UNSUPPORTED). */
+spt_status spt_ctx_create(const char* model_spec, const spt_model_params* params, spt_ctx** out,
+                          char* err, size_t errlen);
+void spt_ctx_destroy(spt_ctx* ctx);
+const char* spt_last_error(const spt_ctx* ctx);
+spt_status spt_ctx_info(const spt_ctx* ctx, spt_model_info* info);
+
+/* one utterance, host PCM (moved Vec<f32> in the app) */
+spt_status spt_transcribe(spt_ctx* ctx, const float* pcm16k, size_t n_samples, const spt_infer_params* params,
+                          spt_result** out);
+/* a batch of utterances, host PCM; out[batch] */
+spt_status spt_transcribe_batch(spt_ctx* ctx, const float* const* pcm, const size_t* n_samples, size_t batch,
+                                const spt_infer_params* params, spt_result** out);
+/* a batch of <= 30 s windows already resident in device memory: pcm_dev[b * stride + i] */
+spt_status spt_transcribe_batch_device(spt_ctx* ctx, const float* pcm_dev, size_t stride, const size_t* n_samples,
+                                       size_t batch, const spt_infer_params* params, spt_result** out);
+void spt_result_free(spt_result* r);
+
+spt_status spt_get_timings(const spt_ctx* ctx, spt_timings* t);
+
+/* test hooks (parity against the CPU restatement) */
+/* normalised log-mel of one window [n_mels][3000] (f32) */
+spt_status spt_debug_mel(spt_ctx* ctx, const float* pcm16k, size_t n_samples, float* out);
+/* encoder output [1500][d] (f32) from a host mel [n_mels][3000] */
+spt_status spt_debug_encode(spt_ctx* ctx, const float* mel, float* out);
+/* sum|w| and sum w of the weight tensor with a given id (oracle/wo_model.c table) */
+spt_status spt_debug_weight_checksum(spt_ctx* ctx, int32_t tensor_id, double* out2);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,91 @@
+"""ctypes binding of the C ABI in include/spittle_hip.h (libspittle_hip.so, in-tree).
+
+The product path has no CPU fallback: if the HIP library is missing this module
+raises, loudly, at import of the engine.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libspittle_hip.so")
+
+# status codes
+SPT_OK, SPT_ERR_INVALID_ARG, SPT_ERR_LOAD, SPT_ERR_DEVICE, SPT_ERR_OOM, SPT_ERR_UNSUPPORTED, SPT_ERR_INTERNAL = range(7)
+STATUS_NAMES = {0: "OK", 1: "INVALID_ARG", 2: "LOAD", 3: "DEVICE", 4: "OOM", 5: "UNSUPPORTED", 6: "INTERNAL"}
+SPT_DTYPE_F32, SPT_DTYPE_BF16 = 0, 1
+SPT_SUPPRESS_BLANK, SPT_NO_TIMESTAMPS, SPT_IGNORE_EOT = 1, 2, 4
+
+# every symbol include/spittle_hip.h declares
+EXPORTS = [
+    "spt_version", "spt_default_model_params", "spt_default_infer_params", "spt_ctx_create",
+    "spt_ctx_destroy", "spt_last_error", "spt_ctx_info", "spt_transcribe", "spt_transcribe_batch",
+    "spt_transcribe_batch_device", "spt_result_free", "spt_get_timings", "spt_debug_mel",
+    "spt_debug_encode", "spt_debug_weight_checksum",
+]
+
+
+class ModelParams(C.Structure):
+    _fields_ = [("dtype", C.c_int32), ("device", C.c_int32), ("max_batch", C.c_int32),
+                ("reserved", C.c_int32), ("seed", C.c_uint64)]
+
+
+class InferParams(C.Structure):
+    _fields_ = [("language", C.c_char_p), ("translate", C.c_int32), ("initial_prompt", C.c_char_p),
+                ("flags", C.c_uint32), ("max_new_tokens", C.c_int32), ("temperature", C.c_float),
+                ("beam_size", C.c_int32), ("forced_tokens", C.POINTER(C.c_int32)), ("n_forced", C.c_int32)]
+
+
+class Result(C.Structure):
+    _fields_ = [("text", C.c_char_p), ("tokens", C.POINTER(C.c_int32)), ("top1", C.POINTER(C.c_float)),
+                ("top2", C.POINTER(C.c_float)), ("n_tokens", C.c_int32), ("n_windows", C.c_int32)]
+
+
+class ModelInfo(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("n_mels", "d", "n_head", "n_enc", "n_dec", "n_vocab", "n_audio_ctx",
+                                          "n_text_ctx", "dtype", "max_batch")] + \
+               [("weight_bytes", C.c_int64), ("workspace_bytes", C.c_int64)]
+
+
+class Timings(C.Structure):
+    _fields_ = [(n, C.c_double) for n in ("mel_ms", "encoder_ms", "cross_kv_ms", "decode_ms", "total_ms",
+                                           "h2d_ms")] + [("n_decode_passes", C.c_int32), ("batch", C.c_int32)]
+
+
+_lib = None
+
+
+def load():
+    """Load libspittle_hip.so (built by __graft_entry__.build / make -C spittle_amd/csrc)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"spittle_amd: HIP library not built: {LIB_PATH} (run `make -C spittle_amd/csrc`)")
+    L = C.CDLL(LIB_PATH)
+    vp, fp = C.c_void_p, C.POINTER(C.c_float)
+    L.spt_version.restype = C.c_char_p
+    L.spt_default_model_params.argtypes = [C.POINTER(ModelParams)]
+    L.spt_default_infer_params.argtypes = [C.POINTER(InferParams)]
+    L.spt_ctx_create.argtypes = [C.c_char_p, C.POINTER(ModelParams), C.POINTER(vp), C.c_char_p, C.c_size_t]
+    L.spt_ctx_create.restype = C.c_int
+    L.spt_ctx_destroy.argtypes = [vp]
+    L.spt_last_error.argtypes = [vp]
+    L.spt_last_error.restype = C.c_char_p
+    L.spt_ctx_info.argtypes = [vp, C.POINTER(ModelInfo)]
+    L.spt_transcribe.argtypes = [vp, fp, C.c_size_t, C.POINTER(InferParams), C.POINTER(C.POINTER(Result))]
+    L.spt_transcribe_batch.argtypes = [vp, C.POINTER(fp), C.POINTER(C.c_size_t), C.c_size_t,
+                                       C.POINTER(InferParams), C.POINTER(C.POINTER(Result))]
+    L.spt_transcribe_batch_device.argtypes = [vp, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t), C.c_size_t,
+                                              C.POINTER(InferParams), C.POINTER(C.POINTER(Result))]
+    L.spt_result_free.argtypes = [C.POINTER(Result)]
+    L.spt_get_timings.argtypes = [vp, C.POINTER(Timings)]
+    L.spt_debug_mel.argtypes = [vp, fp, C.c_size_t, fp]
+    L.spt_debug_encode.argtypes = [vp, fp, fp]
+    L.spt_debug_weight_checksum.argtypes = [vp, C.c_int32, C.POINTER(C.c_double)]
+    for fn in ("spt_ctx_info", "spt_transcribe", "spt_transcribe_batch", "spt_transcribe_batch_device",
+               "spt_get_timings", "spt_debug_mel", "spt_debug_encode", "spt_debug_weight_checksum"):
+        getattr(L, fn).restype = C.c_int
+    _lib = L
+    return L

@@ -1,0 +1,392 @@
+// capi.cpp -- the extern "C" boundary declared in include/spittle_hip.h.
+//
+// Mirrors transcribe-rs' WhisperEngine surface as Spittle uses it
+// (/root/reference/src-tauri/src/managers/transcription.rs: new + load_model 261-276,
+// transcribe_samples 494-503, unload_model 175-208): status codes + message,
+// borrowed input PCM, library-owned results.  Utterances longer than 30 s are cut
+// into 30 s windows that are decoded as independent batch items and their text is
+// concatenated (whisper.cpp's seek loop conditions each window on the previous
+// text and timestamps; that is a documented difference).
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <memory>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/spittle_hip.h"
+#include "common.h"
+#include "engine.h"
+
+using spt::Engine;
+
+struct spt_ctx {
+    std::unique_ptr<Engine> eng;
+    std::string spec;
+    std::string err;
+};
+
+namespace {
+
+constexpr int kWindow = 480000;
+
+void set_err(char* buf, size_t len, const std::string& msg) {
+    if (buf && len) {
+        strncpy(buf, msg.c_str(), len - 1);
+        buf[len - 1] = 0;
+    }
+}
+
+spt_status fail(spt_ctx* c, spt_status s, const std::string& msg) {
+    if (c) c->err = msg;
+    return s;
+}
+
+spt_status classify(const std::exception& e) {
+    if (dynamic_cast<const spt::HipError*>(&e)) return SPT_ERR_DEVICE;
+    if (dynamic_cast<const std::bad_alloc*>(&e)) return SPT_ERR_OOM;
+    const std::string m = e.what();
+    if (m.find("out of device memory") != std::string::npos) return SPT_ERR_OOM;
+    return SPT_ERR_INVALID_ARG;
+}
+
+// whisper_full's prompt_init: [sot] (+ [lang, task] for multilingual) + [notimestamps]
+spt_status build_request(spt_ctx* c, const spt_infer_params* p, spt::DecodeRequest* rq) {
+    spt_infer_params d;
+    spt_default_infer_params(&d);
+    if (!p) p = &d;
+    const spt::ModelDims& dm = c->eng->dims();
+    const spt::Specials sp = spt::specials_for(dm.n_vocab);
+    if (p->beam_size > 1) return fail(c, SPT_ERR_UNSUPPORTED, "beam search is not implemented (greedy only)");
+    if (p->temperature != 0.0f) return fail(c, SPT_ERR_UNSUPPORTED, "only temperature 0 (greedy) is implemented");
+    if (p->initial_prompt && p->initial_prompt[0])
+        return fail(c, SPT_ERR_UNSUPPORTED, "initial_prompt needs a tokenizer vocabulary (ggml model loading not implemented)");
+    rq->prompt.clear();
+    rq->prompt.push_back(sp.sot);
+    if (sp.n_langs > 0) {
+        if (!p->language) return fail(c, SPT_ERR_UNSUPPORTED, "language auto-detection is not implemented; pass a language");
+        const int lid = spt::lang_id(p->language);
+        if (lid < 0 || lid >= sp.n_langs) return fail(c, SPT_ERR_INVALID_ARG, std::string("unknown language '") + p->language + "'");
+        rq->prompt.push_back(sp.sot + 1 + lid);
+        rq->prompt.push_back(p->translate ? sp.translate : sp.transcribe);
+    }
+    if (p->flags & SPT_NO_TIMESTAMPS) rq->prompt.push_back(sp.not_);
+    else return fail(c, SPT_ERR_UNSUPPORTED, "timestamp decoding is not implemented (set SPT_NO_TIMESTAMPS)");
+    int n = p->max_new_tokens > 0 ? p->max_new_tokens : 220;
+    if ((int)rq->prompt.size() + n > dm.n_text_ctx + 1) n = dm.n_text_ctx + 1 - (int)rq->prompt.size();
+    rq->n_steps = n;
+    rq->flags = p->flags;
+    rq->forced = p->forced_tokens;
+    rq->n_forced = p->forced_tokens ? p->n_forced : 0;
+    if (rq->n_forced < 0 || rq->n_forced > dm.n_text_ctx) return fail(c, SPT_ERR_INVALID_ARG, "n_forced out of range");
+    return SPT_OK;
+}
+
+spt_result* make_result(const int* tok, const float* t1, const float* t2, int n_steps, int n_windows, int eot,
+                        std::vector<int>* acc_tok, std::vector<float>* acc1, std::vector<float>* acc2,
+                        std::string* text) {
+    (void)tok; (void)t1; (void)t2; (void)n_steps; (void)eot;
+    spt_result* r = (spt_result*)calloc(1, sizeof(spt_result));
+    if (!r) return nullptr;
+    const size_t n = acc_tok->size();
+    r->n_tokens = (int32_t)n;
+    r->n_windows = n_windows;
+    r->tokens = (int32_t*)malloc(sizeof(int32_t) * (n ? n : 1));
+    r->top1 = (float*)malloc(sizeof(float) * (n ? n : 1));
+    r->top2 = (float*)malloc(sizeof(float) * (n ? n : 1));
+    r->text = (char*)malloc(text->size() + 1);
+    if (!r->tokens || !r->top1 || !r->top2 || !r->text) {
+        spt_result_free(r);
+        return nullptr;
+    }
+    for (size_t i = 0; i < n; ++i) {
+        r->tokens[i] = (*acc_tok)[i];
+        r->top1[i] = (*acc1)[i];
+        r->top2[i] = (*acc2)[i];
+    }
+    memcpy(r->text, text->c_str(), text->size() + 1);
+    return r;
+}
+
+// shared driver: windows (device or host) -> per-utterance results
+struct Window { int utt; const float* host; const float* dev; int n; };
+
+spt_status run_windows(spt_ctx* c, std::vector<Window>& win, size_t n_utt, const spt_infer_params* p,
+                       spt_result** out) {
+    spt::DecodeRequest rq;
+    spt_status s = build_request(c, p, &rq);
+    if (s != SPT_OK) return s;
+    Engine& e = *c->eng;
+    const int eot = spt::specials_for(e.dims().n_vocab).eot;
+    std::vector<std::vector<int>> tok(n_utt);
+    std::vector<std::vector<float>> t1(n_utt), t2(n_utt);
+    std::vector<std::string> text(n_utt);
+    std::vector<int> nwin(n_utt, 0);
+    const int cap = e.max_batch();
+    for (size_t g0 = 0; g0 < win.size(); g0 += cap) {
+        const int B = (int)std::min<size_t>(cap, win.size() - g0);
+        std::vector<int> ns(B);
+        std::vector<const float*> hp(B);
+        for (int b = 0; b < B; ++b) {
+            ns[b] = win[g0 + b].n;
+            hp[b] = win[g0 + b].host;
+        }
+        std::vector<int> otok((size_t)B * rq.n_steps);
+        std::vector<float> o1((size_t)B * rq.n_steps), o2((size_t)B * rq.n_steps);
+        if (win[g0].dev) {
+            // device windows are laid out contiguously by the caller (stride in Window.n is the slot)
+            e.transcribe_device(win[g0].dev, kWindow, ns.data(), B, rq, otok.data(), o1.data(), o2.data());
+        } else {
+            e.transcribe_host(hp.data(), ns.data(), B, rq, otok.data(), o1.data(), o2.data());
+        }
+        for (int b = 0; b < B; ++b) {
+            const int u = win[g0 + b].utt;
+            nwin[u]++;
+            for (int s2 = 0; s2 < rq.n_steps; ++s2) {
+                const int t = otok[(size_t)b * rq.n_steps + s2];
+                if (t < 0) break;
+                tok[u].push_back(t);
+                t1[u].push_back(o1[(size_t)b * rq.n_steps + s2]);
+                t2[u].push_back(o2[(size_t)b * rq.n_steps + s2]);
+                if (t < eot) text[u] += "[" + std::to_string(t) + "]";  // synthetic model: no vocabulary
+                if (t == eot && !(rq.flags & SPT_IGNORE_EOT)) break;
+            }
+        }
+    }
+    for (size_t u = 0; u < n_utt; ++u) {
+        out[u] = make_result(nullptr, nullptr, nullptr, 0, nwin[u], eot, &tok[u], &t1[u], &t2[u], &text[u]);
+        if (!out[u]) {
+            for (size_t v = 0; v < u; ++v) { spt_result_free(out[v]); out[v] = nullptr; }
+            return fail(c, SPT_ERR_OOM, "host allocation failed");
+        }
+    }
+    return SPT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* spt_version(void) { return "spittle_amd 0.1.0 (gfx950, ABI 1)"; }
+
+void spt_default_model_params(spt_model_params* p) {
+    if (!p) return;
+    memset(p, 0, sizeof(*p));
+    p->dtype = SPT_DTYPE_BF16;
+    p->device = 0;
+    p->max_batch = 8;
+    p->seed = 1234;
+}
+
+void spt_default_infer_params(spt_infer_params* p) {
+    if (!p) return;
+    memset(p, 0, sizeof(*p));
+    p->language = "en";
+    p->flags = SPT_SUPPRESS_BLANK | SPT_NO_TIMESTAMPS;
+    p->max_new_tokens = 220;
+    p->temperature = 0.0f;
+    p->beam_size = 1;
+}
+
+spt_status spt_ctx_create(const char* model_spec, const spt_model_params* params, spt_ctx** out, char* err,
+                          size_t errlen) {
+    if (!model_spec || !out) {
+        set_err(err, errlen, "null argument");
+        return SPT_ERR_INVALID_ARG;
+    }
+    *out = nullptr;
+    spt_model_params mp;
+    spt_default_model_params(&mp);
+    if (params) mp = *params;
+    if (mp.dtype != SPT_DTYPE_F32 && mp.dtype != SPT_DTYPE_BF16) {
+        set_err(err, errlen, "bad dtype");
+        return SPT_ERR_INVALID_ARG;
+    }
+    spt::ModelDims dm;
+    uint64_t seed = mp.seed;
+    std::string perr;
+    const std::string spec(model_spec);
+    if (!spt::parse_synthetic_spec(spec, &dm, &seed, &perr)) {
+        FILE* f = fopen(model_spec, "rb");
+        if (!f) {
+            set_err(err, errlen, "model file not found: " + spec);
+            return SPT_ERR_LOAD;
+        }
+        fclose(f);
+        set_err(err, errlen, "ggml model loading is not implemented yet: " + spec);
+        return SPT_ERR_UNSUPPORTED;
+    }
+    if (!perr.empty()) {
+        set_err(err, errlen, perr);
+        return SPT_ERR_LOAD;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        set_err(err, errlen, "no HIP device available");
+        return SPT_ERR_DEVICE;
+    }
+    if (mp.device < 0 || mp.device >= ndev) {
+        set_err(err, errlen, "device ordinal out of range");
+        return SPT_ERR_INVALID_ARG;
+    }
+    spt_ctx* c = new (std::nothrow) spt_ctx();
+    if (!c) return SPT_ERR_OOM;
+    try {
+        c->eng.reset(new Engine(dm, mp.dtype == SPT_DTYPE_BF16 ? spt::DT_BF16 : spt::DT_F32, mp.device,
+                                mp.max_batch, seed));
+    } catch (const std::exception& e) {
+        set_err(err, errlen, e.what());
+        const spt_status s = classify(e);
+        delete c;
+        return s == SPT_ERR_INVALID_ARG ? SPT_ERR_LOAD : s;
+    }
+    c->spec = spec;
+    *out = c;
+    return SPT_OK;
+}
+
+void spt_ctx_destroy(spt_ctx* ctx) { delete ctx; }
+
+const char* spt_last_error(const spt_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+spt_status spt_ctx_info(const spt_ctx* ctx, spt_model_info* info) {
+    if (!ctx || !info) return SPT_ERR_INVALID_ARG;
+    const spt::ModelDims& d = ctx->eng->dims();
+    info->n_mels = d.n_mels; info->d = d.d; info->n_head = d.n_head; info->n_enc = d.n_enc; info->n_dec = d.n_dec;
+    info->n_vocab = d.n_vocab; info->n_audio_ctx = d.n_audio_ctx; info->n_text_ctx = d.n_text_ctx;
+    info->dtype = ctx->eng->dtype() == spt::DT_BF16 ? SPT_DTYPE_BF16 : SPT_DTYPE_F32;
+    info->max_batch = ctx->eng->max_batch();
+    info->weight_bytes = ctx->eng->weight_bytes();
+    info->workspace_bytes = ctx->eng->workspace_bytes();
+    return SPT_OK;
+}
+
+spt_status spt_transcribe_batch(spt_ctx* ctx, const float* const* pcm, const size_t* n_samples, size_t batch,
+                                const spt_infer_params* params, spt_result** out) {
+    if (!ctx || !out || (batch && (!pcm || !n_samples))) return fail(ctx, SPT_ERR_INVALID_ARG, "null argument");
+    std::vector<Window> win;
+    std::vector<size_t> empty;
+    for (size_t u = 0; u < batch; ++u) {
+        out[u] = nullptr;
+        if (n_samples[u] == 0) { empty.push_back(u); continue; }  // "" without an engine call
+        if (!pcm[u]) return fail(ctx, SPT_ERR_INVALID_ARG, "null pcm");
+        for (size_t o = 0; o < n_samples[u]; o += kWindow)
+            win.push_back(Window{(int)u, pcm[u] + o, nullptr, (int)std::min<size_t>(kWindow, n_samples[u] - o)});
+    }
+    try {
+        spt_status s = SPT_OK;
+        if (!win.empty()) {
+            // results for non-empty utterances
+            std::vector<spt_result*> tmp(batch, nullptr);
+            s = run_windows(ctx, win, batch, params, tmp.data());
+            if (s != SPT_OK) return s;
+            for (size_t u = 0; u < batch; ++u) out[u] = tmp[u];
+        }
+        for (size_t u : empty) {
+            if (out[u]) spt_result_free(out[u]);
+            std::vector<int> t; std::vector<float> a, b; std::string txt;
+            out[u] = make_result(nullptr, nullptr, nullptr, 0, 0, 0, &t, &a, &b, &txt);
+        }
+        return SPT_OK;
+    } catch (const std::exception& e) {
+        return fail(ctx, classify(e), e.what());
+    }
+}
+
+spt_status spt_transcribe(spt_ctx* ctx, const float* pcm16k, size_t n_samples, const spt_infer_params* params,
+                          spt_result** out) {
+    if (!ctx || !out) return fail(ctx, SPT_ERR_INVALID_ARG, "null argument");
+    if (n_samples && !pcm16k) return fail(ctx, SPT_ERR_INVALID_ARG, "null pcm");
+    const float* p = pcm16k;
+    return spt_transcribe_batch(ctx, &p, &n_samples, 1, params, out);
+}
+
+spt_status spt_transcribe_batch_device(spt_ctx* ctx, const float* pcm_dev, size_t stride, const size_t* n_samples,
+                                       size_t batch, const spt_infer_params* params, spt_result** out) {
+    if (!ctx || !out || !pcm_dev || !n_samples || batch == 0) return fail(ctx, SPT_ERR_INVALID_ARG, "null argument");
+    if (batch > (size_t)ctx->eng->max_batch()) return fail(ctx, SPT_ERR_INVALID_ARG, "batch exceeds max_batch");
+    if (stride < (size_t)kWindow) return fail(ctx, SPT_ERR_INVALID_ARG, "device stride must be >= 480000");
+    spt::DecodeRequest rq;
+    spt_status s = build_request(ctx, params, &rq);
+    if (s != SPT_OK) return s;
+    try {
+        std::vector<int> ns(batch);
+        for (size_t b = 0; b < batch; ++b) {
+            if (n_samples[b] > (size_t)kWindow) return fail(ctx, SPT_ERR_INVALID_ARG, "device windows hold <= 480000 samples");
+            ns[b] = (int)n_samples[b];
+        }
+        Engine& e = *ctx->eng;
+        const int B = (int)batch;
+        std::vector<int> otok((size_t)B * rq.n_steps);
+        std::vector<float> o1((size_t)B * rq.n_steps), o2((size_t)B * rq.n_steps);
+        e.transcribe_device(pcm_dev, (int64_t)stride, ns.data(), B, rq, otok.data(), o1.data(), o2.data());
+        const int eot = spt::specials_for(e.dims().n_vocab).eot;
+        for (int b = 0; b < B; ++b) {
+            std::vector<int> t; std::vector<float> a, c2; std::string txt;
+            for (int s2 = 0; s2 < rq.n_steps; ++s2) {
+                const int tk = otok[(size_t)b * rq.n_steps + s2];
+                if (tk < 0) break;
+                t.push_back(tk);
+                a.push_back(o1[(size_t)b * rq.n_steps + s2]);
+                c2.push_back(o2[(size_t)b * rq.n_steps + s2]);
+                if (tk < eot) txt += "[" + std::to_string(tk) + "]";
+                if (tk == eot && !(rq.flags & SPT_IGNORE_EOT)) break;
+            }
+            out[b] = make_result(nullptr, nullptr, nullptr, 0, 1, eot, &t, &a, &c2, &txt);
+        }
+        return SPT_OK;
+    } catch (const std::exception& e) {
+        return fail(ctx, classify(e), e.what());
+    }
+}
+
+void spt_result_free(spt_result* r) {
+    if (!r) return;
+    free(r->text);
+    free(r->tokens);
+    free(r->top1);
+    free(r->top2);
+    free(r);
+}
+
+spt_status spt_get_timings(const spt_ctx* ctx, spt_timings* t) {
+    if (!ctx || !t) return SPT_ERR_INVALID_ARG;
+    const spt::Timings& m = ctx->eng->timings();
+    t->mel_ms = m.mel_ms; t->encoder_ms = m.encoder_ms; t->cross_kv_ms = m.cross_kv_ms; t->decode_ms = m.decode_ms;
+    t->total_ms = m.total_ms; t->h2d_ms = m.h2d_ms; t->n_decode_passes = m.n_decode_passes; t->batch = m.batch;
+    return SPT_OK;
+}
+
+spt_status spt_debug_mel(spt_ctx* ctx, const float* pcm16k, size_t n_samples, float* out) {
+    if (!ctx || !out || (n_samples && !pcm16k)) return fail(ctx, SPT_ERR_INVALID_ARG, "null argument");
+    if (n_samples > (size_t)kWindow) return fail(ctx, SPT_ERR_INVALID_ARG, "window longer than 30 s");
+    try {
+        ctx->eng->debug_mel(pcm16k, (int)n_samples, out);
+        return SPT_OK;
+    } catch (const std::exception& e) {
+        return fail(ctx, classify(e), e.what());
+    }
+}
+
+spt_status spt_debug_encode(spt_ctx* ctx, const float* mel, float* out) {
+    if (!ctx || !mel || !out) return fail(ctx, SPT_ERR_INVALID_ARG, "null argument");
+    try {
+        ctx->eng->debug_encode(mel, out);
+        return SPT_OK;
+    } catch (const std::exception& e) {
+        return fail(ctx, classify(e), e.what());
+    }
+}
+
+spt_status spt_debug_weight_checksum(spt_ctx* ctx, int32_t tensor_id, double* out2) {
+    if (!ctx || !out2) return fail(ctx, SPT_ERR_INVALID_ARG, "null argument");
+    try {
+        if (!ctx->eng->debug_weight_checksum(tensor_id, out2)) return fail(ctx, SPT_ERR_INVALID_ARG, "unknown tensor id");
+        return SPT_OK;
+    } catch (const std::exception& e) {
+        return fail(ctx, classify(e), e.what());
+    }
+}
+
+}  // extern "C"

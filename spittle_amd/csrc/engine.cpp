@@ -1,0 +1,656 @@
+// engine.cpp -- device-resident Whisper engine: weights, static memory plan,
+// the mel -> encoder -> cross-KV -> greedy decode pipeline, hipGraph decode steps.
+//
+// Reference path replaced: WhisperEngine::transcribe_samples -> whisper_full
+// (/root/reference/src-tauri/src/managers/transcription.rs:494-503), i.e.
+// whisper.cpp's log_mel_spectrogram, whisper_encode_internal (conv stem +
+// encoder + cross K/V) and the whisper_decode_internal / whisper_process_logits
+// / whisper_sample_token loop, for the greedy, fixed-language, no-timestamp
+// protocol of BASELINE.md.
+#include "engine.h"
+
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <sstream>
+#include <stdexcept>
+
+#include "common.h"
+
+namespace spt {
+
+// ----------------------------------------------------------------------------- vocab
+Specials specials_for(int n_vocab) {
+    // whisper.cpp whisper_vocab defaults, shifted for multilingual vocabularies in
+    // whisper_model_load (language count = n_vocab - 51765 - multilingual)
+    Specials s{50256, 50257, 50357, 50358, 50359, 50360, 50361, 50362, 50363, 0};
+    const bool multi = n_vocab >= 51865;
+    const int n_langs = n_vocab - 51765 - (multi ? 1 : 0);
+    if (multi) {
+        s.eot++;
+        s.sot++;
+        const int dt = n_langs - 98;
+        s.translate += dt; s.transcribe += dt; s.solm += dt; s.prev += dt; s.nosp += dt; s.not_ += dt; s.beg += dt;
+        s.n_langs = n_langs;
+    }
+    return s;
+}
+
+int lang_id(const std::string& code) {
+    static const char* langs[] = {
+        "en", "zh", "de", "es", "ru", "ko", "fr", "ja", "pt", "tr", "pl", "ca", "nl", "ar", "sv", "it", "id",
+        "hi", "fi", "vi", "he", "uk", "el", "ms", "cs", "ro", "da", "hu", "ta", "no", "th", "ur", "hr", "bg",
+        "lt", "la", "mi", "ml", "cy", "sk", "te", "fa", "lv", "bn", "sr", "az", "sl", "kn", "et", "mk", "br",
+        "eu", "is", "hy", "ne", "mn", "bs", "kk", "sq", "sw", "gl", "mr", "pa", "si", "km", "sn", "yo", "so",
+        "af", "oc", "ka", "be", "tg", "sd", "gu", "am", "yi", "lo", "uz", "fo", "ht", "ps", "tk", "nn", "mt",
+        "sa", "lb", "my", "bo", "tl", "mg", "as", "tt", "haw", "ln", "ha", "ba", "jw", "su", "yue"};
+    for (int i = 0; i < (int)(sizeof(langs) / sizeof(langs[0])); ++i)
+        if (code == langs[i]) return i;
+    return -1;
+}
+
+bool parse_synthetic_spec(const std::string& spec, ModelDims* dm, uint64_t* seed, std::string* err) {
+    const std::string pfx = "synthetic:";
+    if (spec.compare(0, pfx.size(), pfx) != 0) return false;
+    std::vector<std::string> parts;
+    std::stringstream ss(spec.substr(pfx.size()));
+    std::string tok;
+    while (std::getline(ss, tok, ':')) parts.push_back(tok);
+    if (parts.empty()) { *err = "empty synthetic spec"; return true; }
+    struct Cfg { const char* name; int n_mels, d, h, ne, nd, V; };
+    static const Cfg cfgs[] = {
+        {"tiny.en", 80, 384, 6, 4, 4, 51864},     {"tiny", 80, 384, 6, 4, 4, 51865},
+        {"base.en", 80, 512, 8, 6, 6, 51864},     {"base", 80, 512, 8, 6, 6, 51865},
+        {"small.en", 80, 768, 12, 12, 12, 51864}, {"small", 80, 768, 12, 12, 12, 51865},
+        {"medium.en", 80, 1024, 16, 24, 24, 51864}, {"medium", 80, 1024, 16, 24, 24, 51865},
+        {"large-v3", 128, 1280, 20, 32, 32, 51866}, {"large-v3-turbo", 128, 1280, 20, 32, 4, 51866},
+    };
+    bool found = false;
+    for (const Cfg& c : cfgs)
+        if (parts[0] == c.name) {
+            dm->name = c.name;
+            dm->n_mels = c.n_mels; dm->d = c.d; dm->n_head = c.h; dm->n_enc = c.ne; dm->n_dec = c.nd;
+            dm->n_vocab = c.V;
+            found = true;
+        }
+    if (!found) { *err = "unknown synthetic model '" + parts[0] + "'"; return true; }
+    for (size_t i = 1; i < parts.size(); ++i) {
+        const std::string& p = parts[i];
+        const size_t eq = p.find('=');
+        if (eq == std::string::npos) { *err = "bad option '" + p + "'"; return true; }
+        const std::string k = p.substr(0, eq), v = p.substr(eq + 1);
+        char* end = nullptr;
+        const unsigned long long x = strtoull(v.c_str(), &end, 10);
+        if (!end || *end) { *err = "bad value in '" + p + "'"; return true; }
+        if (k == "enc") dm->n_enc = (int)x;
+        else if (k == "dec") dm->n_dec = (int)x;
+        else if (k == "seed") *seed = (uint64_t)x;
+        else { *err = "unknown option '" + k + "'"; return true; }
+    }
+    if (dm->n_enc < 0 || dm->n_dec < 1 || dm->n_enc > 64 || dm->n_dec > 64) *err = "layer count out of range";
+    return true;
+}
+
+// ----------------------------------------------------------------------------- helpers
+namespace {
+int fanin_exp(int K) { return (int)floor(log2(sqrt(3.0 / (double)K)) + 0.5); }
+
+struct Carver {
+    char* base;
+    int64_t off = 0;
+    void* take(int64_t bytes) {
+        off = (off + 255) & ~(int64_t)255;
+        void* p = base ? base + off : nullptr;
+        off += bytes;
+        return p;
+    }
+};
+}  // namespace
+
+void Engine::select() const { HIP_CHECK(hipSetDevice(dev_)); }
+
+Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64_t seed)
+    : dm_(dm), dt_(dtype), dev_(device), max_batch_(max_batch), seed_(seed) {
+    if (dm_.d % 128 || dm_.d / 64 != dm_.n_head) throw std::runtime_error("unsupported model width");
+    if (max_batch_ < 1 || max_batch_ > 64) throw std::runtime_error("max_batch must be in 1..64");
+    esz_ = dt_ == DT_BF16 ? 2 : 4;
+    cp_ = ((dm_.n_mels + 63) / 64) * 64;
+    if ((3 * cp_ * esz_) % 128) cp_ = ((dm_.n_mels + 127) / 128) * 128;
+    select();
+    HIP_CHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    ev_.resize(8);
+    for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
+    alloc_weights();
+    generate_weights();
+    upload_tables();
+    alloc_workspace();
+    HIP_CHECK(hipStreamSynchronize(st_));
+}
+
+Engine::~Engine() {
+    (void)hipSetDevice(dev_);
+    if (st_) (void)hipStreamSynchronize(st_);
+    for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
+    if (warena_) (void)hipFree(warena_);
+    if (aarena_) (void)hipFree(aarena_);
+    for (void* p : {(void*)hann_, (void*)sinv_, (void*)cosv_, (void*)filt_, (void*)grp_})
+        if (p) (void)hipFree(p);
+    for (auto& e : ev_) (void)hipEventDestroy(e);
+    if (st_) (void)hipStreamDestroy(st_);
+}
+
+// ----------------------------------------------------------------------------- weights
+void Engine::alloc_weights() {
+    const int64_t d = dm_.d, dd = d * d, V = dm_.n_vocab, L = dm_.n_dec;
+    enc_.resize(dm_.n_enc);
+    dec_.resize(dm_.n_dec);
+    for (int pass = 0; pass < 2; ++pass) {
+        Carver c{pass ? warena_ : nullptr};
+        auto W = [&](int64_t n) { return c.take(n * esz_); };
+        auto F = [&](int64_t n) { return (float*)c.take(n * 4); };
+        conv1_w_ = W(d * 3 * cp_); conv1_b_ = F(d);
+        conv2_w_ = W(dd * 3); conv2_b_ = F(d);
+        enc_pos_ = F((int64_t)dm_.n_audio_ctx * d);
+        lnp_w_ = F(d); lnp_b_ = F(d);
+        for (auto& e : enc_) {
+            e.ln1_w = F(d); e.ln1_b = F(d); e.qkv_w = W(3 * dd); e.qkv_b = F(3 * d); e.o_w = W(dd); e.o_b = F(d);
+            e.ln2_w = F(d); e.ln2_b = F(d); e.fc1_w = W(4 * dd); e.fc1_b = F(4 * d); e.fc2_w = W(4 * dd); e.fc2_b = F(d);
+        }
+        ckv_w_ = W(L * 2 * dd); ckv_b_ = F(L * 2 * d);
+        tok_emb_ = W(V * d); dec_pos_ = F((int64_t)dm_.n_text_ctx * d); lnf_w_ = F(d); lnf_b_ = F(d);
+        for (auto& e : dec_) {
+            e.ln1_w = F(d); e.ln1_b = F(d); e.qkv_w = W(3 * dd); e.qkv_b = F(3 * d); e.so_w = W(dd); e.so_b = F(d);
+            e.ln2_w = F(d); e.ln2_b = F(d); e.cq_w = W(dd); e.cq_b = F(d); e.co_w = W(dd); e.co_b = F(d);
+            e.ln3_w = F(d); e.ln3_b = F(d); e.fc1_w = W(4 * dd); e.fc1_b = F(4 * d); e.fc2_w = W(4 * dd); e.fc2_b = F(d);
+        }
+        if (!pass) {
+            wbytes_ = c.off;
+            if (hipMalloc(&warena_, wbytes_) != hipSuccess) {
+                warena_ = nullptr;
+                throw std::runtime_error("out of device memory for weights (" + std::to_string(wbytes_) + " B)");
+            }
+        }
+    }
+}
+
+void Engine::generate_weights() {
+    const int64_t d = dm_.d, dd = d * d;
+    auto reg = [&](int tid, void* p, int64_t n, int dt) { tref_[tid] = TRef{p, n, dt}; };
+    auto genw = [&](void* p, int64_t n, int tid, int kind, int e) {  // dtype storage
+        gen_weights(dt_, p, n, seed_, (uint32_t)tid, kind, e, st_);
+        reg(tid, p, n, dt_);
+    };
+    auto genf = [&](float* p, int64_t n, int tid, int kind, int e) {  // f32 storage
+        gen_weights(DT_F32, p, n, seed_, (uint32_t)tid, kind, e, st_);
+        reg(tid, p, n, DT_F32);
+    };
+    auto at = [&](void* p, int64_t elems) { return (void*)((char*)p + elems * esz_); };
+    gen_conv_weights(dt_, conv1_w_, (int)d, dm_.n_mels, cp_, seed_, 1, fanin_exp(3 * dm_.n_mels), st_);
+    reg(1, conv1_w_, d * 3 * cp_, dt_);
+    genf(conv1_b_, d, 2, WK_BIAS, -5);
+    gen_conv_weights(dt_, conv2_w_, (int)d, (int)d, (int)d, seed_, 3, fanin_exp(3 * (int)d), st_);
+    reg(3, conv2_w_, dd * 3, dt_);
+    genf(conv2_b_, d, 4, WK_BIAS, -5);
+    genf(lnp_w_, d, 5, WK_LNW, -3);
+    genf(lnp_b_, d, 6, WK_LNB, -4);
+    {  // whisper sinusoids(1500, d), double precision like the oracle
+        std::vector<float> pe((size_t)dm_.n_audio_ctx * d);
+        const int half = (int)d / 2;
+        const double inc = log(10000.0) / (double)(half - 1);
+        for (int t = 0; t < dm_.n_audio_ctx; ++t)
+            for (int i = 0; i < half; ++i) {
+                const double s = (double)t * exp(-inc * (double)i);
+                pe[(size_t)t * d + i] = (float)sin(s);
+                pe[(size_t)t * d + half + i] = (float)cos(s);
+            }
+        HIP_CHECK(hipMemcpy(enc_pos_, pe.data(), pe.size() * 4, hipMemcpyHostToDevice));
+        reg(7, enc_pos_, (int64_t)pe.size(), DT_F32);
+    }
+    for (int l = 0; l < dm_.n_enc; ++l) {
+        EncL& e = enc_[l];
+        const int b = 100 + 32 * l;
+        genf(e.ln1_w, d, b + 0, WK_LNW, -3);
+        genf(e.ln1_b, d, b + 1, WK_LNB, -4);
+        genw(at(e.qkv_w, 0), dd, b + 2, WK_MAT, fanin_exp((int)d));
+        genf(e.qkv_b, d, b + 3, WK_BIAS, -5);
+        genw(at(e.qkv_w, dd), dd, b + 4, WK_MAT, fanin_exp((int)d));
+        fill_f32(e.qkv_b + d, d, 0.0f, st_);
+        genw(at(e.qkv_w, 2 * dd), dd, b + 5, WK_MAT, fanin_exp((int)d));
+        genf(e.qkv_b + 2 * d, d, b + 6, WK_BIAS, -5);
+        genw(e.o_w, dd, b + 7, WK_MAT, fanin_exp((int)d));
+        genf(e.o_b, d, b + 8, WK_BIAS, -5);
+        genf(e.ln2_w, d, b + 9, WK_LNW, -3);
+        genf(e.ln2_b, d, b + 10, WK_LNB, -4);
+        genw(e.fc1_w, 4 * dd, b + 11, WK_MAT, fanin_exp((int)d));
+        genf(e.fc1_b, 4 * d, b + 12, WK_BIAS, -5);
+        genw(e.fc2_w, 4 * dd, b + 13, WK_MAT, fanin_exp(4 * (int)d));
+        genf(e.fc2_b, d, b + 14, WK_BIAS, -5);
+    }
+    genw(tok_emb_, (int64_t)dm_.n_vocab * d, 10, WK_TOK, -2);
+    genf(dec_pos_, (int64_t)dm_.n_text_ctx * d, 11, WK_DPOS, 0);
+    genf(lnf_w_, d, 12, WK_LNW, -3);
+    genf(lnf_b_, d, 13, WK_LNB, -4);
+    for (int l = 0; l < dm_.n_dec; ++l) {
+        DecL& e = dec_[l];
+        const int b = 5000 + 32 * l;
+        genf(e.ln1_w, d, b + 0, WK_LNW, -3);
+        genf(e.ln1_b, d, b + 1, WK_LNB, -4);
+        genw(at(e.qkv_w, 0), dd, b + 2, WK_MAT, fanin_exp((int)d));
+        genf(e.qkv_b, d, b + 3, WK_BIAS, -5);
+        genw(at(e.qkv_w, dd), dd, b + 4, WK_MAT, fanin_exp((int)d));
+        fill_f32(e.qkv_b + d, d, 0.0f, st_);
+        genw(at(e.qkv_w, 2 * dd), dd, b + 5, WK_MAT, fanin_exp((int)d));
+        genf(e.qkv_b + 2 * d, d, b + 6, WK_BIAS, -5);
+        genw(e.so_w, dd, b + 7, WK_MAT, fanin_exp((int)d));
+        genf(e.so_b, d, b + 8, WK_BIAS, -5);
+        genf(e.ln2_w, d, b + 9, WK_LNW, -3);
+        genf(e.ln2_b, d, b + 10, WK_LNB, -4);
+        genw(e.cq_w, dd, b + 11, WK_MAT, fanin_exp((int)d));
+        genf(e.cq_b, d, b + 12, WK_BIAS, -5);
+        genw(at(ckv_w_, (2 * l) * dd), dd, b + 13, WK_MAT, fanin_exp((int)d));
+        fill_f32(ckv_b_ + (2 * l) * d, d, 0.0f, st_);
+        genw(at(ckv_w_, (2 * l + 1) * dd), dd, b + 14, WK_MAT, fanin_exp((int)d));
+        genf(ckv_b_ + (2 * l + 1) * d, d, b + 15, WK_BIAS, -5);
+        genw(e.co_w, dd, b + 16, WK_MAT, fanin_exp((int)d));
+        genf(e.co_b, d, b + 17, WK_BIAS, -5);
+        genf(e.ln3_w, d, b + 18, WK_LNW, -3);
+        genf(e.ln3_b, d, b + 19, WK_LNB, -4);
+        genw(e.fc1_w, 4 * dd, b + 20, WK_MAT, fanin_exp((int)d));
+        genf(e.fc1_b, 4 * d, b + 21, WK_BIAS, -5);
+        genw(e.fc2_w, 4 * dd, b + 22, WK_MAT, fanin_exp(4 * (int)d));
+        genf(e.fc2_b, d, b + 23, WK_BIAS, -5);
+    }
+    HIP_CHECK(hipGetLastError());
+}
+
+void Engine::upload_tables() {
+    // whisper_global_cache: sin/cos tables and periodic Hann from float(theta)
+    std::vector<float> hann(400), sv(400), cv(400);
+    for (int i = 0; i < 400; ++i) {
+        const double theta = (2 * M_PI * i) / 400;
+        sv[i] = sinf((float)theta);
+        cv[i] = cosf((float)theta);
+        hann[i] = (float)(0.5 * (1.0 - cosf((float)((2.0 * M_PI * i) / 400))));
+    }
+    // librosa / slaney mel filterbank (the filters whisper.cpp reads from the model file)
+    const int nm = dm_.n_mels;
+    auto hz2mel = [](double f) {
+        const double lg = 27.0 / log(6.4);
+        return f >= 1000.0 ? 15.0 + log(f / 1000.0) * lg : 3.0 * f / 200.0;
+    };
+    auto mel2hz = [](double m) {
+        const double lg = log(6.4) / 27.0;
+        return m >= 15.0 ? 1000.0 * exp(lg * (m - 15.0)) : 200.0 * m / 3.0;
+    };
+    std::vector<double> ff(nm + 2);
+    const double mmin = hz2mel(0.0), mmax = hz2mel(8000.0);
+    for (int i = 0; i < nm + 2; ++i) {
+        double mm = mmin + (mmax - mmin) * i / (double)(nm + 1);
+        if (i == nm + 1) mm = mmax;
+        ff[i] = mel2hz(mm);
+    }
+    std::vector<float> filt((size_t)nm * 201);
+    std::vector<int> grp(2 * nm);
+    for (int j = 0; j < nm; ++j) {
+        const double en = 2.0 / (ff[j + 2] - ff[j]);
+        int lo = -1, hi = -1;
+        for (int k = 0; k < 201; ++k) {
+            const double fk = 8000.0 * k / 200.0;
+            const double down = -(ff[j] - fk) / (ff[j + 1] - ff[j]);
+            const double up = (ff[j + 2] - fk) / (ff[j + 2] - ff[j + 1]);
+            double v = std::min(down, up);
+            if (v < 0) v = 0;
+            const float fv = (float)(v * en);
+            filt[(size_t)j * 201 + k] = fv;
+            if (fv != 0.0f) {
+                if (lo < 0) lo = k;
+                hi = k;
+            }
+        }
+        if (lo < 0) { grp[2 * j] = 0; grp[2 * j + 1] = 0; }
+        else {
+            grp[2 * j] = lo < 200 ? lo / 4 : 50;
+            grp[2 * j + 1] = (hi < 200 ? hi / 4 : 50) + 1;
+        }
+    }
+    HIP_CHECK(hipMalloc(&hann_, 400 * 4));
+    HIP_CHECK(hipMalloc(&sinv_, 400 * 4));
+    HIP_CHECK(hipMalloc(&cosv_, 400 * 4));
+    HIP_CHECK(hipMalloc(&filt_, filt.size() * 4));
+    HIP_CHECK(hipMalloc(&grp_, grp.size() * 4));
+    HIP_CHECK(hipMemcpy(hann_, hann.data(), 1600, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(sinv_, sv.data(), 1600, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(cosv_, cv.data(), 1600, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(filt_, filt.data(), filt.size() * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(grp_, grp.data(), grp.size() * 4, hipMemcpyHostToDevice));
+}
+
+// ----------------------------------------------------------------------------- workspace
+void Engine::alloc_workspace() {
+    const int64_t B = max_batch_, d = dm_.d, T = dm_.n_audio_ctx, L = dm_.n_dec, ctx = dm_.n_text_ctx;
+    const int64_t H = dm_.n_head, V = dm_.n_vocab, R = B * 4;
+    for (int pass = 0; pass < 2; ++pass) {
+        Carver c{pass ? aarena_ : nullptr};
+        auto A = [&](int64_t n) { return c.take(n * esz_); };
+        pcm_ = (float*)c.take(B * 480000 * 4);
+        nsamp_ = (int*)c.take(B * 4);
+        mel_raw_ = (float*)c.take(B * MEL_ROWS * dm_.n_mels * 4);
+        mel_max_ = (unsigned*)c.take(B * 4);
+        mel_in_ = A(B * MEL_ROWS * cp_);
+        y1p_ = A(B * MEL_ROWS * d);
+        x_ = (float*)c.take(B * T * d * 4);
+        xn_ = A(B * T * d);
+        qkv_ = A(B * T * 3 * d);
+        ao_ = A(B * T * d);
+        ff_ = A(B * T * 4 * d);
+        enc_out_ = A(B * T * d);
+        ckv_ = A(L * 2 * B * T * d);
+        skv_ = A(L * 2 * B * ctx * d);
+        dx_ = (float*)c.take(R * d * 4);
+        dq_ = A(R * d);
+        dao_ = A(R * d);
+        dff_ = A(R * 4 * d);
+        part_ = (float*)c.take(R * H * n_split_ * 66 * 4);
+        logits_ = (float*)c.take(B * V * 4);
+        tok_in_ = (int*)c.take(R * 4);
+        out_tok_ = (int*)c.take(B * ctx * 4);
+        out_t1_ = (float*)c.take(B * ctx * 4);
+        out_t2_ = (float*)c.take(B * ctx * 4);
+        done_ = (int*)c.take(B * 4);
+        forced_ = (int*)c.take(B * ctx * 4);
+        suppress_ = (uint32_t*)c.take((V / 32 + 1) * 4);
+        ds_ = (DecState*)c.take(sizeof(DecState));
+        scratch_ = (double*)c.take(64);
+        if (!pass) {
+            abytes_ = c.off;
+            if (hipMalloc(&aarena_, abytes_) != hipSuccess) {
+                aarena_ = nullptr;
+                throw std::runtime_error("out of device memory for workspace (" + std::to_string(abytes_) + " B)");
+            }
+        }
+    }
+    // zero everything once: padding rows of the conv inputs stay zero forever
+    HIP_CHECK(hipMemsetAsync(aarena_, 0, abytes_, st_));
+}
+
+// ----------------------------------------------------------------------------- pipeline
+void Engine::run_mel(const float* pcm_dev, int64_t stride, int B, float* dbg) {
+    MelTables t{hann_, sinv_, cosv_, filt_, grp_};
+    mel_frames(pcm_dev, stride, nsamp_, B, dm_.n_mels, t, mel_raw_, mel_max_, st_);
+    mel_norm(dt_, mel_raw_, mel_max_, nsamp_, B, dm_.n_mels, cp_, mel_in_, dbg, st_);
+}
+
+void Engine::run_encoder(int B) {
+    const int d = dm_.d, T = dm_.n_audio_ctx, H = dm_.n_head, M = B * T;
+    GemmArgs g{};
+    // conv1 (k3, s1, p1) + GELU -> y1p rows 1..3000
+    g.A = mel_in_; g.lda = cp_; g.sA = (int64_t)MEL_ROWS * cp_;
+    g.W = conv1_w_; g.ldw = 3 * cp_;
+    g.M = 2 * T; g.N = d; g.K = 3 * cp_;
+    g.bias = conv1_b_;
+    g.C = (char*)y1p_ + (size_t)d * esz_; g.ldc = d; g.sC = (int64_t)MEL_ROWS * d;
+    gemm_nt(dt_, EPI_BIAS_GELU, g, B, st_);
+    // conv2 (k3, s2, p1) + GELU + positional embedding -> residual stream x (f32)
+    g = GemmArgs{};
+    g.A = y1p_; g.lda = 2 * d; g.sA = (int64_t)MEL_ROWS * d;
+    g.W = conv2_w_; g.ldw = 3 * d;
+    g.M = T; g.N = d; g.K = 3 * d;
+    g.bias = conv2_b_;
+    g.C = x_; g.ldc = d; g.sC = (int64_t)T * d;
+    g.pos = enc_pos_;
+    gemm_nt(dt_, EPI_BIAS_GELU_POS, g, B, st_);
+    for (int l = 0; l < dm_.n_enc; ++l) {
+        const EncL& e = enc_[l];
+        layernorm(dt_, x_, M, d, e.ln1_w, e.ln1_b, xn_, st_);
+        g = GemmArgs{};
+        g.A = xn_; g.lda = d; g.W = e.qkv_w; g.ldw = d; g.M = M; g.N = 3 * d; g.K = d; g.bias = e.qkv_b;
+        g.C = qkv_; g.ldc = 3 * d;
+        gemm_nt(dt_, EPI_BIAS, g, 1, st_);
+        enc_attention(dt_, qkv_, B, T, H, ao_, st_);
+        g = GemmArgs{};
+        g.A = ao_; g.lda = d; g.W = e.o_w; g.ldw = d; g.M = M; g.N = d; g.K = d; g.bias = e.o_b;
+        g.C = x_; g.ldc = d;
+        gemm_nt(dt_, EPI_BIAS_RESID, g, 1, st_);
+        layernorm(dt_, x_, M, d, e.ln2_w, e.ln2_b, xn_, st_);
+        g = GemmArgs{};
+        g.A = xn_; g.lda = d; g.W = e.fc1_w; g.ldw = d; g.M = M; g.N = 4 * d; g.K = d; g.bias = e.fc1_b;
+        g.C = ff_; g.ldc = 4 * d;
+        gemm_nt(dt_, EPI_BIAS_GELU, g, 1, st_);
+        g = GemmArgs{};
+        g.A = ff_; g.lda = 4 * d; g.W = e.fc2_w; g.ldw = 4 * d; g.M = M; g.N = d; g.K = 4 * d; g.bias = e.fc2_b;
+        g.C = x_; g.ldc = d;
+        gemm_nt(dt_, EPI_BIAS_RESID, g, 1, st_);
+    }
+    layernorm(dt_, x_, M, d, lnp_w_, lnp_b_, enc_out_, st_);
+}
+
+void Engine::run_cross_kv(int B) {
+    const int d = dm_.d, T = dm_.n_audio_ctx;
+    GemmArgs g{};
+    g.A = enc_out_; g.lda = d; g.W = ckv_w_; g.ldw = d; g.M = B * T; g.N = dm_.n_dec * 2 * d; g.K = d;
+    g.bias = ckv_b_; g.C = ckv_; g.kv_B = B; g.kv_T = T; g.kv_H = dm_.n_head;
+    gemm_nt(dt_, EPI_KVSPLIT, g, 1, st_);
+}
+
+void Engine::enqueue_decoder_pass(int B, int Tq, const DecodeRequest& rq, int out_cap) {
+    const int d = dm_.d, H = dm_.n_head, ctx = dm_.n_text_ctx, T = dm_.n_audio_ctx, R = B * Tq;
+    const int64_t self_layer = (int64_t)2 * B * H * ctx * 64, cross_layer = (int64_t)2 * B * H * T * 64;
+    dec_embed(dt_, tok_in_, R, Tq, d, tok_emb_, dec_pos_, ds_, dx_, st_);
+    for (int l = 0; l < dm_.n_dec; ++l) {
+        const DecL& e = dec_[l];
+        void* skv_l = (char*)skv_ + self_layer * l * esz_;
+        const void* ckv_l = (const char*)ckv_ + cross_layer * l * esz_;
+        GemvArgs a{};
+        a.A = dx_; a.lda = d; a.ln_w = e.ln1_w; a.ln_b = e.ln1_b; a.R = R;
+        a.W = e.qkv_w; a.N = 3 * d; a.K = d; a.bias = e.qkv_b; a.C = dq_; a.ldc = d;
+        a.cache = skv_l; a.cache_B = B; a.cache_H = H; a.cache_ctx = ctx; a.Tq = Tq; a.st = ds_;
+        gemv(dt_, GV_QKV_CACHE, a, st_);
+        dec_self_attn(dt_, dq_, skv_l, B, H, ctx, Tq, ds_, dao_, st_);
+        a = GemvArgs{};
+        a.A = dao_; a.lda = d; a.R = R; a.W = e.so_w; a.N = d; a.K = d; a.bias = e.so_b; a.C = dx_; a.ldc = d;
+        gemv(dt_, GV_BIAS_RESID, a, st_);
+        a = GemvArgs{};
+        a.A = dx_; a.lda = d; a.ln_w = e.ln2_w; a.ln_b = e.ln2_b; a.R = R;
+        a.W = e.cq_w; a.N = d; a.K = d; a.bias = e.cq_b; a.C = dq_; a.ldc = d;
+        gemv(dt_, GV_BIAS, a, st_);
+        dec_cross_attn(dt_, dq_, ckv_l, B, H, T, Tq, n_split_, part_, dao_, st_);
+        a = GemvArgs{};
+        a.A = dao_; a.lda = d; a.R = R; a.W = e.co_w; a.N = d; a.K = d; a.bias = e.co_b; a.C = dx_; a.ldc = d;
+        gemv(dt_, GV_BIAS_RESID, a, st_);
+        a = GemvArgs{};
+        a.A = dx_; a.lda = d; a.ln_w = e.ln3_w; a.ln_b = e.ln3_b; a.R = R;
+        a.W = e.fc1_w; a.N = 4 * d; a.K = d; a.bias = e.fc1_b; a.C = dff_; a.ldc = 4 * d;
+        gemv(dt_, GV_BIAS_GELU, a, st_);
+        a = GemvArgs{};
+        a.A = dff_; a.lda = 4 * d; a.R = R; a.W = e.fc2_w; a.N = d; a.K = 4 * d; a.bias = e.fc2_b; a.C = dx_;
+        a.ldc = d;
+        gemv(dt_, GV_BIAS_RESID, a, st_);
+    }
+    GemvArgs a{};
+    a.A = dx_; a.lda = Tq * d; a.a_row0 = (Tq - 1) * d; a.ln_w = lnf_w_; a.ln_b = lnf_b_; a.R = B;
+    a.W = tok_emb_; a.N = dm_.n_vocab; a.K = d; a.C = logits_; a.ldc = dm_.n_vocab;
+    gemv(dt_, GV_LOGITS, a, st_);
+    const Specials sp = specials_for(dm_.n_vocab);
+    ArgmaxArgs m{};
+    m.logits = logits_; m.V = dm_.n_vocab; m.suppress = suppress_;
+    m.blank0 = (rq.flags & 1u) ? sp.eot : -1;
+    m.blank1 = (rq.flags & 1u) ? 220 : -1;
+    m.eot = sp.eot; m.ignore_eot = (rq.flags & 4u) ? 1 : 0;
+    m.forced = rq.n_forced > 0 ? forced_ : nullptr; m.forced_len = rq.n_forced;
+    m.next_tok = tok_in_; m.out_tok = out_tok_; m.out_top1 = out_t1_; m.out_top2 = out_t2_; m.out_cap = out_cap;
+    m.done = done_; m.ds = ds_;
+    dec_argmax(m, B, st_);
+    dec_advance(ds_, Tq, st_);
+}
+
+void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1, float* top2) {
+    const int Tq = (int)rq.prompt.size();
+    const int ctx = dm_.n_text_ctx;
+    if (Tq < 1 || Tq > 4) throw std::runtime_error("prompt must have 1..4 tokens");
+    if (B * Tq > 64) throw std::runtime_error("batch x prompt rows exceed 64");
+    if (rq.n_steps < 1 || Tq + rq.n_steps > ctx + 1) throw std::runtime_error("n_steps out of range");
+    if (rq.n_forced > ctx) throw std::runtime_error("too many forced tokens");
+    const int out_cap = rq.n_steps;
+    const Specials sp = specials_for(dm_.n_vocab);
+    // always-suppressed ids (whisper_process_logits, no-timestamp greedy subset)
+    const uint32_t sflags = rq.flags & 2u;
+    if (suppress_flags_ != sflags) {
+        const int V = dm_.n_vocab;
+        host_suppress_.assign(V / 32 + 1, 0u);
+        auto set = [&](int i) { if (i >= 0 && i < V) host_suppress_[i >> 5] |= 1u << (i & 31); };
+        set(sp.not_);
+        if (rq.flags & 2u)
+            for (int i = sp.beg; i < V; ++i) set(i);
+        set(sp.sot); set(sp.nosp); set(sp.solm); set(sp.translate); set(sp.transcribe); set(sp.prev);
+        for (int i = 0; i < sp.n_langs; ++i) set(sp.sot + 1 + i);
+        HIP_CHECK(hipMemcpyAsync(suppress_, host_suppress_.data(), host_suppress_.size() * 4, hipMemcpyHostToDevice, st_));
+        HIP_CHECK(hipStreamSynchronize(st_));
+        suppress_flags_ = sflags;
+    }
+    std::vector<int> tin((size_t)B * Tq);
+    for (int b = 0; b < B; ++b)
+        for (int t = 0; t < Tq; ++t) tin[(size_t)b * Tq + t] = rq.prompt[t];
+    HIP_CHECK(hipMemcpyAsync(tok_in_, tin.data(), tin.size() * 4, hipMemcpyHostToDevice, st_));
+    if (rq.n_forced > 0)
+        HIP_CHECK(hipMemcpyAsync(forced_, rq.forced, (size_t)B * rq.n_forced * 4, hipMemcpyHostToDevice, st_));
+    HIP_CHECK(hipMemsetAsync(done_, 0, B * 4, st_));
+    HIP_CHECK(hipMemsetAsync(out_tok_, 0xFF, (size_t)B * out_cap * 4, st_));
+    fill_f32(out_t1_, (int64_t)B * out_cap, -INFINITY, st_);
+    fill_f32(out_t2_, (int64_t)B * out_cap, -INFINITY, st_);
+    dec_reset(ds_, st_);
+    enqueue_decoder_pass(B, Tq, rq, out_cap);  // prompt pass produces token 0
+    int passes = 1;
+    if (rq.n_steps > 1) {
+        const GraphKey key{B, out_cap, rq.n_forced, rq.flags};
+        auto it = graphs_.find(key);
+        if (it == graphs_.end()) {
+            hipGraph_t graph;
+            HIP_CHECK(hipStreamBeginCapture(st_, hipStreamCaptureModeThreadLocal));
+            enqueue_decoder_pass(B, 1, rq, out_cap);
+            HIP_CHECK(hipStreamEndCapture(st_, &graph));
+            hipGraphExec_t exec;
+            HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+            HIP_CHECK(hipGraphDestroy(graph));
+            it = graphs_.emplace(key, exec).first;
+        }
+        const bool early_exit = !(rq.flags & 4u);
+        std::vector<int> hdone(B);
+        for (int s = 1; s < rq.n_steps; ++s) {
+            HIP_CHECK(hipGraphLaunch(it->second, st_));
+            ++passes;
+            if (early_exit && (s % 16) == 0) {
+                HIP_CHECK(hipMemcpyAsync(hdone.data(), done_, B * 4, hipMemcpyDeviceToHost, st_));
+                HIP_CHECK(hipStreamSynchronize(st_));
+                if (std::all_of(hdone.begin(), hdone.end(), [](int v) { return v != 0; })) break;
+            }
+        }
+    }
+    tm_.n_decode_passes = passes;
+    HIP_CHECK(hipMemcpyAsync(tokens, out_tok_, (size_t)B * out_cap * 4, hipMemcpyDeviceToHost, st_));
+    if (top1) HIP_CHECK(hipMemcpyAsync(top1, out_t1_, (size_t)B * out_cap * 4, hipMemcpyDeviceToHost, st_));
+    if (top2) HIP_CHECK(hipMemcpyAsync(top2, out_t2_, (size_t)B * out_cap * 4, hipMemcpyDeviceToHost, st_));
+}
+
+void Engine::transcribe_device(const float* pcm_dev, int64_t stride, const int* n_samples, int B,
+                               const DecodeRequest& rq, int* tokens, float* top1, float* top2) {
+    select();
+    if (B < 1 || B > max_batch_) throw std::runtime_error("batch exceeds the context's max_batch");
+    for (int b = 0; b < B; ++b)
+        if (n_samples[b] < 0 || n_samples[b] > 480000 || (int64_t)n_samples[b] > stride)
+            throw std::runtime_error("each window must hold 0..480000 samples within its stride");
+    HIP_CHECK(hipEventRecord(ev_[0], st_));
+    HIP_CHECK(hipMemcpyAsync(nsamp_, n_samples, B * 4, hipMemcpyHostToDevice, st_));
+    HIP_CHECK(hipEventRecord(ev_[1], st_));
+    run_mel(pcm_dev, stride, B, nullptr);
+    HIP_CHECK(hipEventRecord(ev_[2], st_));
+    run_encoder(B);
+    HIP_CHECK(hipEventRecord(ev_[3], st_));
+    run_cross_kv(B);
+    HIP_CHECK(hipEventRecord(ev_[4], st_));
+    run_decode(B, rq, tokens, top1, top2);
+    HIP_CHECK(hipEventRecord(ev_[5], st_));
+    HIP_CHECK(hipStreamSynchronize(st_));
+    HIP_CHECK(hipGetLastError());
+    float ms;
+    const double h2d = tm_.h2d_ms;
+    HIP_CHECK(hipEventElapsedTime(&ms, ev_[1], ev_[2])); tm_.mel_ms = ms;
+    HIP_CHECK(hipEventElapsedTime(&ms, ev_[2], ev_[3])); tm_.encoder_ms = ms;
+    HIP_CHECK(hipEventElapsedTime(&ms, ev_[3], ev_[4])); tm_.cross_kv_ms = ms;
+    HIP_CHECK(hipEventElapsedTime(&ms, ev_[4], ev_[5])); tm_.decode_ms = ms;
+    HIP_CHECK(hipEventElapsedTime(&ms, ev_[0], ev_[5])); tm_.total_ms = ms;
+    tm_.h2d_ms = h2d;
+    tm_.batch = B;
+}
+
+void Engine::stage_pcm(const float* const* pcm, const int* n, int B) {
+    HIP_CHECK(hipEventRecord(ev_[6], st_));
+    for (int b = 0; b < B; ++b) {
+        if (n[b] < 0 || n[b] > 480000) throw std::runtime_error("window longer than 30 s");
+        if (n[b] > 0)
+            HIP_CHECK(hipMemcpyAsync(pcm_ + (size_t)b * 480000, pcm[b], (size_t)n[b] * 4, hipMemcpyHostToDevice, st_));
+    }
+    HIP_CHECK(hipEventRecord(ev_[7], st_));
+    HIP_CHECK(hipEventSynchronize(ev_[7]));
+    float ms;
+    HIP_CHECK(hipEventElapsedTime(&ms, ev_[6], ev_[7]));
+    tm_.h2d_ms = ms;
+}
+
+void Engine::transcribe_host(const float* const* pcm, const int* n_samples, int B, const DecodeRequest& rq,
+                             int* tokens, float* top1, float* top2) {
+    select();
+    if (B < 1 || B > max_batch_) throw std::runtime_error("batch exceeds the context's max_batch");
+    stage_pcm(pcm, n_samples, B);
+    transcribe_device(pcm_, 480000, n_samples, B, rq, tokens, top1, top2);
+}
+
+// ----------------------------------------------------------------------------- debug hooks
+void Engine::debug_mel(const float* pcm_host, int n, float* out_host) {
+    select();
+    const float* p = pcm_host;
+    stage_pcm(&p, &n, 1);
+    HIP_CHECK(hipMemcpyAsync(nsamp_, &n, 4, hipMemcpyHostToDevice, st_));
+    float* dbg = nullptr;
+    const size_t bytes = (size_t)dm_.n_mels * 3000 * 4;
+    HIP_CHECK(hipMalloc(&dbg, bytes));
+    run_mel(pcm_, 480000, 1, dbg);
+    HIP_CHECK(hipMemcpyAsync(out_host, dbg, bytes, hipMemcpyDeviceToHost, st_));
+    HIP_CHECK(hipStreamSynchronize(st_));
+    HIP_CHECK(hipFree(dbg));
+}
+
+void Engine::debug_encode(const float* mel_host, float* out_host) {
+    select();
+    const int nm = dm_.n_mels, d = dm_.d, T = dm_.n_audio_ctx;
+    std::vector<char> img((size_t)MEL_ROWS * cp_ * esz_, 0);
+    for (int t = 0; t < 3000; ++t)
+        for (int c = 0; c < nm; ++c) {
+            const float v = mel_host[(size_t)c * 3000 + t];
+            const size_t o = (size_t)(t + 1) * cp_ + c;
+            if (esz_ == 2) ((uint16_t*)img.data())[o] = f2bf(v);
+            else ((float*)img.data())[o] = v;
+        }
+    HIP_CHECK(hipMemcpyAsync(mel_in_, img.data(), img.size(), hipMemcpyHostToDevice, st_));
+    run_encoder(1);
+    float* tmp = nullptr;
+    HIP_CHECK(hipMalloc(&tmp, (size_t)T * d * 4));
+    to_f32(dt_, enc_out_, tmp, (int64_t)T * d, st_);
+    HIP_CHECK(hipMemcpyAsync(out_host, tmp, (size_t)T * d * 4, hipMemcpyDeviceToHost, st_));
+    HIP_CHECK(hipStreamSynchronize(st_));
+    HIP_CHECK(hipFree(tmp));
+}
+
+bool Engine::debug_weight_checksum(int tid, double* out2) {
+    select();
+    auto it = tref_.find(tid);
+    if (it == tref_.end()) return false;
+    HIP_CHECK(hipMemsetAsync(scratch_, 0, 16, st_));
+    tensor_checksum(it->second.dt, it->second.p, it->second.n, scratch_, st_);
+    HIP_CHECK(hipMemcpyAsync(out2, scratch_, 16, hipMemcpyDeviceToHost, st_));
+    HIP_CHECK(hipStreamSynchronize(st_));
+    return true;
+}
+
+}  // namespace spt

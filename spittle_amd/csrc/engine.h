@@ -1,0 +1,151 @@
+// engine.h -- the device-resident Whisper engine behind the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+
+namespace spt {
+
+struct ModelDims {
+    std::string name;
+    int n_mels = 80, d = 384, n_head = 6, n_enc = 4, n_dec = 4, n_vocab = 51864;
+    int n_audio_ctx = 1500, n_text_ctx = 448;
+};
+
+// special token ids (whisper.cpp whisper_vocab + multilingual shift)
+struct Specials {
+    int eot, sot, translate, transcribe, solm, prev, nosp, not_, beg, n_langs;
+};
+Specials specials_for(int n_vocab);
+int lang_id(const std::string& code);  // whisper.cpp g_lang order; -1 if unknown
+
+struct DecodeRequest {
+    std::vector<int> prompt;    // shared by every sequence of the batch
+    int n_steps = 128;
+    uint32_t flags = 3;         // SUPPRESS_BLANK | NO_TIMESTAMPS
+    const int32_t* forced = nullptr;
+    int n_forced = 0;
+};
+
+struct Timings {
+    double mel_ms = 0, encoder_ms = 0, cross_kv_ms = 0, decode_ms = 0, total_ms = 0, h2d_ms = 0;
+    int n_decode_passes = 0, batch = 0;
+};
+
+class Engine {
+public:
+    Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64_t seed);
+    ~Engine();
+    Engine(const Engine&) = delete;
+    Engine& operator=(const Engine&) = delete;
+
+    const ModelDims& dims() const { return dm_; }
+    int dtype() const { return dt_; }
+    int max_batch() const { return max_batch_; }
+    int64_t weight_bytes() const { return wbytes_; }
+    int64_t workspace_bytes() const { return abytes_; }
+    const Timings& timings() const { return tm_; }
+
+    // pcm_dev: B windows of <= 480000 samples at pcm_dev + b * stride (device memory)
+    // tokens/top1/top2: host [B][n_steps]
+    void transcribe_device(const float* pcm_dev, int64_t stride, const int* n_samples, int B, const DecodeRequest& rq,
+                           int* tokens, float* top1, float* top2);
+    // host PCM convenience (stages into the engine's pcm buffer)
+    void transcribe_host(const float* const* pcm, const int* n_samples, int B, const DecodeRequest& rq, int* tokens,
+                         float* top1, float* top2);
+
+    void debug_mel(const float* pcm_host, int n, float* out_host);
+    void debug_encode(const float* mel_host, float* out_host);
+    bool debug_weight_checksum(int tid, double* out2);
+
+private:
+    void select() const;
+    void alloc_weights();
+    void generate_weights();
+    void alloc_workspace();
+    void upload_tables();
+    void stage_pcm(const float* const* pcm, const int* n, int B);
+    void run_mel(const float* pcm_dev, int64_t stride, int B, float* dbg);
+    void run_encoder(int B);
+    void run_cross_kv(int B);
+    void run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1, float* top2);
+    void enqueue_decoder_pass(int B, int Tq, const DecodeRequest& rq, int out_cap);
+
+    ModelDims dm_;
+    int dt_, dev_, max_batch_;
+    uint64_t seed_;
+    int esz_;     // bytes per weight / activation element
+    int cp_;      // padded mel channels (conv1 K = 3 * cp_)
+    hipStream_t st_ = nullptr;
+    std::vector<hipEvent_t> ev_;
+
+    // ---- weights (one arena)
+    char* warena_ = nullptr;
+    int64_t wbytes_ = 0;
+    struct EncL { float *ln1_w, *ln1_b; void* qkv_w; float* qkv_b; void* o_w; float* o_b; float *ln2_w, *ln2_b;
+                  void* fc1_w; float* fc1_b; void* fc2_w; float* fc2_b; };
+    struct DecL { float *ln1_w, *ln1_b; void* qkv_w; float* qkv_b; void* so_w; float* so_b; float *ln2_w, *ln2_b;
+                  void* cq_w; float* cq_b; void* co_w; float* co_b; float *ln3_w, *ln3_b; void* fc1_w; float* fc1_b;
+                  void* fc2_w; float* fc2_b; };
+    void *conv1_w_, *conv2_w_, *ckv_w_, *tok_emb_;
+    float *conv1_b_, *conv2_b_, *enc_pos_, *lnp_w_, *lnp_b_, *ckv_b_, *dec_pos_, *lnf_w_, *lnf_b_;
+    std::vector<EncL> enc_;
+    std::vector<DecL> dec_;
+    struct TRef { void* p; int64_t n; int dt; };
+    std::map<int, TRef> tref_;  // tensor id -> device location (for checksums)
+
+    // ---- tables
+    float *hann_ = nullptr, *sinv_ = nullptr, *cosv_ = nullptr, *filt_ = nullptr;
+    int* grp_ = nullptr;
+
+    // ---- workspace (one arena)
+    char* aarena_ = nullptr;
+    int64_t abytes_ = 0;
+    float* pcm_ = nullptr;
+    int* nsamp_ = nullptr;
+    float* mel_raw_ = nullptr;
+    unsigned* mel_max_ = nullptr;
+    void* mel_in_ = nullptr;
+    void* y1p_ = nullptr;
+    float* x_ = nullptr;
+    void *xn_ = nullptr, *qkv_ = nullptr, *ao_ = nullptr, *ff_ = nullptr, *enc_out_ = nullptr;
+    void* ckv_ = nullptr;   // cross K/V [L][2][B][H][1500][64]
+    void* skv_ = nullptr;   // self K/V  [L][2][B][H][ctx][64]
+    float* dx_ = nullptr;
+    void *dq_ = nullptr, *dao_ = nullptr, *dff_ = nullptr;
+    float* part_ = nullptr;
+    float* logits_ = nullptr;
+    int *tok_in_ = nullptr, *out_tok_ = nullptr, *done_ = nullptr, *forced_ = nullptr;
+    float *out_t1_ = nullptr, *out_t2_ = nullptr;
+    uint32_t* suppress_ = nullptr;
+    DecState* ds_ = nullptr;
+    double* scratch_ = nullptr;
+    int n_split_ = 4;
+
+    // ---- graphs (generation step, keyed by batch / decode configuration)
+    struct GraphKey {
+        int B, out_cap, n_forced;
+        uint32_t flags;
+        bool operator<(const GraphKey& o) const {
+            if (B != o.B) return B < o.B;
+            if (out_cap != o.out_cap) return out_cap < o.out_cap;
+            if (n_forced != o.n_forced) return n_forced < o.n_forced;
+            return flags < o.flags;
+        }
+    };
+    std::map<GraphKey, hipGraphExec_t> graphs_;
+    std::vector<uint32_t> host_suppress_;
+    uint32_t suppress_flags_ = ~0u;
+
+    Timings tm_;
+};
+
+// parse "synthetic:<model>[:enc=N][:dec=N][:seed=S]"; returns false if not synthetic
+bool parse_synthetic_spec(const std::string& spec, ModelDims* dm, uint64_t* seed, std::string* err);
+
+}  // namespace spt

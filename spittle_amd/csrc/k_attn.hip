@@ -1,0 +1,280 @@
+// k_attn.hip -- encoder self-attention (non-causal, T = 1500, d_head = 64),
+// flash style: the T x T score matrix never leaves registers.
+//
+// Replaces whisper.cpp's encoder attention (ggml mul_mat K.Q, soft_max_ext with
+// scale 1/sqrt(64), mul_mat V.P -- or flash_attn_ext) in whisper_build_graph_encoder.
+//
+// Workgroup = 4 waves = 128 queries of one (batch, head); each wave owns 32
+// queries.  K/V tiles of 64 keys are staged global -> LDS with
+// global_load_lds_dwordx4 (K XOR-swizzled on the source address), double
+// buffered.  Scores are computed transposed, S^T = K . Q^T, so each lane owns one
+// query column: the row max / row sum of the online softmax are in-lane plus one
+// cross-half shuffle, and the accumulator is directly the B operand of the next
+// product O^T += V^T . P^T (CDNA4 accumulator-as-operand layout); V^T fragments
+// come from ds_read_b64_tr_b16 transposed LDS reads.
+//   bf16: v_mfma_f32_32x32x16_bf16, f32 accumulate, bf16 P.
+//   f32 : v_mfma_f32_32x32x2_f32 (exact f32), P kept in f32 registers.
+#include "common.h"
+#include "kernels.h"
+
+namespace spt {
+
+namespace {
+
+constexpr float kScaleLog2 = 0.125f * 1.4426950408889634f;  // (1/sqrt(64)) * log2(e)
+
+__device__ __forceinline__ void glds16(const void* g, SPT_LDS void* l) {
+    __builtin_amdgcn_global_load_lds((const void*)g, l, 16, 0, 0);
+}
+
+__device__ __forceinline__ int key_of(int kt2, int r, int hf) { return 32 * kt2 + (r & 3) + 8 * (r >> 2) + 4 * hf; }
+
+// -------------------------------------------------------------------- bf16
+__global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16* __restrict__ qkv, int T, int H,
+                                                           bf16* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128];  // [buf][K|V][64 keys][128 B]
+    const int d = H * 64, ld = 3 * d;
+    const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int l32 = lane & 31, hf = lane >> 5;
+    const bf16* base = qkv + (size_t)b * T * ld;
+
+    const int q_abs = qt * 128 + wid * 32 + l32;
+    const bf16* qp = base + (size_t)min(q_abs, T - 1) * ld + h * 64;
+    bf16x8 qf[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s + 8 * hf);
+
+    auto lds_k = [&](int buf) -> SPT_LDS char* { return (SPT_LDS char*)smem + (buf * 2 + 0) * 8192; };
+    auto lds_v = [&](int buf) -> SPT_LDS char* { return (SPT_LDS char*)smem + (buf * 2 + 1) * 8192; };
+    const int prow = lane >> 3, pch = lane & 7;
+    auto stage = [&](int buf, int kt) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int p = wid * 2 + i;
+            const int rt = 8 * p + prow;
+            const int key = min(kt * 64 + rt, T - 1);
+            const bf16* kr = base + (size_t)key * ld + d + h * 64;
+            glds16(kr + 8 * (pch ^ (rt & 7)), lds_k(buf) + p * 1024);
+            glds16(kr + d + 8 * pch, lds_v(buf) + p * 1024);
+        }
+    };
+
+    float m_run = -INFINITY, l_run = 0.f;
+    f32x16 o[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
+
+    const int nkt = cdiv(T, 64);
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nkt) stage(cur ^ 1, kt + 1);
+        const SPT_LDS char* lk = lds_k(cur);
+        const SPT_LDS char* lv = lds_v(cur);
+        f32x16 s[2];
+#pragma unroll
+        for (int kt2 = 0; kt2 < 2; ++kt2) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) s[kt2][i] = 0.f;
+            const int row = 32 * kt2 + l32;
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                const int c = 2 * st + hf;
+                const bf16x8 a = *(const SPT_LDS bf16x8*)(lk + row * 128 + ((c ^ (row & 7)) << 4));
+                s[kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[st], s[kt2], 0, 0, 0);
+            }
+        }
+        if (kt * 64 + 64 > T) {
+#pragma unroll
+            for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (kt * 64 + key_of(kt2, r, hf) >= T) s[kt2][r] = -INFINITY;
+        }
+        float mloc = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mloc = fmaxf(mloc, fmaxf(s[0][r], s[1][r]));
+        mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+        const float m_new = fmaxf(m_run, mloc);
+        const float alpha = exp2f((m_run - m_new) * kScaleLog2);
+        const float mc = m_new * kScaleLog2;
+        float lsum = 0.f;
+        bf16x8 pf[2][2];
+#pragma unroll
+        for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float p = exp2f(s[kt2][r] * kScaleLog2 - mc);
+                lsum += p;
+                pf[kt2][r >> 3][r & 7] = (short)f2bf(p);
+            }
+        l_run = l_run * alpha + lsum;
+        m_run = m_new;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
+        // O^T += V^T . P^T
+        const int g = lane >> 4, i16 = lane & 15;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+            const int col = 32 * dt + 16 * (g & 1) + 4 * (i16 & 3);
+#pragma unroll
+            for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+                for (int sp = 0; sp < 2; ++sp) {
+                    const int key0 = 32 * kt2 + 16 * sp + 4 * hf + (i16 >> 2);
+                    const bf16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (SPT_LDS bf16x4v*)(lv + key0 * 128 + col * 2));
+                    const bf16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (SPT_LDS bf16x4v*)(lv + (key0 + 8) * 128 + col * 2));
+                    bf16x8 va;
+                    va[0] = lo[0]; va[1] = lo[1]; va[2] = lo[2]; va[3] = lo[3];
+                    va[4] = hi[0]; va[5] = hi[1]; va[6] = hi[2]; va[7] = hi[3];
+                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pf[kt2][sp], o[dt], 0, 0, 0);
+                }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+    const float inv = 1.0f / l_tot;
+    if (q_abs < T) {
+        bf16* orow = out + ((size_t)b * T + q_abs) * d + h * 64;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg) {
+                const int dd = 32 * dt + 8 * gg + 4 * hf;
+                *(uint2*)(orow + dd) = make_uint2(pack_bf2(o[dt][4 * gg + 0] * inv, o[dt][4 * gg + 1] * inv),
+                                                  pack_bf2(o[dt][4 * gg + 2] * inv, o[dt][4 * gg + 3] * inv));
+            }
+    }
+}
+
+// -------------------------------------------------------------------- f32
+__global__ __launch_bounds__(256, 1) void attn_f32_kernel(const float* __restrict__ qkv, int T, int H,
+                                                          float* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 256];  // [buf][K|V][64 keys][256 B]
+    const int d = H * 64, ld = 3 * d;
+    const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int l32 = lane & 31, hf = lane >> 5;
+    const float* base = qkv + (size_t)b * T * ld;
+
+    const int q_abs = qt * 128 + wid * 32 + l32;
+    const float* qp = base + (size_t)min(q_abs, T - 1) * ld + h * 64 + 32 * hf;
+    float qf[32];
+#pragma unroll
+    for (int s = 0; s < 32; s += 4) {
+        const float4 v = *(const float4*)(qp + s);
+        qf[s] = v.x; qf[s + 1] = v.y; qf[s + 2] = v.z; qf[s + 3] = v.w;
+    }
+    auto lds_k = [&](int buf) -> SPT_LDS char* { return (SPT_LDS char*)smem + (buf * 2 + 0) * 16384; };
+    auto lds_v = [&](int buf) -> SPT_LDS char* { return (SPT_LDS char*)smem + (buf * 2 + 1) * 16384; };
+    const int prow = lane >> 4, pch = lane & 15;
+    auto stage = [&](int buf, int kt) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int p = wid * 4 + i;  // 16 pieces of 4 rows x 256 B
+            const int rt = 4 * p + prow;
+            const int key = min(kt * 64 + rt, T - 1);
+            const float* kr = base + (size_t)key * ld + d + h * 64;
+            glds16(kr + 4 * (pch ^ (rt & 15)), lds_k(buf) + p * 1024);
+            glds16(kr + d + 4 * pch, lds_v(buf) + p * 1024);
+        }
+    };
+    float m_run = -INFINITY, l_run = 0.f;
+    f32x16 o[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
+    const int nkt = cdiv(T, 64);
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nkt) stage(cur ^ 1, kt + 1);
+        const SPT_LDS char* lk = lds_k(cur);
+        const SPT_LDS float* lv = (const SPT_LDS float*)lds_v(cur);
+        f32x16 s[2];
+#pragma unroll
+        for (int kt2 = 0; kt2 < 2; ++kt2) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) s[kt2][i] = 0.f;
+            const int row = 32 * kt2 + l32;
+#pragma unroll
+            for (int c8 = 0; c8 < 8; ++c8) {
+                const int c = 8 * hf + c8;
+                const f32x4 kv = *(const SPT_LDS f32x4*)(lk + row * 256 + ((c ^ (row & 15)) << 4));
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    s[kt2] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv[e], qf[4 * c8 + e], s[kt2], 0, 0, 0);
+            }
+        }
+        if (kt * 64 + 64 > T) {
+#pragma unroll
+            for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (kt * 64 + key_of(kt2, r, hf) >= T) s[kt2][r] = -INFINITY;
+        }
+        float mloc = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mloc = fmaxf(mloc, fmaxf(s[0][r], s[1][r]));
+        mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+        const float m_new = fmaxf(m_run, mloc);
+        const float alpha = exp2f((m_run - m_new) * kScaleLog2);
+        const float mc = m_new * kScaleLog2;
+        float lsum = 0.f;
+#pragma unroll
+        for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float p = exp2f(s[kt2][r] * kScaleLog2 - mc);
+                s[kt2][r] = p;
+                lsum += p;
+            }
+        l_run = l_run * alpha + lsum;
+        m_run = m_new;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+                for (int st = 0; st < 16; ++st) {
+                    const float va = lv[key_of(kt2, st, hf) * 64 + 32 * dt + l32];
+                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x2f32(va, s[kt2][st], o[dt], 0, 0, 0);
+                }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+    const float inv = 1.0f / l_tot;
+    if (q_abs < T) {
+        float* orow = out + ((size_t)b * T + q_abs) * d + h * 64;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg) {
+                const int dd = 32 * dt + 8 * gg + 4 * hf;
+                *(float4*)(orow + dd) = make_float4(o[dt][4 * gg + 0] * inv, o[dt][4 * gg + 1] * inv,
+                                                    o[dt][4 * gg + 2] * inv, o[dt][4 * gg + 3] * inv);
+            }
+    }
+}
+
+}  // namespace
+
+void enc_attention(int dtype, const void* qkv, int B, int T, int H, void* out, hipStream_t st) {
+    dim3 grid(cdiv(T, 128), H, B);
+    if (dtype == DT_BF16)
+        hipLaunchKernelGGL(attn_bf16_kernel, grid, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
+    else
+        hipLaunchKernelGGL(attn_f32_kernel, grid, dim3(256), 0, st, (const float*)qkv, T, H, (float*)out);
+}
+
+}  // namespace spt

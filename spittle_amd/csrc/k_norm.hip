@@ -1,0 +1,106 @@
+// k_norm.hip -- LayerNorm (eps 1e-5) of the f32 residual stream into the GEMM
+// input dtype.  Replaces ggml_norm + ggml_mul + ggml_add of whisper.cpp's
+// encoder blocks (pre-attention / pre-MLP LN and ln_post).  One wave per row,
+// the whole row held in registers as float4 (d <= 1280 -> 5 per lane), two-pass
+// mean / variance like ggml_compute_forward_norm_f32; HBM-bound.
+#include "common.h"
+#include "kernels.h"
+
+namespace spt {
+
+namespace {
+
+template <typename T> __device__ __forceinline__ void store4(T* p, float a, float b, float c, float d);
+template <> __device__ __forceinline__ void store4<float>(float* p, float a, float b, float c, float d) {
+    *(float4*)p = make_float4(a, b, c, d);
+}
+template <> __device__ __forceinline__ void store4<bf16>(bf16* p, float a, float b, float c, float d) {
+    *(uint2*)p = make_uint2(pack_bf2(a, b), pack_bf2(c, d));
+}
+
+template <typename T, int NV>
+__global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ x, int M, int d,
+                                                 const float* __restrict__ w, const float* __restrict__ bb,
+                                                 T* __restrict__ y) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const int n4 = d >> 2;
+    const float4* xr = (const float4*)(x + (size_t)row * d);
+    float4 v[NV];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int idx = lane + 64 * i;
+        if (idx < n4) {
+            v[i] = xr[idx];
+            s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+        } else {
+            v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+    const float mean = wave_sum(s) / (float)d;
+    float s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int idx = lane + 64 * i;
+        if (idx < n4) {
+            const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, e = v[i].w - mean;
+            s2 += (a * a + b * b) + (c * c + e * e);
+        }
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(s2) / (float)d + 1e-5f);
+    const float4* w4 = (const float4*)w;
+    const float4* b4 = (const float4*)bb;
+    T* yr = y + (size_t)row * d;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int idx = lane + 64 * i;
+        if (idx < n4) {
+            const float4 g = w4[idx], o = b4[idx];
+            store4<T>(yr + 4 * idx, (v[i].x - mean) * rstd * g.x + o.x, (v[i].y - mean) * rstd * g.y + o.y,
+                      (v[i].z - mean) * rstd * g.z + o.z, (v[i].w - mean) * rstd * g.w + o.w);
+        }
+    }
+}
+
+template <typename T>
+void ln_dispatch(const float* x, int M, int d, const float* w, const float* b, T* y, hipStream_t st) {
+    dim3 grid(cdiv(M, 4));
+    const int nv = cdiv(d, 256);
+    switch (nv) {
+        case 1: hipLaunchKernelGGL((ln_kernel<T, 1>), grid, dim3(256), 0, st, x, M, d, w, b, y); break;
+        case 2: hipLaunchKernelGGL((ln_kernel<T, 2>), grid, dim3(256), 0, st, x, M, d, w, b, y); break;
+        case 3: hipLaunchKernelGGL((ln_kernel<T, 3>), grid, dim3(256), 0, st, x, M, d, w, b, y); break;
+        case 4: hipLaunchKernelGGL((ln_kernel<T, 4>), grid, dim3(256), 0, st, x, M, d, w, b, y); break;
+        case 5: hipLaunchKernelGGL((ln_kernel<T, 5>), grid, dim3(256), 0, st, x, M, d, w, b, y); break;
+        case 6: hipLaunchKernelGGL((ln_kernel<T, 6>), grid, dim3(256), 0, st, x, M, d, w, b, y); break;
+        default: throw std::runtime_error("layernorm: d too large");
+    }
+}
+
+template <typename T>
+__global__ void to_f32_kernel(const T* __restrict__ s, float* __restrict__ d, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        d[i] = to_f<T>(s[i]);
+}
+
+}  // namespace
+
+void layernorm(int dtype, const float* x, int M, int d, const float* w, const float* b, void* y, hipStream_t st) {
+    if (d % 4) throw std::runtime_error("layernorm: d % 4");
+    if (dtype == DT_BF16) ln_dispatch<bf16>(x, M, d, w, b, (bf16*)y, st);
+    else ln_dispatch<float>(x, M, d, w, b, (float*)y, st);
+}
+
+void to_f32(int dtype, const void* src, float* dst, int64_t n, hipStream_t st) {
+    int64_t g = (n + 255) / 256;
+    if (g > 8192) g = 8192;
+    if (g < 1) g = 1;
+    if (dtype == DT_BF16)
+        hipLaunchKernelGGL(to_f32_kernel<bf16>, dim3((int)g), dim3(256), 0, st, (const bf16*)src, dst, n);
+    else
+        hipLaunchKernelGGL(to_f32_kernel<float>, dim3((int)g), dim3(256), 0, st, (const float*)src, dst, n);
+}
+
+}  // namespace spt

@@ -1,0 +1,110 @@
+// kernels.h -- host launchers of the spittle_amd HIP kernels (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace spt {
+
+enum { DT_F32 = 0, DT_BF16 = 1 };
+
+// ------------------------------------------------------------------ GEMM (k_gemm.hip)
+enum { EPI_BIAS = 0, EPI_BIAS_GELU = 1, EPI_BIAS_GELU_POS = 2, EPI_BIAS_RESID = 3, EPI_KVSPLIT = 4 };
+
+struct GemmArgs {
+    const void* A; int lda; int64_t sA;   // A rows (+ batch stride, elements)
+    const void* W; int ldw;               // W [N][K] row-major (K contiguous)
+    int M, N, K;                          // M rows per batch item
+    const float* bias;                    // [N] or nullptr
+    void* C; int ldc; int64_t sC;         // output rows (+ batch stride)
+    const float* pos;                     // EPI_BIAS_GELU_POS: [M][N] f32
+    int kv_B, kv_T, kv_H;                 // EPI_KVSPLIT: dest [L][2][kv_B][kv_H][kv_T][64]
+};
+void gemm_nt(int dtype, int epi, const GemmArgs& g, int batch, hipStream_t st);
+
+// ------------------------------------------------------------------ weights (k_init.hip)
+enum { WK_MAT = 0, WK_BIAS = 1, WK_LNW = 2, WK_LNB = 3, WK_TOK = 4, WK_DPOS = 5 };
+// dst[i] = value(seed, tid, i) for i in [0, n); stored as f32 or bf16 (RNE)
+void gen_weights(int store_dtype, void* dst, int64_t n, uint64_t seed, uint32_t tid, int kind,
+                 int scale_exp, hipStream_t st);
+// canonical conv weight [N][C][3] -> device [N][3][Cp] (zero for c >= C)
+void gen_conv_weights(int store_dtype, void* dst, int N, int C, int Cp, uint64_t seed, uint32_t tid,
+                      int scale_exp, hipStream_t st);
+void fill_f32(float* dst, int64_t n, float v, hipStream_t st);
+// weight checksum helper for tests: sum of |w| and sum of w (f64) of a device tensor
+void tensor_checksum(int dtype, const void* src, int64_t n, double* out2_dev, hipStream_t st);
+
+// ------------------------------------------------------------------ mel (k_mel.hip)
+struct MelTables {
+    const float* hann;   // [400]
+    const float* sinv;   // [400]
+    const float* cosv;   // [400]
+    const float* filt;   // [n_mels][201]
+    const int* grp;      // [n_mels][2] first / last+1 group of 4 bins with a nonzero weight
+};
+constexpr int MEL_ROWS = 3002;  // padded time-major rows: [zero][3000 frames][zero]
+// log10 mel of every computed frame of each chunk; mel_raw [B][3002][n_mels]; max key per chunk
+void mel_frames(const float* pcm, int64_t pcm_stride, const int* n_samples, int B, int n_mels,
+                MelTables t, float* mel_raw, unsigned* mel_max, hipStream_t st);
+// clamp / normalise -> conv1 input [B][3002][Cp] (row 0 and 3001 zero); optional f32 [B][n_mels][3000]
+void mel_norm(int dtype, const float* mel_raw, const unsigned* mel_max, const int* n_samples, int B,
+              int n_mels, int Cp, void* mel_in, float* dbg, hipStream_t st);
+
+// ------------------------------------------------------------------ norm (k_norm.hip)
+// y[m] = LN(x[m]) * w + b ; x f32 [M][d], y f32/bf16 [M][d]
+void layernorm(int dtype, const float* x, int M, int d, const float* w, const float* b, void* y,
+               hipStream_t st);
+// convert an activation buffer to f32 (debug / tests)
+void to_f32(int dtype, const void* src, float* dst, int64_t n, hipStream_t st);
+
+// ------------------------------------------------------------------ encoder attention (k_attn.hip)
+// qkv [B*T][3*d] (q | k | v, head h at h*64), out [B*T][d]; non-causal, scale 1/8
+void enc_attention(int dtype, const void* qkv, int B, int T, int H, void* out, hipStream_t st);
+
+// ------------------------------------------------------------------ decoder (k_dec.hip)
+struct DecState {        // device-resident step state
+    int pos0;            // position of the first token fed this pass
+    int step;            // index of the token being produced
+};
+
+enum { GV_BIAS = 0, GV_BIAS_GELU = 1, GV_BIAS_RESID = 2, GV_QKV_CACHE = 3, GV_LOGITS = 4 };
+struct GemvArgs {
+    // A: either LN(x) of f32 rows (ln_w != nullptr) or a dtype activation
+    const void* A; int lda; int a_row0;   // row i of A at A + (i * lda + a_row0)
+    const float* ln_w; const float* ln_b; // fused pre-LayerNorm when non-null (A is f32 then)
+    int R;                                // rows (<= 64)
+    const void* W; int N, K;              // W [N][K]
+    const float* bias;
+    void* C; int ldc;                     // output rows (GV_BIAS*, GV_LOGITS)
+    // GV_QKV_CACHE: q -> C, k/v -> cache [2][B][H][ctx][64] at position pos0 + t (row = b*Tq + t)
+    void* cache; int cache_B, cache_H, cache_ctx, Tq;
+    const DecState* st;
+};
+void gemv(int dtype, int mode, const GemvArgs& a, hipStream_t st);
+
+// x[b*Tq + t] = tok_emb[tok[b*Tq+t]] + pos_emb[pos0 + t]
+void dec_embed(int dtype, const int* tok, int R, int Tq, int d, const void* tok_emb,
+               const float* pos_emb, const DecState* ds, float* x, hipStream_t st);
+// self attention over the cache: q [R][d] (row b*Tq + t at position pos0 + t), keys 0..pos0+t
+void dec_self_attn(int dtype, const void* q, const void* cache, int B, int H, int ctx, int Tq,
+                   const DecState* ds, void* out, hipStream_t st);
+// cross attention over T_enc keys, split over key chunks; partials then combine
+void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int H, int T_enc, int Tq,
+                    int n_split, float* part, void* out, hipStream_t st);
+
+struct ArgmaxArgs {
+    const float* logits; int V;           // [B][V]
+    const uint32_t* suppress;             // [V/32 + 1] bitmask, always-suppressed ids
+    int blank0, blank1;                   // suppressed only on the first generated step (-1 = none)
+    int eot; int ignore_eot;
+    const int* forced; int forced_len;    // [B][forced_len] teacher forcing (nullptr = off)
+    int* next_tok;                        // [B] token fed next
+    int* out_tok; float* out_top1; float* out_top2; int out_cap;  // [B][out_cap]
+    int* done;                            // [B]
+    const DecState* ds;
+};
+void dec_argmax(const ArgmaxArgs& a, int B, hipStream_t st);
+// advance the step state: pos0 += Tq; step += 1
+void dec_advance(DecState* ds, int Tq, hipStream_t st);
+void dec_reset(DecState* ds, hipStream_t st);
+
+}  // namespace spt

@@ -1,0 +1,223 @@
+"""Host-side mirror of transcribe-rs' Whisper engine surface, over the C ABI.
+
+Reference interface (transcribe-rs 0.2.3, used by
+/root/reference/src-tauri/src/managers/transcription.rs):
+  * ``WhisperEngine::new()`` / ``load_model(&path)``        (transcription.rs:261-276)
+  * ``transcribe_samples(Vec<f32>, Option<WhisperInferenceParams>)
+     -> Result<TranscriptionResult>``                        (transcription.rs:494-503)
+  * ``unload_model()``                                       (transcription.rs:175-208)
+  * ``WhisperInferenceParams { language, translate, initial_prompt, ..Default }``
+                                                             (transcription.rs:445-499)
+  * ``TranscriptionResult { text, segments }``; the app uses ``.text``
+                                                             (transcription.rs:537-546)
+
+Same names, same meaning, same error behaviour (an exception carrying the
+status and message where the Rust engine returns ``Err(Box<dyn Error>)``).
+Everything below the boundary runs on the GPU (libspittle_hip.so); there is no
+CPU path here.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib as L
+
+
+class TranscriptionError(RuntimeError):
+    def __init__(self, status: int, message: str):
+        super().__init__(f"{L.STATUS_NAMES.get(status, status)}: {message}")
+        self.status = status
+        self.message = message
+
+
+@dataclass
+class WhisperModelParams:
+    dtype: str = "bf16"          # "bf16" | "f32"
+    device: int = 0
+    max_batch: int = 8
+    seed: int = 1234             # synthetic weights
+
+
+@dataclass
+class WhisperInferenceParams:
+    language: Optional[str] = None      # None = auto-detect (settings "auto")
+    translate: bool = False
+    initial_prompt: Optional[str] = None
+    # whisper_full_params the app leaves at their defaults
+    suppress_blank: bool = True
+    no_timestamps: bool = True
+    max_new_tokens: int = 220
+    temperature: float = 0.0
+    beam_size: int = 1
+    # benchmark / test hooks
+    ignore_eot: bool = False
+    forced_tokens: Optional[np.ndarray] = None  # [batch][n] teacher forcing
+
+
+@dataclass
+class TranscriptionSegment:
+    start: float
+    end: float
+    text: str
+
+
+@dataclass
+class TranscriptionResult:
+    text: str
+    segments: list = field(default_factory=list)
+    tokens: list = field(default_factory=list)
+    top1: Optional[np.ndarray] = None
+    top2: Optional[np.ndarray] = None
+    n_windows: int = 0
+
+
+def _infer_params(p: Optional[WhisperInferenceParams], keep: list) -> L.InferParams:
+    p = p or WhisperInferenceParams()
+    ip = L.InferParams()
+    ip.language = p.language.encode() if p.language else None
+    ip.translate = int(bool(p.translate))
+    ip.initial_prompt = p.initial_prompt.encode() if p.initial_prompt else None
+    ip.flags = (L.SPT_SUPPRESS_BLANK if p.suppress_blank else 0) | \
+               (L.SPT_NO_TIMESTAMPS if p.no_timestamps else 0) | (L.SPT_IGNORE_EOT if p.ignore_eot else 0)
+    ip.max_new_tokens = int(p.max_new_tokens)
+    ip.temperature = float(p.temperature)
+    ip.beam_size = int(p.beam_size)
+    if p.forced_tokens is not None:
+        f = np.ascontiguousarray(p.forced_tokens, dtype=np.int32)
+        keep.append(f)
+        ip.forced_tokens = f.ctypes.data_as(C.POINTER(C.c_int32))
+        ip.n_forced = int(f.shape[-1])
+    return ip
+
+
+def _take_result(rp) -> TranscriptionResult:
+    r = rp.contents
+    n = r.n_tokens
+    toks = [r.tokens[i] for i in range(n)]
+    t1 = np.ctypeslib.as_array(r.top1, shape=(n,)).copy() if n else np.zeros(0, np.float32)
+    t2 = np.ctypeslib.as_array(r.top2, shape=(n,)).copy() if n else np.zeros(0, np.float32)
+    res = TranscriptionResult(text=(r.text or b"").decode("utf-8", "replace"), segments=[], tokens=toks, top1=t1,
+                              top2=t2, n_windows=r.n_windows)
+    L.load().spt_result_free(rp)
+    return res
+
+
+class WhisperEngine:
+    """transcribe_rs::engines::whisper::WhisperEngine, MI355X-native."""
+
+    def __init__(self, params: Optional[WhisperModelParams] = None):
+        self._lib = L.load()
+        self._ctx = None
+        self.params = params or WhisperModelParams()
+        self.model_path = None
+
+    # -- lifecycle ----------------------------------------------------------
+    def load_model(self, model_path: str) -> None:
+        """`model_path`: a ggml .bin path (not yet supported) or
+        ``synthetic:<name>[:enc=N][:dec=N][:seed=S]``."""
+        self.unload_model()
+        mp = L.ModelParams()
+        self._lib.spt_default_model_params(C.byref(mp))
+        mp.dtype = L.SPT_DTYPE_BF16 if self.params.dtype == "bf16" else L.SPT_DTYPE_F32
+        mp.device = int(self.params.device)
+        mp.max_batch = int(self.params.max_batch)
+        mp.seed = int(self.params.seed)
+        ctx = C.c_void_p()
+        err = C.create_string_buffer(1024)
+        st = self._lib.spt_ctx_create(str(model_path).encode(), C.byref(mp), C.byref(ctx), err, 1024)
+        if st != L.SPT_OK:
+            raise TranscriptionError(st, err.value.decode())
+        self._ctx = ctx
+        self.model_path = model_path
+
+    def unload_model(self) -> None:
+        if self._ctx:
+            self._lib.spt_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def is_loaded(self) -> bool:
+        return bool(self._ctx)
+
+    def __del__(self):
+        try:
+            self.unload_model()
+        except Exception:
+            pass
+
+    def _check(self, st: int):
+        if st != L.SPT_OK:
+            raise TranscriptionError(st, self._lib.spt_last_error(self._ctx).decode())
+
+    def _need(self):
+        if not self._ctx:
+            raise TranscriptionError(L.SPT_ERR_INVALID_ARG, "Model is not loaded for transcription.")
+
+    # -- inference ----------------------------------------------------------
+    def transcribe_samples(self, samples, params: Optional[WhisperInferenceParams] = None) -> TranscriptionResult:
+        return self.transcribe_batch([samples], params)[0]
+
+    def transcribe_batch(self, batch: Sequence, params: Optional[WhisperInferenceParams] = None):
+        self._need()
+        keep: list = []
+        ip = _infer_params(params, keep)
+        arrs = [np.ascontiguousarray(np.asarray(s, dtype=np.float32).reshape(-1)) for s in batch]
+        n = len(arrs)
+        ptrs = (C.POINTER(C.c_float) * n)(*[a.ctypes.data_as(C.POINTER(C.c_float)) for a in arrs])
+        lens = (C.c_size_t * n)(*[a.size for a in arrs])
+        out = (C.POINTER(L.Result) * n)()
+        self._check(self._lib.spt_transcribe_batch(self._ctx, ptrs, lens, n, C.byref(ip), out))
+        return [_take_result(out[i]) for i in range(n)]
+
+    def transcribe_batch_device(self, dev_ptr: int, stride: int, lengths: Sequence[int],
+                                params: Optional[WhisperInferenceParams] = None):
+        """Windows (<= 30 s each) already resident in device memory at dev_ptr + b*stride floats."""
+        self._need()
+        keep: list = []
+        ip = _infer_params(params, keep)
+        n = len(lengths)
+        lens = (C.c_size_t * n)(*[int(x) for x in lengths])
+        out = (C.POINTER(L.Result) * n)()
+        self._check(self._lib.spt_transcribe_batch_device(self._ctx, C.c_void_p(dev_ptr), int(stride), lens, n,
+                                                          C.byref(ip), out))
+        return [_take_result(out[i]) for i in range(n)]
+
+    # -- introspection / test hooks -----------------------------------------
+    def info(self) -> dict:
+        self._need()
+        mi = L.ModelInfo()
+        self._check(self._lib.spt_ctx_info(self._ctx, C.byref(mi)))
+        return {k: getattr(mi, k) for k, _ in mi._fields_}
+
+    def timings(self) -> dict:
+        self._need()
+        t = L.Timings()
+        self._check(self._lib.spt_get_timings(self._ctx, C.byref(t)))
+        return {k: getattr(t, k) for k, _ in t._fields_}
+
+    def debug_mel(self, samples) -> np.ndarray:
+        self._need()
+        x = np.ascontiguousarray(np.asarray(samples, np.float32).reshape(-1))
+        out = np.empty((self.info()["n_mels"], 3000), np.float32)
+        self._check(self._lib.spt_debug_mel(self._ctx, x.ctypes.data_as(C.POINTER(C.c_float)), x.size,
+                                            out.ctypes.data_as(C.POINTER(C.c_float))))
+        return out
+
+    def debug_encode(self, mel) -> np.ndarray:
+        self._need()
+        info = self.info()
+        m = np.ascontiguousarray(mel, dtype=np.float32)
+        assert m.shape == (info["n_mels"], 3000)
+        out = np.empty((info["n_audio_ctx"], info["d"]), np.float32)
+        self._check(self._lib.spt_debug_encode(self._ctx, m.ctypes.data_as(C.POINTER(C.c_float)),
+                                               out.ctypes.data_as(C.POINTER(C.c_float))))
+        return out
+
+    def weight_checksum(self, tensor_id: int):
+        self._need()
+        o = (C.c_double * 2)()
+        self._check(self._lib.spt_debug_weight_checksum(self._ctx, int(tensor_id), o))
+        return float(o[0]), float(o[1])
