@@ -1,0 +1,165 @@
+"""RTFx benchmark of the MI355X Whisper backend (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2], one GPU): Whisper-large-v3 dimensions, bf16
+weights/activations (f32 accumulation), batch of 8 synthetic 30 s 16 kHz chunks
+(BASELINE.md §3 signal, seeds 1000+i), greedy decode with language "en",
+<|notimestamps|>, a 4-token prompt and 128 forced decode steps (EOT ignored:
+random-init weights never stop).  Weights are random-init from the shared seeded
+PRNG (no checkpoints offline).  One "step" = one batched call through the C ABI
+(spt_transcribe_batch_device): PCM resident in HBM -> log-mel -> encoder ->
+cross K/V -> 132 decoder passes -> tokens on the host.
+
+N > 1: one process per GPU (torchrun), each rank transcribes its own shard of
+8 utterances (weak scaling, no data-path collective), max time over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "RTFx (audio-sec/wall-sec) Whisper-large-v3 30s chunks @1/2/4/8 MI355X"
+MODEL_SPEC = "synthetic:large-v3"
+CHUNK_S = 30.0
+PROMPT_LEN = 4
+N_STEPS = 128
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
+MFMA_PEAK_BF16_TFS = 2500.0  # dense bf16
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=8, help="30 s chunks per GPU")
+    ap.add_argument("--model", default=MODEL_SPEC)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--decode-steps", type=int, default=N_STEPS)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-steps", type=int, default=4)
+    return ap.parse_args()
+
+
+def cpu_baseline(model_spec: str, sample_steps: int, decode_steps: int) -> dict:
+    """CPU baseline leg: the oracle (C restatement of the whisper-rs/whisper.cpp CPU
+    path, fp32, OpenMP) on a bounded sample of the same workload: one 30 s chunk
+    through log-mel + encoder + cross K/V + `sample_steps` decoder passes; the
+    decoder time is scaled to the full prompt + decode_steps passes."""
+    from oracle import oracle as O
+    name = model_spec.split(":")[1]
+    threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
+    O.set_threads(threads)
+    dims = O.dims_for(name)
+    m = O.Model(dims, 1234, O.W_F32)
+    x = O.synth_audio(0)
+    prompt = O.default_prompt(dims.n_vocab)
+    t0 = time.perf_counter()
+    mel = O.mel(x, dims.n_mels)
+    t1 = time.perf_counter()
+    enc = m.encode(mel)
+    t2 = time.perf_counter()
+    O.lib()  # cross K/V is computed inside decode; time it with a 1-step decode
+    m.decode(enc, prompt, 1, O.SUPPRESS_BLANK | O.NO_TIMESTAMPS | O.IGNORE_EOT)
+    t3 = time.perf_counter()
+    m.decode(enc, prompt, 1 + sample_steps, O.SUPPRESS_BLANK | O.NO_TIMESTAMPS | O.IGNORE_EOT)
+    t4 = time.perf_counter()
+    per_pass = max(((t4 - t3) - (t3 - t2)) / sample_steps, 1e-9)
+    first = t3 - t2  # cross K/V + prompt pass
+    total = (t1 - t0) + (t2 - t1) + first + per_pass * (decode_steps - 1)
+    m.close()
+    return {"value": round(CHUNK_S / total, 4), "unit": "audio-sec/wall-sec", "cores": threads, "kind": "port",
+            "sample": f"1 x 30 s chunk, {name} dims fp32: mel {t1 - t0:.2f}s + encoder {t2 - t1:.2f}s + "
+                      f"cross-KV+prompt pass {first:.2f}s + {sample_steps} timed decoder passes "
+                      f"({per_pass:.3f}s each) scaled to {decode_steps - 1}; est. {total:.1f}s per chunk"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from spittle_amd import WhisperEngine, WhisperInferenceParams, WhisperModelParams
+    from spittle_amd.synth import synth_audio
+
+    B = args.batch
+    # this rank's shard of the global utterance list
+    pcm = np.stack([synth_audio(rank * B + i) for i in range(B)])
+    pcm_dev = torch.from_numpy(pcm).to(dev)
+    torch.cuda.synchronize()
+
+    eng = WhisperEngine(WhisperModelParams(dtype=args.dtype, device=local, max_batch=B, seed=1234))
+    eng.load_model(args.model)
+    info = eng.info()
+    params = WhisperInferenceParams(language="en", ignore_eot=True, max_new_tokens=args.decode_steps)
+    lens = [pcm.shape[1]] * B
+
+    def step():
+        return eng.transcribe_batch_device(pcm_dev.data_ptr(), pcm.shape[1], lens, params)
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    assert all(len(r.tokens) == args.decode_steps for r in res)
+    phases = eng.timings()
+
+    audio_s = world * B * CHUNK_S * args.steps
+    value = audio_s / dt
+    ms_per_step = dt * 1000.0 / args.steps
+
+    roof = None
+    cpu = None
+    if rank == 0:
+        roof = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.model, args.cpu_sample_steps, args.decode_steps)
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "audio-sec/wall-sec", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic (BASELINE.md §3 seeded 16 kHz signal; random-init large-v3 weights)",
+            "config": {"workload": f"whisper-large-v3 30s chunks, batch {B}/GPU, greedy en, "
+                                   f"{PROMPT_LEN}-token prompt + {args.decode_steps} decode steps",
+                       "model": args.model, "global_batch": world * B, "seq_len": 1500,
+                       "decode_steps": args.decode_steps, "parallelism": f"replicas x{world} (utterance shards)"},
+            "phases_ms": {k: round(v, 3) for k, v in phases.items() if k.endswith("_ms")},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    eng.unload_model()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -352,7 +352,8 @@ void Engine::alloc_workspace() {
         dq_ = A(R * d);
         dao_ = A(R * d);
         dff_ = A(R * 4 * d);
-        part_ = (float*)c.take(R * H * n_split_ * 66 * 4);
+        part_ = (float*)c.take(B * ((V + 15) / 16) * 16);
+        arrive_ = (unsigned*)c.take(64);
         logits_ = (float*)c.take(B * V * 4);
         tok_in_ = (int*)c.take(R * 4);
         out_tok_ = (int*)c.take(B * ctx * 4);
@@ -437,7 +438,8 @@ void Engine::run_cross_kv(int B) {
 void Engine::enqueue_decoder_pass(int B, int Tq, const DecodeRequest& rq, int out_cap) {
     const int d = dm_.d, H = dm_.n_head, ctx = dm_.n_text_ctx, T = dm_.n_audio_ctx, R = B * Tq;
     const int64_t self_layer = (int64_t)2 * B * H * ctx * 64, cross_layer = (int64_t)2 * B * H * T * 64;
-    dec_embed(dt_, tok_in_, R, Tq, d, tok_emb_, dec_pos_, ds_, dx_, st_);
+    // dx_ already holds this pass's input embeddings (dec_embed for the prompt pass,
+    // dec_finalize of the previous pass afterwards)
     for (int l = 0; l < dm_.n_dec; ++l) {
         const DecL& e = dec_[l];
         void* skv_l = (char*)skv_ + self_layer * l * esz_;
@@ -455,7 +457,7 @@ void Engine::enqueue_decoder_pass(int B, int Tq, const DecodeRequest& rq, int ou
         a.A = dx_; a.lda = d; a.ln_w = e.ln2_w; a.ln_b = e.ln2_b; a.R = R;
         a.W = e.cq_w; a.N = d; a.K = d; a.bias = e.cq_b; a.C = dq_; a.ldc = d;
         gemv(dt_, GV_BIAS, a, st_);
-        dec_cross_attn(dt_, dq_, ckv_l, B, H, T, Tq, n_split_, part_, dao_, st_);
+        dec_cross_attn(dt_, dq_, ckv_l, B, H, T, Tq, 1, nullptr, dao_, st_);
         a = GemvArgs{};
         a.A = dao_; a.lda = d; a.R = R; a.W = e.co_w; a.N = d; a.K = d; a.bias = e.co_b; a.C = dx_; a.ldc = d;
         gemv(dt_, GV_BIAS_RESID, a, st_);
@@ -468,21 +470,25 @@ void Engine::enqueue_decoder_pass(int B, int Tq, const DecodeRequest& rq, int ou
         a.ldc = d;
         gemv(dt_, GV_BIAS_RESID, a, st_);
     }
+    const Specials sp = specials_for(dm_.n_vocab);
+    const int n_tiles = (dm_.n_vocab + 15) / 16;
     GemvArgs a{};
     a.A = dx_; a.lda = Tq * d; a.a_row0 = (Tq - 1) * d; a.ln_w = lnf_w_; a.ln_b = lnf_b_; a.R = B;
-    a.W = tok_emb_; a.N = dm_.n_vocab; a.K = d; a.C = logits_; a.ldc = dm_.n_vocab;
+    a.W = tok_emb_; a.N = dm_.n_vocab; a.K = d; a.C = logits_; a.ldc = dm_.n_vocab; a.st = ds_;
+    a.suppress = suppress_;
+    a.blank0 = (rq.flags & 1u) ? sp.eot : -1;
+    a.blank1 = (rq.flags & 1u) ? 220 : -1;
+    a.part = part_; a.n_tiles = n_tiles;
     gemv(dt_, GV_LOGITS, a, st_);
-    const Specials sp = specials_for(dm_.n_vocab);
-    ArgmaxArgs m{};
-    m.logits = logits_; m.V = dm_.n_vocab; m.suppress = suppress_;
-    m.blank0 = (rq.flags & 1u) ? sp.eot : -1;
-    m.blank1 = (rq.flags & 1u) ? 220 : -1;
-    m.eot = sp.eot; m.ignore_eot = (rq.flags & 4u) ? 1 : 0;
-    m.forced = rq.n_forced > 0 ? forced_ : nullptr; m.forced_len = rq.n_forced;
-    m.next_tok = tok_in_; m.out_tok = out_tok_; m.out_top1 = out_t1_; m.out_top2 = out_t2_; m.out_cap = out_cap;
-    m.done = done_; m.ds = ds_;
-    dec_argmax(m, B, st_);
-    dec_advance(ds_, Tq, st_);
+    FinalizeArgs f{};
+    f.part = part_; f.n_tiles = n_tiles;
+    f.eot = sp.eot; f.ignore_eot = (rq.flags & 4u) ? 1 : 0;
+    f.forced = rq.n_forced > 0 ? forced_ : nullptr; f.forced_len = rq.n_forced;
+    f.next_tok = tok_in_; f.out_tok = out_tok_; f.out_top1 = out_t1_; f.out_top2 = out_t2_; f.out_cap = out_cap;
+    f.done = done_;
+    f.emb = tok_emb_; f.pos = dec_pos_; f.d = d; f.ctx = ctx; f.Tq = Tq; f.x = dx_;
+    f.ds = ds_; f.arrive = arrive_;
+    dec_finalize(dt_, f, B, st_);
 }
 
 void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1, float* top2) {
@@ -519,7 +525,8 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
     HIP_CHECK(hipMemsetAsync(out_tok_, 0xFF, (size_t)B * out_cap * 4, st_));
     fill_f32(out_t1_, (int64_t)B * out_cap, -INFINITY, st_);
     fill_f32(out_t2_, (int64_t)B * out_cap, -INFINITY, st_);
-    dec_reset(ds_, st_);
+    dec_reset(ds_, arrive_, st_);
+    dec_embed(dt_, tok_in_, B * Tq, Tq, dm_.d, tok_emb_, dec_pos_, ds_, dx_, st_);
     enqueue_decoder_pass(B, Tq, rq, out_cap);  // prompt pass produces token 0
     int passes = 1;
     if (rq.n_steps > 1) {

@@ -118,7 +118,8 @@ private:
     void* skv_ = nullptr;   // self K/V  [L][2][B][H][ctx][64]
     float* dx_ = nullptr;
     void *dq_ = nullptr, *dao_ = nullptr, *dff_ = nullptr;
-    float* part_ = nullptr;
+    float* part_ = nullptr;     // logits top-2 partials [B][V/16]
+    unsigned* arrive_ = nullptr;
     float* logits_ = nullptr;
     int *tok_in_ = nullptr, *out_tok_ = nullptr, *done_ = nullptr, *forced_ = nullptr;
     float *out_t1_ = nullptr, *out_t2_ = nullptr;

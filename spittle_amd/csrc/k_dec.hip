@@ -4,14 +4,19 @@
 // the next step's input, and the per-step state (position, step index) lives in
 // device memory so one captured hipGraph replays every step.
 //
-// At batch <= 32 rows every projection is a weight stream (HBM-bound), so the
-// projections are "GEMV" kernels: a workgroup owns 16 output columns, its 4 waves
-// split K, each lane streams 64 contiguous bytes of one weight row per step
-// straight into registers (no LDS round trip), and the rows x 16 tile is an
-// MFMA (16x16x32 bf16 / 16x16x4 f32) with the activations as the A operand.
-// The pre-LayerNorm is fused into the projection that consumes it (row stats
-// recomputed per workgroup from the f32 residual), and bias / GELU / residual /
-// KV-cache append are fused epilogues.
+// At <= 64 rows every projection is a weight stream (HBM-bound), so projections
+// are "GEMV" kernels: a workgroup owns 16 x CT output columns; its 4 waves split
+// the column tiles and K; each lane streams 64 contiguous bytes of one weight
+// row per step straight into registers (two steps in flight, no LDS round trip)
+// and the rows x 16 tile is an MFMA (16x16x32 bf16 / 16x16x4 f32) with the
+// activations as the A operand.  A fused pre-LayerNorm is computed once per
+// workgroup into a bank-padded LDS image that the MFMA A fragments read;
+// bias / GELU / residual / KV-cache append are fused epilogues.
+//
+// Attention over the caches (self: <= 448 keys, cross: 1500 keys) is a
+// flash-decoding kernel: one workgroup of 8 waves per (batch, head), 8 lanes per
+// key so every load is a fully coalesced 16-byte-per-lane sweep of the K/V rows,
+// online softmax per wave, a one-shot cross-wave merge in LDS.
 #include "common.h"
 #include "kernels.h"
 
@@ -41,130 +46,207 @@ template <> struct GV<float> {
     typedef f32x4 frag;
 };
 
-template <typename T, int MODE, bool LN, int RG>
-__global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
+constexpr int GV_LDS_BYTES = 98304;  // LN image budget: rows x (K + pad) x sizeof(T)
+__host__ __device__ inline int gv_img_bytes(int R, int K, int esz) {
+    return ((R * (K + 16 / esz) * esz) + 15) & ~15;
+}
+
+struct alignas(16) TopP { float v1; int i1; float v2; int pad; };
+__device__ __forceinline__ TopP top_merge(TopP a, TopP b) {
+    const bool aw = (a.v1 > b.v1) || (a.v1 == b.v1 && a.i1 < b.i1);
+    TopP r;
+    r.pad = 0;
+    if (aw) { r.v1 = a.v1; r.i1 = a.i1; r.v2 = fmaxf(a.v2, b.v1); }
+    else { r.v1 = b.v1; r.i1 = b.i1; r.v2 = fmaxf(b.v2, a.v1); }
+    return r;
+}
+__device__ __forceinline__ TopP top_shfl(TopP t, int mask) {
+    TopP u;
+    u.v1 = __shfl_xor(t.v1, mask, 64);
+    u.i1 = __shfl_xor(t.i1, mask, 64);
+    u.v2 = __shfl_xor(t.v2, mask, 64);
+    u.pad = 0;
+    return u;
+}
+
+// NWV waves; CT column tiles of 16 per workgroup; KSPLIT = NWV / CT waves share a tile
+// and split its K.  Each wave keeps up to MAXJ super-steps of weights in flight.
+template <typename T, int MODE, bool LN, int RG, int NWV, int CT>
+__global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
     constexpr int KS = GV<T>::KS;
-    constexpr int EPL = KS / 4;  // elements per lane per super-step (64 bytes)
-    __shared__ float s_stat[64][2];
-    __shared__ f32x4 s_red[4][RG][64];
+    constexpr int EPL = KS / 4;          // elements per lane per super-step (64 bytes)
+    constexpr int CPE = 16 / sizeof(T);  // elements per 16-byte chunk
+    constexpr int KSPLIT = NWV / CT;
+    constexpr int MAXJ = 4;
+    typedef typename GV<T>::frag frag;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int fr = lane & 15, fq = lane >> 4;
-    const int n0 = blockIdx.x * 16;
+    const int ct = wid % CT, ks = wid / CT;
+    const int tile = blockIdx.x * CT + ct;
+    const int n0 = tile * 16;
     const int K = a.K;
+    const int lds_ld = K + CPE;  // padded row stride (elements): rows land 4 banks apart
+    const int nss = K / KS;
+    const T* wrow = (const T*)a.W + (size_t)min(n0 + fr, a.N - 1) * K + fq * EPL;
+
+    frag w[MAXJ][4];
+    auto load_chunk = [&](int j0) {
+#pragma unroll
+        for (int j = 0; j < MAXJ; ++j) {
+            const int ss = ks + (j0 + j) * KSPLIT;
+            if (ss < nss) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) w[j][i] = *(const frag*)(wrow + (size_t)ss * KS + i * CPE);
+            }
+        }
+    };
+    load_chunk(0);  // the first weight fetch overlaps the LayerNorm prologue
 
     if constexpr (LN) {
-        for (int r = wid; r < a.R; r += 4) {
+        T* img = (T*)smem;
+        for (int r = wid; r < a.R; r += NWV) {
             const float* xr = (const float*)a.A + (size_t)r * a.lda + a.a_row0;
+            float4 v[6];
             float s = 0.f;
-            for (int k = lane * 4; k < K; k += 256) {
-                const float4 v = *(const float4*)(xr + k);
-                s += (v.x + v.y) + (v.z + v.w);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const int k = lane * 4 + 256 * i;
+                if (k < K) {
+                    v[i] = *(const float4*)(xr + k);
+                    s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+                }
             }
             const float mean = wave_sum(s) / (float)K;
             float s2 = 0.f;
-            for (int k = lane * 4; k < K; k += 256) {
-                const float4 v = *(const float4*)(xr + k);
-                const float p = v.x - mean, q = v.y - mean, u = v.z - mean, w = v.w - mean;
-                s2 += (p * p + q * q) + (u * u + w * w);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const int k = lane * 4 + 256 * i;
+                if (k < K) {
+                    const float p = v[i].x - mean, q = v[i].y - mean, u = v[i].z - mean, ww = v[i].w - mean;
+                    s2 += (p * p + q * q) + (u * u + ww * ww);
+                }
             }
             const float rstd = 1.0f / sqrtf(wave_sum(s2) / (float)K + 1e-5f);
-            if (lane == 0) { s_stat[r][0] = mean; s_stat[r][1] = rstd; }
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const int k = lane * 4 + 256 * i;
+                if (k < K) {
+                    const float4 g = *(const float4*)(a.ln_w + k);
+                    const float4 b = *(const float4*)(a.ln_b + k);
+                    T* o = img + (size_t)r * lds_ld + k;
+                    o[0] = from_f<T>((v[i].x - mean) * rstd * g.x + b.x);
+                    o[1] = from_f<T>((v[i].y - mean) * rstd * g.y + b.y);
+                    o[2] = from_f<T>((v[i].z - mean) * rstd * g.z + b.z);
+                    o[3] = from_f<T>((v[i].w - mean) * rstd * g.w + b.w);
+                }
+            }
         }
         __syncthreads();
     }
 
-    const T* wrow = (const T*)a.W + (size_t)min(n0 + fr, a.N - 1) * K;
     f32x4 acc[RG];
 #pragma unroll
     for (int g = 0; g < RG; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    const int nss = K / KS;
-    for (int ss = wid; ss < nss; ss += 4) {
-        const int kb = ss * KS + fq * EPL;  // this lane's 64-byte slice of K
-        typename GV<T>::frag wf[4];
+    auto compute_chunk = [&](int j0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) wf[i] = *(const typename GV<T>::frag*)(wrow + kb + i * (16 / sizeof(T)));
+        for (int j = 0; j < MAXJ; ++j) {
+            const int ss = ks + (j0 + j) * KSPLIT;
+            if (ss >= nss) break;
+            const int kb = ss * KS + fq * EPL;
 #pragma unroll
-        for (int g = 0; g < RG; ++g) {
-            const int row = g * 16 + fr;
-            typename GV<T>::frag af[4];
-            if (row < a.R) {
-                if constexpr (LN) {
-                    const float* xr = (const float*)a.A + (size_t)row * a.lda + a.a_row0 + kb;
-                    const float mean = s_stat[row][0], rstd = s_stat[row][1];
-                    const float* gw = a.ln_w + kb;
-                    const float* gb = a.ln_b + kb;
-                    if constexpr (sizeof(T) == 2) {
+            for (int g = 0; g < RG; ++g) {
+                const int row = g * 16 + fr;
+                frag af[4];
+                if (row < a.R) {
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-#pragma unroll
-                            for (int j = 0; j < 8; j += 4) {
-                                const float4 v = *(const float4*)(xr + 8 * i + j);
-                                const float4 w = *(const float4*)(gw + 8 * i + j);
-                                const float4 bb = *(const float4*)(gb + 8 * i + j);
-                                af[i][j + 0] = (short)f2bf((v.x - mean) * rstd * w.x + bb.x);
-                                af[i][j + 1] = (short)f2bf((v.y - mean) * rstd * w.y + bb.y);
-                                af[i][j + 2] = (short)f2bf((v.z - mean) * rstd * w.z + bb.z);
-                                af[i][j + 3] = (short)f2bf((v.w - mean) * rstd * w.w + bb.w);
-                            }
-                        }
-                    } else {
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            const float4 v = *(const float4*)(xr + 4 * i);
-                            const float4 w = *(const float4*)(gw + 4 * i);
-                            const float4 bb = *(const float4*)(gb + 4 * i);
-                            af[i][0] = (v.x - mean) * rstd * w.x + bb.x;
-                            af[i][1] = (v.y - mean) * rstd * w.y + bb.y;
-                            af[i][2] = (v.z - mean) * rstd * w.z + bb.z;
-                            af[i][3] = (v.w - mean) * rstd * w.w + bb.w;
-                        }
+                    for (int i = 0; i < 4; ++i) {
+                        if constexpr (LN)
+                            af[i] = *(const frag*)((const T*)smem + (size_t)row * lds_ld + kb + i * CPE);
+                        else
+                            af[i] = *(const frag*)((const T*)a.A + (size_t)row * a.lda + a.a_row0 + kb + i * CPE);
                     }
                 } else {
-                    const T* ar = (const T*)a.A + (size_t)row * a.lda + a.a_row0 + kb;
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) af[i] = *(const typename GV<T>::frag*)(ar + i * (16 / sizeof(T)));
+                    for (int i = 0; i < 4; ++i) af[i] = frag{};
                 }
-            } else {
+                if constexpr (sizeof(T) == 2) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) af[i] = typename GV<T>::frag{};
-            }
-            if constexpr (sizeof(T) == 2) {
+                    for (int i = 0; i < 4; ++i)
+                        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], w[j][i], acc[g], 0, 0, 0);
+                } else {
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], wf[i], acc[g], 0, 0, 0);
-            } else {
+                    for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][e], wf[i][e], acc[g], 0, 0, 0);
+                        for (int e = 0; e < 4; ++e)
+                            acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][e], w[j][i][e], acc[g], 0, 0, 0);
+                }
             }
         }
+    };
+    for (int j0 = 0; ks + j0 * KSPLIT < nss; j0 += MAXJ) {
+        if (j0 > 0) load_chunk(j0);
+        compute_chunk(j0);
     }
+
+    // cross-wave K reduction (waves sharing a column tile)
+    if constexpr (KSPLIT > 1) {
+        f32x4* red = (f32x4*)(smem + (LN ? gv_img_bytes(a.R, K, sizeof(T)) : 0));
+        if (LN) __syncthreads();  // the LN image region is not reused, but keep waves in step
 #pragma unroll
-    for (int g = 0; g < RG; ++g) s_red[wid][g][lane] = acc[g];
-    __syncthreads();
-    if (wid != 0) return;
+        for (int g = 0; g < RG; ++g) red[(wid * RG + g) * 64 + lane] = acc[g];
+        __syncthreads();
+        if (ks != 0) return;
+#pragma unroll
+        for (int g = 0; g < RG; ++g) {
+            f32x4 v = acc[g];
+#pragma unroll
+            for (int s = 1; s < KSPLIT; ++s) v += red[(((s * CT) + ct) * RG + g) * 64 + lane];
+            acc[g] = v;
+        }
+    }
     const int n = n0 + fr;
+    if constexpr (MODE == GV_LOGITS) {
+        // logits + this tile's suppressed top-2 per row (finished by dec_finalize)
+        const int step = a.st->step;
+        const bool nvalid = n < a.N;
+        bool sup = !nvalid;
+        if (nvalid) {
+            sup = (a.suppress[n >> 5] >> (n & 31)) & 1u;
+            if (step == 0 && (n == a.blank0 || n == a.blank1)) sup = true;
+        }
+#pragma unroll
+        for (int g = 0; g < RG; ++g) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = g * 16 + 4 * fq + r;
+                const float v = acc[g][r];
+                if (nvalid && row < a.R) ((float*)a.C)[(size_t)row * a.ldc + n] = v;
+                TopP t{sup ? -INFINITY : v, nvalid ? n : 0x7fffffff, -INFINITY, 0};
+                t = top_merge(t, top_shfl(t, 1));
+                t = top_merge(t, top_shfl(t, 2));
+                t = top_merge(t, top_shfl(t, 4));
+                t = top_merge(t, top_shfl(t, 8));
+                if (fr == 0 && row < a.R) ((TopP*)a.part)[(size_t)row * a.n_tiles + tile] = t;
+            }
+        }
+        return;
+    }
     if (n >= a.N) return;
     const float bv = a.bias ? a.bias[n] : 0.0f;
 #pragma unroll
     for (int g = 0; g < RG; ++g) {
-        const f32x4 v = s_red[0][g][lane] + s_red[1][g][lane] + s_red[2][g][lane] + s_red[3][g][lane];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int row = g * 16 + 4 * fq + r;
             if (row >= a.R) continue;
-            const float y = v[r] + bv;
+            const float y = acc[g][r] + bv;
             if constexpr (MODE == GV_BIAS) {
                 ((T*)a.C)[(size_t)row * a.ldc + n] = from_f<T>(y);
             } else if constexpr (MODE == GV_BIAS_GELU) {
                 ((T*)a.C)[(size_t)row * a.ldc + n] = from_f<T>(gelu_tanh(y));
             } else if constexpr (MODE == GV_BIAS_RESID) {
                 ((float*)a.C)[(size_t)row * a.ldc + n] += y;
-            } else if constexpr (MODE == GV_LOGITS) {
-                ((float*)a.C)[(size_t)row * a.ldc + n] = v[r];
             } else if constexpr (MODE == GV_QKV_CACHE) {
                 const int d = a.cache_H * 64;
                 if (n < d) {
@@ -183,235 +265,267 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
     }
 }
 
+template <typename T, int MODE, bool LN, int RG, int NWV, int CT>
+void gemv_launch_cfg(const GemvArgs& a, hipStream_t st) {
+    const int red = NWV * RG * 64 * (int)sizeof(f32x4);
+    const int lds = (LN ? gv_img_bytes(a.R, a.K, sizeof(T)) : 0) + (NWV / CT > 1 ? red : 0);
+    static bool attr_set = false;  // allow > 64 KiB of dynamic LDS (one-time, per instantiation)
+    if (!attr_set) {
+        HIP_CHECK(hipFuncSetAttribute((const void*)gemv_kernel<T, MODE, LN, RG, NWV, CT>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, GV_LDS_BYTES + red));
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((gemv_kernel<T, MODE, LN, RG, NWV, CT>), dim3(cdiv(a.N, 16 * CT)), dim3(64 * NWV), lds, st,
+                       a);
+}
+
+template <typename T, int MODE, bool LN, int RG>
+void gemv_launch_rg(const GemvArgs& a, hipStream_t st) {
+    // wide weight streams (logits): 64 columns x 8 waves per workgroup; the rest:
+    // 16 columns x 8 waves, each wave holding up to 4 super-steps of its K slice in flight
+    if (a.N >= 16384) gemv_launch_cfg<T, MODE, LN, RG, 8, 4>(a, st);
+    else gemv_launch_cfg<T, MODE, LN, RG, 8, 1>(a, st);
+}
+
 template <typename T, int MODE>
 void gemv_launch(const GemvArgs& a, hipStream_t st) {
-    dim3 grid(cdiv(a.N, 16));
     const bool ln = a.ln_w != nullptr;
+    if (ln && (gv_img_bytes(a.R, a.K, sizeof(T)) > GV_LDS_BYTES || a.K > 1536))
+        throw std::runtime_error("gemv: LayerNorm image exceeds LDS budget");
     if (a.R <= 16) {
-        if (ln) hipLaunchKernelGGL((gemv_kernel<T, MODE, true, 1>), grid, dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((gemv_kernel<T, MODE, false, 1>), grid, dim3(256), 0, st, a);
+        if (ln) gemv_launch_rg<T, MODE, true, 1>(a, st);
+        else gemv_launch_rg<T, MODE, false, 1>(a, st);
     } else if (a.R <= 32) {
-        if (ln) hipLaunchKernelGGL((gemv_kernel<T, MODE, true, 2>), grid, dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((gemv_kernel<T, MODE, false, 2>), grid, dim3(256), 0, st, a);
+        if (ln) gemv_launch_rg<T, MODE, true, 2>(a, st);
+        else gemv_launch_rg<T, MODE, false, 2>(a, st);
     } else {
-        if (ln) hipLaunchKernelGGL((gemv_kernel<T, MODE, true, 4>), grid, dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((gemv_kernel<T, MODE, false, 4>), grid, dim3(256), 0, st, a);
+        if (ln) gemv_launch_rg<T, MODE, true, 4>(a, st);
+        else gemv_launch_rg<T, MODE, false, 4>(a, st);
     }
 }
 
 // ------------------------------------------------------------------ attention (decode)
-// One workgroup per (b, h, key chunk).  Scores thread-per-key (Tq <= 4 queries),
-// softmax over the chunk, then P.V with 64 dims x 4 key groups.
-template <typename T>
-__device__ __forceinline__ void load_row64(const T* p, float* v) {
-    if constexpr (sizeof(T) == 2) {
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const bf16x8 x = *(const bf16x8*)(p + 8 * c);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[8 * c + j] = bf2f((bf16)x[j]);
-        }
-    } else {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) {
-            const float4 x = *(const float4*)(p + 4 * c);
-            v[4 * c] = x.x; v[4 * c + 1] = x.y; v[4 * c + 2] = x.z; v[4 * c + 3] = x.w;
-        }
-    }
-}
+constexpr int AW = 8;                 // waves per (b, h) workgroup
+constexpr float kLog2Scale = 0.125f * 1.4426950408889634f;
 
-constexpr int MAXQ = 4;       // queries per (b, h) in one pass (prompt of <= 4 tokens)
-constexpr int MAXKC = 512;    // keys per workgroup chunk
+template <typename T> struct KVChunk;  // 8 dims of one key row per lane
+template <> struct KVChunk<bf16> {
+    bf16x8 v;
+    __device__ __forceinline__ void load(const bf16* p) { v = *(const bf16x8*)p; }
+    __device__ __forceinline__ float at(int e) const { return bf2f((bf16)v[e]); }
+};
+template <> struct KVChunk<float> {
+    f32x4 a, b;
+    __device__ __forceinline__ void load(const float* p) { a = *(const f32x4*)p; b = *(const f32x4*)(p + 4); }
+    __device__ __forceinline__ float at(int e) const { return e < 4 ? a[e] : b[e - 4]; }
+};
 
-// Kc: keys [kc0, kc1) of the K/V arrays (row stride 64); queries q[t] (t < Tq) see keys
-// < kv_lim(t).  Writes unnormalised (m, l, o) of each query.
-template <typename T>
-__device__ void attn_chunk(const T* __restrict__ Kc, const T* __restrict__ Vc, int kc0, int kc1, const float* sq,
-                           int Tq, const int* kv_lim, float* s_p, float* s_red, float* out_m, float* out_l,
-                           float* out_o /* [Tq][64] */) {
-    const int tid = threadIdx.x;
-    const int nk = kc1 - kc0;
-    // scores
-    for (int j = tid; j < nk; j += 256) {
-        float kv[64];
-        load_row64<T>(Kc + (size_t)(kc0 + j) * 64, kv);
-        for (int t = 0; t < Tq; ++t) {
-            float s = 0.f;
-#pragma unroll
-            for (int e = 0; e < 64; ++e) s += sq[t * 64 + e] * kv[e];
-            s_p[t * MAXKC + j] = (kc0 + j < kv_lim[t]) ? s * 0.125f : -INFINITY;
-        }
-    }
-    __syncthreads();
-    for (int t = 0; t < Tq; ++t) {
-        // max
-        float m = -INFINITY;
-        for (int j = tid; j < nk; j += 256) m = fmaxf(m, s_p[t * MAXKC + j]);
-        m = wave_max(m);
-        if ((tid & 63) == 0) s_red[tid >> 6] = m;
-        __syncthreads();
-        m = fmaxf(fmaxf(s_red[0], s_red[1]), fmaxf(s_red[2], s_red[3]));
-        __syncthreads();
-        float l = 0.f;
-        for (int j = tid; j < nk; j += 256) {
-            const float s = s_p[t * MAXKC + j];
-            const float p = (m == -INFINITY) ? 0.f : __expf(s - m);
-            s_p[t * MAXKC + j] = p;
-            l += p;
-        }
-        l = wave_sum(l);
-        if ((tid & 63) == 0) s_red[tid >> 6] = l;
-        __syncthreads();
-        l = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
-        if (tid == 0) { out_m[t] = m; out_l[t] = l; }
-        __syncthreads();
-    }
-    // P.V : thread (e = tid & 63, g = tid >> 6) sums keys j = g, g+4, ...
-    const int e = tid & 63, g = tid >> 6;
-    float accv[MAXQ] = {0.f, 0.f, 0.f, 0.f};
-    for (int j = g; j < nk; j += 4) {
-        const float v = to_f<T>(Vc[(size_t)(kc0 + j) * 64 + e]);
-        for (int t = 0; t < Tq; ++t) accv[t] += s_p[t * MAXKC + j] * v;
-    }
-    __shared__ float s_acc[4][MAXQ][64];
-    for (int t = 0; t < Tq; ++t) s_acc[g][t][e] = accv[t];
-    __syncthreads();
-    if (g == 0)
-        for (int t = 0; t < Tq; ++t) out_o[t * 64 + e] = (s_acc[0][t][e] + s_acc[1][t][e]) + (s_acc[2][t][e] + s_acc[3][t][e]);
-    __syncthreads();
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void self_attn_kernel(const T* __restrict__ q, const T* __restrict__ cache, int B,
-                                                        int H, int ctx, int Tq, const DecState* __restrict__ ds,
-                                                        T* __restrict__ out) {
-    __shared__ float sq[MAXQ * 64];
-    __shared__ float s_p[MAXQ * MAXKC];
-    __shared__ float s_red[4];
-    __shared__ float s_m[MAXQ], s_l[MAXQ], s_o[MAXQ * 64];
+// q rows: q + (b*Tq + t)*q_ld + h*64; K/V rows of (b, h): base + ((kv*B + b)*H + h)*ctx*64
+template <typename T, int NQ>
+__global__ __launch_bounds__(64 * AW) void dec_attn_kernel(const T* __restrict__ q, int q_ld,
+                                                           const T* __restrict__ kv, int B, int H, int ctx,
+                                                           int n_keys_static, int causal, int Tq,
+                                                           const DecState* __restrict__ ds, T* __restrict__ out) {
+    __shared__ float s_m[AW][NQ], s_l[AW][NQ];
+    __shared__ float s_o[AW][NQ][64];
     const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
-    const int d = H * 64;
-    const int pos0 = ds->pos0;
-    for (int i = threadIdx.x; i < Tq * 64; i += 256) {
-        const int t = i >> 6, e = i & 63;
-        sq[i] = to_f<T>(q[(size_t)(b * Tq + t) * d + h * 64 + e]);
-    }
-    int lim[MAXQ];
-    for (int t = 0; t < MAXQ; ++t) lim[t] = pos0 + t + 1;
-    __syncthreads();
-    const T* Kc = cache + (((size_t)0 * B + b) * H + h) * ctx * 64;
-    const T* Vc = cache + (((size_t)1 * B + b) * H + h) * ctx * 64;
-    attn_chunk<T>(Kc, Vc, 0, pos0 + Tq, sq, Tq, lim, s_p, s_red, s_m, s_l, s_o);
-    for (int i = threadIdx.x; i < Tq * 64; i += 256) {
-        const int t = i >> 6, e = i & 63;
-        out[(size_t)(b * Tq + t) * d + h * 64 + e] = from_f<T>(s_o[i] / s_l[t]);
-    }
-}
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int slot = lane >> 3, g = lane & 7;  // key slot within a group of 8, dim group (8 dims)
+    const int pos0 = causal ? ds->pos0 : 0;
+    const int n_keys = causal ? pos0 + Tq : n_keys_static;
+    const T* Kb = kv + (((size_t)0 * B + b) * H + h) * (size_t)ctx * 64 + 8 * g;
+    const T* Vb = kv + (((size_t)1 * B + b) * H + h) * (size_t)ctx * 64 + 8 * g;
 
-template <typename T>
-__global__ __launch_bounds__(256) void cross_attn_kernel(const T* __restrict__ q, const T* __restrict__ kv, int B,
-                                                         int H, int Tenc, int Tq, int nsplit, float* __restrict__ part) {
-    __shared__ float sq[MAXQ * 64];
-    __shared__ float s_p[MAXQ * MAXKC];
-    __shared__ float s_red[4];
-    __shared__ float s_m[MAXQ], s_l[MAXQ], s_o[MAXQ * 64];
-    const int sp = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-    const int d = H * 64;
-    for (int i = threadIdx.x; i < Tq * 64; i += 256) {
-        const int t = i >> 6, e = i & 63;
-        sq[i] = to_f<T>(q[(size_t)(b * Tq + t) * d + h * 64 + e]);
-    }
-    int lim[MAXQ];
-    for (int t = 0; t < MAXQ; ++t) lim[t] = Tenc;
-    __syncthreads();
-    const int chunk = cdiv(Tenc, nsplit);
-    const int k0 = sp * chunk, k1 = min(Tenc, k0 + chunk);
-    const T* Kc = kv + (((size_t)0 * B + b) * H + h) * Tenc * 64;
-    const T* Vc = kv + (((size_t)1 * B + b) * H + h) * Tenc * 64;
-    attn_chunk<T>(Kc, Vc, k0, k1, sq, Tq, lim, s_p, s_red, s_m, s_l, s_o);
-    // part layout [b*Tq + t][h][split][66] : m, l, o[64]
-    for (int i = threadIdx.x; i < Tq * 66; i += 256) {
-        const int t = i / 66, c = i - t * 66;
-        const float v = c == 0 ? s_m[t] : (c == 1 ? s_l[t] : s_o[t * 64 + c - 2]);
-        part[(((size_t)(b * Tq + t) * H + h) * nsplit + sp) * 66 + c] = v;
-    }
-}
-
-template <typename T>
-__global__ void combine_kernel(const float* __restrict__ part, int H, int nsplit, T* __restrict__ out) {
-    const int r = blockIdx.x, h = blockIdx.y, e = threadIdx.x;
-    const float* p = part + ((size_t)r * H + h) * nsplit * 66;
-    float m = -INFINITY;
-    for (int s = 0; s < nsplit; ++s) m = fmaxf(m, p[s * 66]);
-    float l = 0.f, o = 0.f;
-    for (int s = 0; s < nsplit; ++s) {
-        const float w = __expf(p[s * 66] - m);
-        l += p[s * 66 + 1] * w;
-        o += p[s * 66 + 2 + e] * w;
-    }
-    out[(size_t)r * H * 64 + h * 64 + e] = from_f<T>(o / l);
-}
-
-// ------------------------------------------------------------------ argmax + suppression
-struct Top { float v1; int i1; float v2; };
-__device__ __forceinline__ Top top_merge(Top a, Top b) {
-    const bool aw = (a.v1 > b.v1) || (a.v1 == b.v1 && a.i1 < b.i1);
-    Top r;
-    if (aw) { r.v1 = a.v1; r.i1 = a.i1; r.v2 = fmaxf(a.v2, b.v1); }
-    else { r.v1 = b.v1; r.i1 = b.i1; r.v2 = fmaxf(b.v2, a.v1); }
-    return r;
-}
-
-__global__ __launch_bounds__(1024) void argmax_kernel(ArgmaxArgs a) {
-    __shared__ Top s_top[16];
-    const int b = blockIdx.x, tid = threadIdx.x;
-    const int step = a.ds->step;
-    const float* lg = a.logits + (size_t)b * a.V;
-    Top t{-INFINITY, 0x7fffffff, -INFINITY};
-    for (int i = tid; i < a.V; i += 1024) {
-        float v = lg[i];
-        if ((a.suppress[i >> 5] >> (i & 31)) & 1u) v = -INFINITY;
-        if (step == 0 && (i == a.blank0 || i == a.blank1)) v = -INFINITY;
-        Top u{v, i, -INFINITY};
-        t = top_merge(t, u);
-    }
+    float qv[NQ][8], m[NQ], l[NQ], o[NQ][8];
+    int lim[NQ];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        Top u;
-        u.v1 = __shfl_xor(t.v1, o, 64);
-        u.i1 = __shfl_xor(t.i1, o, 64);
-        u.v2 = __shfl_xor(t.v2, o, 64);
-        t = top_merge(t, u);
+    for (int t = 0; t < NQ; ++t) {
+        const int tt = t < Tq ? t : Tq - 1;
+        const T* qr = q + (size_t)(b * Tq + tt) * q_ld + h * 64 + 8 * g;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qv[t][e] = to_f<T>(qr[e]) * kLog2Scale;
+        m[t] = -INFINITY;
+        l[t] = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[t][e] = 0.f;
+        lim[t] = causal ? pos0 + tt + 1 : n_keys;
     }
+    // NI groups of 8 keys per block; raw K/V chunks ping-pong so the next block streams in
+    constexpr int NI = (sizeof(T) == 2) ? (NQ == 1 ? 8 : 4) : (NQ == 1 ? 4 : 2);
+    constexpr int KB = 8 * NI;
+    const int nblk = cdiv(n_keys, KB);
+    KVChunk<T> kA[NI], vA[NI], kB[NI], vB[NI];
+    auto load_blk = [&](KVChunk<T>(&kc)[NI], KVChunk<T>(&vc)[NI], int blk) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int key = min(blk * KB + 8 * i + slot, n_keys - 1);
+            kc[i].load(Kb + (size_t)key * 64);
+            vc[i].load(Vb + (size_t)key * 64);
+        }
+    };
+    auto process = [&](const KVChunk<T>(&kc)[NI], const KVChunk<T>(&vc)[NI], int kbase) {
+#pragma unroll
+        for (int t = 0; t < NQ; ++t) {
+            if (t >= Tq) break;
+            float s[NI];
+            float mb = -INFINITY;
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                float v = 0.f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v += qv[t][e] * kc[i].at(e);
+                v += __shfl_xor(v, 1, 64);
+                v += __shfl_xor(v, 2, 64);
+                v += __shfl_xor(v, 4, 64);
+                if (kbase + 8 * i + slot >= lim[t]) v = -INFINITY;
+                s[i] = v;
+                mb = fmaxf(mb, v);
+            }
+            mb = fmaxf(mb, __shfl_xor(mb, 8, 64));
+            mb = fmaxf(mb, __shfl_xor(mb, 16, 64));
+            mb = fmaxf(mb, __shfl_xor(mb, 32, 64));
+            if (mb == -INFINITY) continue;
+            const float mn = fmaxf(m[t], mb);
+            const float alpha = exp2f(m[t] - mn);
+            float ls = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[t][e] *= alpha;
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const float p = exp2f(s[i] - mn);
+                ls += p;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[t][e] += p * vc[i].at(e);
+            }
+            l[t] = l[t] * alpha + ls;
+            m[t] = mn;
+        }
+    };
+    int blk = wid;
+    if (blk < nblk) load_blk(kA, vA, blk);
+    while (blk < nblk) {
+        int nb = blk + AW;
+        if (nb < nblk) load_blk(kB, vB, nb);
+        process(kA, vA, blk * KB);
+        blk = nb;
+        if (blk >= nblk) break;
+        nb = blk + AW;
+        if (nb < nblk) load_blk(kA, vA, nb);
+        process(kB, vB, blk * KB);
+        blk = nb;
+    }
+    // wave merge: sum l and o over the 8 key slots (m is wave-uniform)
+#pragma unroll
+    for (int t = 0; t < NQ; ++t) {
+        float lt = l[t];
+        lt += __shfl_xor(lt, 8, 64);
+        lt += __shfl_xor(lt, 16, 64);
+        lt += __shfl_xor(lt, 32, 64);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            float v = o[t][e];
+            v += __shfl_xor(v, 8, 64);
+            v += __shfl_xor(v, 16, 64);
+            v += __shfl_xor(v, 32, 64);
+            o[t][e] = v;
+        }
+        if (lane < 8) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s_o[wid][t][8 * g + e] = o[t][e];
+        }
+        if (lane == 0) {
+            s_m[wid][t] = m[t];
+            s_l[wid][t] = lt;
+        }
+    }
+    __syncthreads();
+    // workgroup merge: thread (t, e)
+    if (tid < 64 * Tq) {
+        const int t = tid >> 6, e = tid & 63;
+        float M = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < AW; ++w) M = fmaxf(M, s_m[w][t]);
+        float L = 0.f, O = 0.f;
+#pragma unroll
+        for (int w = 0; w < AW; ++w) {
+            if (s_m[w][t] == -INFINITY) continue;
+            const float f = exp2f(s_m[w][t] - M);
+            L += s_l[w][t] * f;
+            O += s_o[w][t][e] * f;
+        }
+        out[(size_t)(b * Tq + t) * (H * 64) + h * 64 + e] = from_f<T>(O / L);
+    }
+}
+
+template <typename T>
+void dec_attn_launch(const T* q, const T* kv, int B, int H, int ctx, int n_keys, int causal, int Tq,
+                     const DecState* ds, T* out, hipStream_t st) {
+    if (Tq == 1)
+        hipLaunchKernelGGL((dec_attn_kernel<T, 1>), dim3(B * H), dim3(64 * AW), 0, st, q, H * 64, kv, B, H, ctx, n_keys,
+                           causal, Tq, ds, out);
+    else
+        hipLaunchKernelGGL((dec_attn_kernel<T, 4>), dim3(B * H), dim3(64 * AW), 0, st, q, H * 64, kv, B, H, ctx, n_keys,
+                           causal, Tq, ds, out);
+}
+
+// ------------------------------------------------------------------ finalize
+// Per sequence: reduce the logits tiles' top-2, record the token, choose the next
+// input (argmax or forced), embed it for the next pass; the last block advances
+// the step state (every block reads it before arriving).
+template <typename T>
+__global__ __launch_bounds__(256) void finalize_kernel(FinalizeArgs a) {
+    __shared__ TopP s_top[4];
+    __shared__ int s_tok;
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const int step = a.ds->step, pos0 = a.ds->pos0;
+    TopP t{-INFINITY, 0x7fffffff, -INFINITY, 0};
+    const TopP* p = (const TopP*)a.part + (size_t)b * a.n_tiles;
+    for (int i = tid; i < a.n_tiles; i += 256) t = top_merge(t, p[i]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t = top_merge(t, top_shfl(t, o));
     if ((tid & 63) == 0) s_top[tid >> 6] = t;
     __syncthreads();
-    if (tid != 0) return;
-    for (int w = 1; w < 16; ++w) t = top_merge(t, s_top[w]);
-    const int oi = b * a.out_cap + step;
-    if (step >= a.out_cap) return;
-    if (a.done[b]) {
-        a.out_tok[oi] = -1;
-        a.out_top1[oi] = -INFINITY;
-        a.out_top2[oi] = -INFINITY;
-        a.next_tok[b] = a.eot;
-        return;
+    if (tid == 0) {
+        for (int w = 1; w < 4; ++w) t = top_merge(t, s_top[w]);
+        int nxt = a.eot;
+        if (step < a.out_cap) {
+            const int oi = b * a.out_cap + step;
+            if (a.done[b]) {
+                a.out_tok[oi] = -1;
+                a.out_top1[oi] = -INFINITY;
+                a.out_top2[oi] = -INFINITY;
+            } else {
+                a.out_tok[oi] = t.i1;
+                a.out_top1[oi] = t.v1;
+                a.out_top2[oi] = t.v2;
+                nxt = t.i1;
+                if (a.forced && step < a.forced_len) nxt = a.forced[b * a.forced_len + step];
+                if (!a.ignore_eot && t.i1 == a.eot) a.done[b] = 1;
+            }
+        }
+        a.next_tok[b] = nxt;
+        s_tok = nxt;
     }
-    a.out_tok[oi] = t.i1;
-    a.out_top1[oi] = t.v1;
-    a.out_top2[oi] = t.v2;
-    int nxt = t.i1;
-    if (a.forced && step < a.forced_len) nxt = a.forced[b * a.forced_len + step];
-    a.next_tok[b] = nxt;
-    if (!a.ignore_eot && t.i1 == a.eot) a.done[b] = 1;
+    __syncthreads();
+    const int tok = s_tok;
+    const int pn = min(pos0 + a.Tq, a.ctx - 1);
+    const T* e = (const T*)a.emb + (size_t)tok * a.d;
+    const float* pp = a.pos + (size_t)pn * a.d;
+    for (int i = tid; i < a.d; i += 256) a.x[(size_t)b * a.d + i] = to_f<T>(e[i]) + pp[i];
+    if (tid == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == (unsigned)gridDim.x - 1) {
+            a.ds->pos0 = pos0 + a.Tq;
+            a.ds->step = step + 1;
+            __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
-__global__ void advance_kernel(DecState* ds, int Tq) {
-    ds->pos0 += Tq;
-    ds->step += 1;
-}
-__global__ void reset_kernel(DecState* ds) {
+__global__ void reset_kernel(DecState* ds, unsigned* arrive) {
     ds->pos0 = 0;
     ds->step = 0;
+    *arrive = 0u;
 }
 
 }  // namespace
@@ -442,37 +556,31 @@ void dec_embed(int dtype, const int* tok, int R, int Tq, int d, const void* tok_
 
 void dec_self_attn(int dtype, const void* q, const void* cache, int B, int H, int ctx, int Tq, const DecState* ds,
                    void* out, hipStream_t st) {
-    if (Tq > MAXQ || ctx > MAXKC) throw std::runtime_error("dec_self_attn: shape");
+    if (Tq < 1 || Tq > 4) throw std::runtime_error("dec_self_attn: 1..4 queries per sequence");
     if (dtype == DT_BF16)
-        hipLaunchKernelGGL(self_attn_kernel<bf16>, dim3(B * H), dim3(256), 0, st, (const bf16*)q, (const bf16*)cache, B, H,
-                           ctx, Tq, ds, (bf16*)out);
+        dec_attn_launch<bf16>((const bf16*)q, (const bf16*)cache, B, H, ctx, 0, 1, Tq, ds, (bf16*)out, st);
     else
-        hipLaunchKernelGGL(self_attn_kernel<float>, dim3(B * H), dim3(256), 0, st, (const float*)q, (const float*)cache, B,
-                           H, ctx, Tq, ds, (float*)out);
+        dec_attn_launch<float>((const float*)q, (const float*)cache, B, H, ctx, 0, 1, Tq, ds, (float*)out, st);
 }
 
 void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int H, int T_enc, int Tq, int n_split, float* part,
                     void* out, hipStream_t st) {
-    if (Tq > MAXQ || cdiv(T_enc, n_split) > MAXKC) throw std::runtime_error("dec_cross_attn: shape");
-    dim3 grid(n_split, H, B);
-    if (dtype == DT_BF16) {
-        hipLaunchKernelGGL(cross_attn_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)q, (const bf16*)kv, B, H, T_enc,
-                           Tq, n_split, part);
-        hipLaunchKernelGGL(combine_kernel<bf16>, dim3(B * Tq, H), dim3(64), 0, st, part, H, n_split, (bf16*)out);
-    } else {
-        hipLaunchKernelGGL(cross_attn_kernel<float>, grid, dim3(256), 0, st, (const float*)q, (const float*)kv, B, H, T_enc,
-                           Tq, n_split, part);
-        hipLaunchKernelGGL(combine_kernel<float>, dim3(B * Tq, H), dim3(64), 0, st, part, H, n_split, (float*)out);
-    }
+    (void)n_split;
+    (void)part;
+    if (Tq < 1 || Tq > 4) throw std::runtime_error("dec_cross_attn: 1..4 queries per sequence");
+    if (dtype == DT_BF16)
+        dec_attn_launch<bf16>((const bf16*)q, (const bf16*)kv, B, H, T_enc, T_enc, 0, Tq, nullptr, (bf16*)out, st);
+    else
+        dec_attn_launch<float>((const float*)q, (const float*)kv, B, H, T_enc, T_enc, 0, Tq, nullptr, (float*)out, st);
 }
 
-void dec_argmax(const ArgmaxArgs& a, int B, hipStream_t st) {
-    hipLaunchKernelGGL(argmax_kernel, dim3(B), dim3(1024), 0, st, a);
+void dec_finalize(int dtype, const FinalizeArgs& a, int B, hipStream_t st) {
+    if (dtype == DT_BF16) hipLaunchKernelGGL(finalize_kernel<bf16>, dim3(B), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(finalize_kernel<float>, dim3(B), dim3(256), 0, st, a);
 }
 
-void dec_advance(DecState* ds, int Tq, hipStream_t st) {
-    hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(1), 0, st, ds, Tq);
+void dec_reset(DecState* ds, unsigned* arrive, hipStream_t st) {
+    hipLaunchKernelGGL(reset_kernel, dim3(1), dim3(1), 0, st, ds, arrive);
 }
-void dec_reset(DecState* ds, hipStream_t st) { hipLaunchKernelGGL(reset_kernel, dim3(1), dim3(1), 0, st, ds); }
 
 }  // namespace spt

@@ -78,6 +78,9 @@ struct GemvArgs {
     // GV_QKV_CACHE: q -> C, k/v -> cache [2][B][H][ctx][64] at position pos0 + t (row = b*Tq + t)
     void* cache; int cache_B, cache_H, cache_ctx, Tq;
     const DecState* st;
+    // GV_LOGITS: suppression + per-16-column-tile top-2 partials [R][n_tiles] (16 B each)
+    const uint32_t* suppress; int blank0, blank1;
+    void* part; int n_tiles;
 };
 void gemv(int dtype, int mode, const GemvArgs& a, hipStream_t st);
 
@@ -91,20 +94,19 @@ void dec_self_attn(int dtype, const void* q, const void* cache, int B, int H, in
 void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int H, int T_enc, int Tq,
                     int n_split, float* part, void* out, hipStream_t st);
 
-struct ArgmaxArgs {
-    const float* logits; int V;           // [B][V]
-    const uint32_t* suppress;             // [V/32 + 1] bitmask, always-suppressed ids
-    int blank0, blank1;                   // suppressed only on the first generated step (-1 = none)
+struct FinalizeArgs {
+    const void* part; int n_tiles;        // logits top-2 partials [B][n_tiles]
     int eot; int ignore_eot;
     const int* forced; int forced_len;    // [B][forced_len] teacher forcing (nullptr = off)
-    int* next_tok;                        // [B] token fed next
+    int* next_tok;                        // [B]
     int* out_tok; float* out_top1; float* out_top2; int out_cap;  // [B][out_cap]
     int* done;                            // [B]
-    const DecState* ds;
+    const void* emb; const float* pos; int d, ctx, Tq;  // next-pass embedding -> x rows 0..B-1
+    float* x;
+    DecState* ds; unsigned* arrive;       // step state, last-arriver counter
 };
-void dec_argmax(const ArgmaxArgs& a, int B, hipStream_t st);
-// advance the step state: pos0 += Tq; step += 1
-void dec_advance(DecState* ds, int Tq, hipStream_t st);
-void dec_reset(DecState* ds, hipStream_t st);
+// argmax reduce + record + next-token embed + step advance (replaces embed/argmax/advance)
+void dec_finalize(int dtype, const FinalizeArgs& a, int B, hipStream_t st);
+void dec_reset(DecState* ds, unsigned* arrive, hipStream_t st);
 
 }  // namespace spt
