@@ -79,6 +79,43 @@ def cpu_baseline(model_spec: str, sample_steps: int, decode_steps: int) -> dict:
                       f"({per_pass:.3f}s each) scaled to {decode_steps - 1}; est. {total:.1f}s per chunk"}
 
 
+DOMINANT = "dec_cross_attn"  # largest share of device time (profiles/*_kernel_stats.csv)
+KERNEL_NAMES = {
+    "dec_cross_attn": "dec_attn_kernel<bf16,1,false> (decoder cross-attention, 1 layer)",
+    "dec_logits": "gemv_kernel<bf16,GV_LOGITS,...> (final LN + logits + top-2)",
+    "dec_fc1": "gemv_kernel<bf16,GV_BIAS_GELU,...> (decoder LN + fc1 + GELU)",
+    "enc_fc1_gemm": "gemm_nt_kernel<bf16,EPI_BIAS_GELU> (encoder fc1)",
+    "enc_attn": "attn_bf16_kernel (encoder flash attention, 1 layer)",
+}
+
+
+def roofline(eng, iters: int = 50):
+    """Dominant-kernel roofline from HIP events on the engine stream (spt_probe_kernel:
+    the kernel re-launched back to back on the buffers of the last timed call).
+    achieved = algorithmic bytes (or flops) per launch / average launch duration.
+    traffic = PMC-measured HBM bytes per launch of the same kernel, from the committed
+    rocprofv3 --pmc summary (profiles/pmc_<kernel>.json), when present."""
+    rows = {}
+    for k, name in KERNEL_NAMES.items():
+        p = eng.probe(k, iters)
+        if p["work_is_flops"]:
+            ach, peak, unit = p["work"] / p["avg_us"] / 1e6, MFMA_PEAK_BF16_TFS, "TFLOP/s"
+        else:
+            ach, peak, unit = p["work"] / p["avg_us"] / 1e3, HBM_PEAK_GBS, "GB/s"
+        rows[k] = {"kernel": name, "bound": "mfma" if p["work_is_flops"] else "hbm", "avg_us": round(p["avg_us"], 3),
+                   "work_per_launch": p["work"], "achieved": round(ach, 1), "peak": peak, "unit": unit,
+                   "frac": round(ach / peak, 4)}
+    dom = dict(rows[DOMINANT])
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", f"pmc_{DOMINANT}.json")
+    if os.path.exists(pmc):
+        traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+    roof = {"kernel": dom["kernel"], "bound": dom["bound"], "achieved": dom["achieved"], "peak": dom["peak"],
+            "unit": dom["unit"], "frac": dom["frac"], "traffic": traffic, "avg_us": dom["avg_us"],
+            "algorithmic_bytes_per_launch": dom["work_per_launch"]}
+    return roof, rows
+
+
 def main():
     args = parse()
     import numpy as np
@@ -139,7 +176,7 @@ def main():
     roof = None
     cpu = None
     if rank == 0:
-        roof = None
+        roof, kernels = roofline(eng)
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.model, args.cpu_sample_steps, args.decode_steps)
     if rank == 0:
@@ -153,7 +190,7 @@ def main():
                        "model": args.model, "global_batch": world * B, "seq_len": 1500,
                        "decode_steps": args.decode_steps, "parallelism": f"replicas x{world} (utterance shards)"},
             "phases_ms": {k: round(v, 3) for k, v in phases.items() if k.endswith("_ms")},
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "kernels": kernels, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     eng.unload_model()

@@ -122,6 +122,21 @@ void spt_result_free(spt_result* r);
 
 spt_status spt_get_timings(const spt_ctx* ctx, spt_timings* t);
 
+/* Kernel probe (measurement): re-launch one hot-path kernel `iters` times back to
+ * back on the engine stream, on the buffers of the last call, between two HIP
+ * events.  avg_us = mean launch-to-launch time; work = algorithmic bytes (HBM-bound
+ * kernels) or flops (MFMA-bound kernels) per launch, work_is_flops says which. */
+typedef enum {
+    SPT_PROBE_DEC_CROSS_ATTN = 0,  /* decoder cross-attention, one layer */
+    SPT_PROBE_DEC_SELF_ATTN = 1,   /* decoder self-attention, one layer */
+    SPT_PROBE_DEC_LOGITS = 2,      /* final LayerNorm + logits + top-2 partials */
+    SPT_PROBE_DEC_FC1 = 3,         /* decoder LayerNorm + fc1 + GELU (weight stream) */
+    SPT_PROBE_ENC_FC1_GEMM = 4,    /* encoder fc1 GEMM + bias + GELU */
+    SPT_PROBE_ENC_ATTN = 5         /* encoder flash attention, one layer */
+} spt_probe_kind;
+spt_status spt_probe_kernel(spt_ctx* ctx, int32_t kind, int32_t iters, double* avg_us, double* work,
+                            int32_t* work_is_flops);
+
 /* test hooks (parity against the CPU restatement) */
 /* normalised log-mel of one window [n_mels][3000] (f32) */
 spt_status spt_debug_mel(spt_ctx* ctx, const float* pcm16k, size_t n_samples, float* out);

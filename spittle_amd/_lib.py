@@ -22,8 +22,10 @@ EXPORTS = [
     "spt_version", "spt_default_model_params", "spt_default_infer_params", "spt_ctx_create",
     "spt_ctx_destroy", "spt_last_error", "spt_ctx_info", "spt_transcribe", "spt_transcribe_batch",
     "spt_transcribe_batch_device", "spt_result_free", "spt_get_timings", "spt_debug_mel",
-    "spt_debug_encode", "spt_debug_weight_checksum",
+    "spt_debug_encode", "spt_debug_weight_checksum", "spt_probe_kernel",
 ]
+PROBES = {"dec_cross_attn": 0, "dec_self_attn": 1, "dec_logits": 2, "dec_fc1": 3, "enc_fc1_gemm": 4,
+          "enc_attn": 5}
 
 
 class ModelParams(C.Structure):
@@ -84,8 +86,11 @@ def load():
     L.spt_debug_mel.argtypes = [vp, fp, C.c_size_t, fp]
     L.spt_debug_encode.argtypes = [vp, fp, fp]
     L.spt_debug_weight_checksum.argtypes = [vp, C.c_int32, C.POINTER(C.c_double)]
+    L.spt_probe_kernel.argtypes = [vp, C.c_int32, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                   C.POINTER(C.c_int32)]
     for fn in ("spt_ctx_info", "spt_transcribe", "spt_transcribe_batch", "spt_transcribe_batch_device",
-               "spt_get_timings", "spt_debug_mel", "spt_debug_encode", "spt_debug_weight_checksum"):
+               "spt_get_timings", "spt_debug_mel", "spt_debug_encode", "spt_debug_weight_checksum",
+               "spt_probe_kernel"):
         getattr(L, fn).restype = C.c_int
     _lib = L
     return L

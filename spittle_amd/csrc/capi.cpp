@@ -390,3 +390,16 @@ spt_status spt_debug_weight_checksum(spt_ctx* ctx, int32_t tensor_id, double* ou
 }
 
 }  // extern "C"
+
+extern "C" spt_status spt_probe_kernel(spt_ctx* ctx, int32_t kind, int32_t iters, double* avg_us, double* work,
+                                       int32_t* work_is_flops) {
+    if (!ctx || !avg_us || !work || !work_is_flops) return fail(ctx, SPT_ERR_INVALID_ARG, "null argument");
+    try {
+        int f = 0;
+        *avg_us = ctx->eng->probe(kind, iters, work, &f);
+        *work_is_flops = f;
+        return SPT_OK;
+    } catch (const std::exception& e) {
+        return fail(ctx, classify(e), e.what());
+    }
+}

@@ -27,6 +27,9 @@ struct HipError : std::runtime_error {
                                   " (" __FILE__ ":" + std::to_string(__LINE__) + ")");      \
     } while (0)
 
+// surface launch-configuration errors at the launch site (works under stream capture)
+#define SPT_LAUNCH_CHECK() HIP_CHECK(hipGetLastError())
+
 __host__ __device__ inline float bf2f(bf16 v) {
     union { uint32_t u; float f; } x;
     x.u = (uint32_t)v << 16;

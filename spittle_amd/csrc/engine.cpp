@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <functional>
 #include <cstdlib>
 #include <sstream>
 #include <stdexcept>
@@ -118,10 +119,17 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     esz_ = dt_ == DT_BF16 ? 2 : 4;
     cp_ = ((dm_.n_mels + 63) / 64) * 64;
     if ((3 * cp_ * esz_) % 128) cp_ = ((dm_.n_mels + 127) / 128) * 128;
+    if (const char* g = getenv("SPT_DECODE_GROUPS")) n_groups_ = std::max(1, std::min(2, atoi(g)));
     select();
     HIP_CHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     ev_.resize(8);
     for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
+    groups_.resize(n_groups_);
+    for (auto& g : groups_) {
+        HIP_CHECK(hipStreamCreateWithFlags(&g.st, hipStreamNonBlocking));
+        HIP_CHECK(hipEventCreateWithFlags(&g.ev, hipEventDisableTiming));
+    }
+    gemv_prepare(dt_);
     alloc_weights();
     generate_weights();
     upload_tables();
@@ -132,7 +140,12 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
 Engine::~Engine() {
     (void)hipSetDevice(dev_);
     if (st_) (void)hipStreamSynchronize(st_);
-    for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
+    for (auto& g : groups_) {
+        if (g.st) (void)hipStreamSynchronize(g.st);
+        for (auto& kv : g.graphs) (void)hipGraphExecDestroy(kv.second);
+        if (g.ev) (void)hipEventDestroy(g.ev);
+        if (g.st) (void)hipStreamDestroy(g.st);
+    }
     if (warena_) (void)hipFree(warena_);
     if (aarena_) (void)hipFree(aarena_);
     for (void* p : {(void*)hann_, (void*)sinv_, (void*)cosv_, (void*)filt_, (void*)grp_})
@@ -347,23 +360,25 @@ void Engine::alloc_workspace() {
         ff_ = A(B * T * 4 * d);
         enc_out_ = A(B * T * d);
         ckv_ = A(L * 2 * B * T * d);
-        skv_ = A(L * 2 * B * ctx * d);
-        dx_ = (float*)c.take(R * d * 4);
-        dq_ = A(R * d);
-        dao_ = A(R * d);
-        dff_ = A(R * 4 * d);
-        part_ = (float*)c.take(B * ((V + 15) / 16) * 16);
-        arrive_ = (unsigned*)c.take(64);
-        logits_ = (float*)c.take(B * V * 4);
-        tok_in_ = (int*)c.take(R * 4);
-        out_tok_ = (int*)c.take(B * ctx * 4);
-        out_t1_ = (float*)c.take(B * ctx * 4);
-        out_t2_ = (float*)c.take(B * ctx * 4);
-        done_ = (int*)c.take(B * 4);
-        forced_ = (int*)c.take(B * ctx * 4);
         suppress_ = (uint32_t*)c.take((V / 32 + 1) * 4);
-        ds_ = (DecState*)c.take(sizeof(DecState));
         scratch_ = (double*)c.take(64);
+        for (DecGroup& g : groups_) {  // each group sized for the whole batch (groups are re-sliced per call)
+            g.dx = (float*)c.take(R * d * 4);
+            g.dq = A(R * d);
+            g.dao = A(R * d);
+            g.dff = A(R * 4 * d);
+            g.skv = A(L * 2 * B * ctx * d);
+            g.logits = (float*)c.take(B * V * 4);
+            g.part = c.take(B * ((V + 15) / 16) * 16);
+            g.arrive = (unsigned*)c.take(64);
+            g.tok_in = (int*)c.take(R * 4);
+            g.out_tok = (int*)c.take(B * ctx * 4);
+            g.out_t1 = (float*)c.take(B * ctx * 4);
+            g.out_t2 = (float*)c.take(B * ctx * 4);
+            g.done = (int*)c.take(B * 4);
+            g.forced = (int*)c.take(B * ctx * 4);
+            g.ds = (DecState*)c.take(sizeof(DecState));
+        }
         if (!pass) {
             abytes_ = c.off;
             if (hipMalloc(&aarena_, abytes_) != hipSuccess) {
@@ -435,60 +450,62 @@ void Engine::run_cross_kv(int B) {
     gemm_nt(dt_, EPI_KVSPLIT, g, 1, st_);
 }
 
-void Engine::enqueue_decoder_pass(int B, int Tq, const DecodeRequest& rq, int out_cap) {
-    const int d = dm_.d, H = dm_.n_head, ctx = dm_.n_text_ctx, T = dm_.n_audio_ctx, R = B * Tq;
-    const int64_t self_layer = (int64_t)2 * B * H * ctx * 64, cross_layer = (int64_t)2 * B * H * T * 64;
-    // dx_ already holds this pass's input embeddings (dec_embed for the prompt pass,
+void Engine::enqueue_decoder_pass(DecGroup& g, int B_total, int Tq, const DecodeRequest& rq, int out_cap) {
+    const int d = dm_.d, H = dm_.n_head, ctx = dm_.n_text_ctx, T = dm_.n_audio_ctx, B = g.B, R = B * Tq;
+    const int64_t self_layer = (int64_t)2 * B * H * ctx * 64, cross_layer = (int64_t)2 * B_total * H * T * 64;
+    hipStream_t st = g.st;
+    // g.dx already holds this pass's input embeddings (dec_embed for the prompt pass,
     // dec_finalize of the previous pass afterwards)
     for (int l = 0; l < dm_.n_dec; ++l) {
         const DecL& e = dec_[l];
-        void* skv_l = (char*)skv_ + self_layer * l * esz_;
-        const void* ckv_l = (const char*)ckv_ + cross_layer * l * esz_;
+        void* skv_l = (char*)g.skv + self_layer * l * esz_;
+        // this group's sequences inside the [2][B_total][H][T][64] cross K/V of layer l
+        const void* ckv_l = (const char*)ckv_ + (cross_layer * l + (int64_t)g.b0 * H * T * 64) * esz_;
         GemvArgs a{};
-        a.A = dx_; a.lda = d; a.ln_w = e.ln1_w; a.ln_b = e.ln1_b; a.R = R;
-        a.W = e.qkv_w; a.N = 3 * d; a.K = d; a.bias = e.qkv_b; a.C = dq_; a.ldc = d;
-        a.cache = skv_l; a.cache_B = B; a.cache_H = H; a.cache_ctx = ctx; a.Tq = Tq; a.st = ds_;
-        gemv(dt_, GV_QKV_CACHE, a, st_);
-        dec_self_attn(dt_, dq_, skv_l, B, H, ctx, Tq, ds_, dao_, st_);
+        a.A = g.dx; a.lda = d; a.ln_w = e.ln1_w; a.ln_b = e.ln1_b; a.R = R;
+        a.W = e.qkv_w; a.N = 3 * d; a.K = d; a.bias = e.qkv_b; a.C = g.dq; a.ldc = d;
+        a.cache = skv_l; a.cache_B = B; a.cache_H = H; a.cache_ctx = ctx; a.Tq = Tq; a.st = g.ds;
+        gemv(dt_, GV_QKV_CACHE, a, st);
+        dec_self_attn(dt_, g.dq, skv_l, B, H, ctx, Tq, g.ds, g.dao, st);
         a = GemvArgs{};
-        a.A = dao_; a.lda = d; a.R = R; a.W = e.so_w; a.N = d; a.K = d; a.bias = e.so_b; a.C = dx_; a.ldc = d;
-        gemv(dt_, GV_BIAS_RESID, a, st_);
+        a.A = g.dao; a.lda = d; a.R = R; a.W = e.so_w; a.N = d; a.K = d; a.bias = e.so_b; a.C = g.dx; a.ldc = d;
+        gemv(dt_, GV_BIAS_RESID, a, st);
         a = GemvArgs{};
-        a.A = dx_; a.lda = d; a.ln_w = e.ln2_w; a.ln_b = e.ln2_b; a.R = R;
-        a.W = e.cq_w; a.N = d; a.K = d; a.bias = e.cq_b; a.C = dq_; a.ldc = d;
-        gemv(dt_, GV_BIAS, a, st_);
-        dec_cross_attn(dt_, dq_, ckv_l, B, H, T, Tq, 1, nullptr, dao_, st_);
+        a.A = g.dx; a.lda = d; a.ln_w = e.ln2_w; a.ln_b = e.ln2_b; a.R = R;
+        a.W = e.cq_w; a.N = d; a.K = d; a.bias = e.cq_b; a.C = g.dq; a.ldc = d;
+        gemv(dt_, GV_BIAS, a, st);
+        dec_cross_attn(dt_, g.dq, ckv_l, B, B_total, H, T, Tq, g.dao, st);
         a = GemvArgs{};
-        a.A = dao_; a.lda = d; a.R = R; a.W = e.co_w; a.N = d; a.K = d; a.bias = e.co_b; a.C = dx_; a.ldc = d;
-        gemv(dt_, GV_BIAS_RESID, a, st_);
+        a.A = g.dao; a.lda = d; a.R = R; a.W = e.co_w; a.N = d; a.K = d; a.bias = e.co_b; a.C = g.dx; a.ldc = d;
+        gemv(dt_, GV_BIAS_RESID, a, st);
         a = GemvArgs{};
-        a.A = dx_; a.lda = d; a.ln_w = e.ln3_w; a.ln_b = e.ln3_b; a.R = R;
-        a.W = e.fc1_w; a.N = 4 * d; a.K = d; a.bias = e.fc1_b; a.C = dff_; a.ldc = 4 * d;
-        gemv(dt_, GV_BIAS_GELU, a, st_);
+        a.A = g.dx; a.lda = d; a.ln_w = e.ln3_w; a.ln_b = e.ln3_b; a.R = R;
+        a.W = e.fc1_w; a.N = 4 * d; a.K = d; a.bias = e.fc1_b; a.C = g.dff; a.ldc = 4 * d;
+        gemv(dt_, GV_BIAS_GELU, a, st);
         a = GemvArgs{};
-        a.A = dff_; a.lda = 4 * d; a.R = R; a.W = e.fc2_w; a.N = d; a.K = 4 * d; a.bias = e.fc2_b; a.C = dx_;
+        a.A = g.dff; a.lda = 4 * d; a.R = R; a.W = e.fc2_w; a.N = d; a.K = 4 * d; a.bias = e.fc2_b; a.C = g.dx;
         a.ldc = d;
-        gemv(dt_, GV_BIAS_RESID, a, st_);
+        gemv(dt_, GV_BIAS_RESID, a, st);
     }
     const Specials sp = specials_for(dm_.n_vocab);
     const int n_tiles = (dm_.n_vocab + 15) / 16;
     GemvArgs a{};
-    a.A = dx_; a.lda = Tq * d; a.a_row0 = (Tq - 1) * d; a.ln_w = lnf_w_; a.ln_b = lnf_b_; a.R = B;
-    a.W = tok_emb_; a.N = dm_.n_vocab; a.K = d; a.C = logits_; a.ldc = dm_.n_vocab; a.st = ds_;
+    a.A = g.dx; a.lda = Tq * d; a.a_row0 = (Tq - 1) * d; a.ln_w = lnf_w_; a.ln_b = lnf_b_; a.R = B;
+    a.W = tok_emb_; a.N = dm_.n_vocab; a.K = d; a.C = g.logits; a.ldc = dm_.n_vocab; a.st = g.ds;
     a.suppress = suppress_;
     a.blank0 = (rq.flags & 1u) ? sp.eot : -1;
     a.blank1 = (rq.flags & 1u) ? 220 : -1;
-    a.part = part_; a.n_tiles = n_tiles;
-    gemv(dt_, GV_LOGITS, a, st_);
+    a.part = g.part; a.n_tiles = n_tiles;
+    gemv(dt_, GV_LOGITS, a, st);
     FinalizeArgs f{};
-    f.part = part_; f.n_tiles = n_tiles;
+    f.part = g.part; f.n_tiles = n_tiles;
     f.eot = sp.eot; f.ignore_eot = (rq.flags & 4u) ? 1 : 0;
-    f.forced = rq.n_forced > 0 ? forced_ : nullptr; f.forced_len = rq.n_forced;
-    f.next_tok = tok_in_; f.out_tok = out_tok_; f.out_top1 = out_t1_; f.out_top2 = out_t2_; f.out_cap = out_cap;
-    f.done = done_;
-    f.emb = tok_emb_; f.pos = dec_pos_; f.d = d; f.ctx = ctx; f.Tq = Tq; f.x = dx_;
-    f.ds = ds_; f.arrive = arrive_;
-    dec_finalize(dt_, f, B, st_);
+    f.forced = rq.n_forced > 0 ? g.forced : nullptr; f.forced_len = rq.n_forced;
+    f.next_tok = g.tok_in; f.out_tok = g.out_tok; f.out_top1 = g.out_t1; f.out_top2 = g.out_t2; f.out_cap = out_cap;
+    f.done = g.done;
+    f.emb = tok_emb_; f.pos = dec_pos_; f.d = d; f.ctx = ctx; f.Tq = Tq; f.x = g.dx;
+    f.ds = g.ds; f.arrive = g.arrive;
+    dec_finalize(dt_, f, B, st);
 }
 
 void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1, float* top2) {
@@ -515,49 +532,82 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         HIP_CHECK(hipStreamSynchronize(st_));
         suppress_flags_ = sflags;
     }
-    std::vector<int> tin((size_t)B * Tq);
-    for (int b = 0; b < B; ++b)
-        for (int t = 0; t < Tq; ++t) tin[(size_t)b * Tq + t] = rq.prompt[t];
-    HIP_CHECK(hipMemcpyAsync(tok_in_, tin.data(), tin.size() * 4, hipMemcpyHostToDevice, st_));
-    if (rq.n_forced > 0)
-        HIP_CHECK(hipMemcpyAsync(forced_, rq.forced, (size_t)B * rq.n_forced * 4, hipMemcpyHostToDevice, st_));
-    HIP_CHECK(hipMemsetAsync(done_, 0, B * 4, st_));
-    HIP_CHECK(hipMemsetAsync(out_tok_, 0xFF, (size_t)B * out_cap * 4, st_));
-    fill_f32(out_t1_, (int64_t)B * out_cap, -INFINITY, st_);
-    fill_f32(out_t2_, (int64_t)B * out_cap, -INFINITY, st_);
-    dec_reset(ds_, arrive_, st_);
-    dec_embed(dt_, tok_in_, B * Tq, Tq, dm_.d, tok_emb_, dec_pos_, ds_, dx_, st_);
-    enqueue_decoder_pass(B, Tq, rq, out_cap);  // prompt pass produces token 0
+    // split the batch over the decode groups; each waits for the encoder / cross-K/V
+    const int G = std::min(n_groups_, B);
+    HIP_CHECK(hipEventRecord(ev_[6], st_));
+    std::vector<DecGroup*> act;
+    static thread_local std::vector<std::vector<int>> tins;  // host sources of async copies outlive the call
+    tins.resize(G);
+    for (int gi = 0, b0 = 0; gi < G; ++gi) {
+        DecGroup& g = groups_[gi];
+        g.b0 = b0;
+        g.B = B / G + (gi < B % G ? 1 : 0);
+        b0 += g.B;
+        act.push_back(&g);
+        HIP_CHECK(hipStreamWaitEvent(g.st, ev_[6], 0));
+        std::vector<int>& tin = tins[gi];
+        tin.resize((size_t)g.B * Tq);
+        for (int b = 0; b < g.B; ++b)
+            for (int t = 0; t < Tq; ++t) tin[(size_t)b * Tq + t] = rq.prompt[t];
+        HIP_CHECK(hipMemcpyAsync(g.tok_in, tin.data(), tin.size() * 4, hipMemcpyHostToDevice, g.st));
+        if (rq.n_forced > 0)
+            HIP_CHECK(hipMemcpyAsync(g.forced, rq.forced + (size_t)g.b0 * rq.n_forced, (size_t)g.B * rq.n_forced * 4,
+                                     hipMemcpyHostToDevice, g.st));
+        HIP_CHECK(hipMemsetAsync(g.done, 0, g.B * 4, g.st));
+        HIP_CHECK(hipMemsetAsync(g.out_tok, 0xFF, (size_t)g.B * out_cap * 4, g.st));
+        fill_f32(g.out_t1, (int64_t)g.B * out_cap, -INFINITY, g.st);
+        fill_f32(g.out_t2, (int64_t)g.B * out_cap, -INFINITY, g.st);
+        dec_reset(g.ds, g.arrive, g.st);
+        dec_embed(dt_, g.tok_in, g.B * Tq, Tq, dm_.d, tok_emb_, dec_pos_, g.ds, g.dx, g.st);
+        enqueue_decoder_pass(g, B, Tq, rq, out_cap);  // prompt pass produces token 0
+    }
     int passes = 1;
-    if (rq.n_steps > 1) {
-        const GraphKey key{B, out_cap, rq.n_forced, rq.flags};
-        auto it = graphs_.find(key);
-        if (it == graphs_.end()) {
-            hipGraph_t graph;
-            HIP_CHECK(hipStreamBeginCapture(st_, hipStreamCaptureModeThreadLocal));
-            enqueue_decoder_pass(B, 1, rq, out_cap);
-            HIP_CHECK(hipStreamEndCapture(st_, &graph));
-            hipGraphExec_t exec;
-            HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
-            HIP_CHECK(hipGraphDestroy(graph));
-            it = graphs_.emplace(key, exec).first;
+    static const bool no_graph = getenv("SPT_NO_GRAPH") != nullptr;  // eager passes (profilers, debugging)
+    if (rq.n_steps > 1 && no_graph) {
+        for (int s = 1; s < rq.n_steps; ++s, ++passes)
+            for (DecGroup* g : act) enqueue_decoder_pass(*g, B, 1, rq, out_cap);
+    } else if (rq.n_steps > 1) {
+        std::vector<hipGraphExec_t> ex;
+        for (DecGroup* g : act) {
+            const GraphKey key{g->B, out_cap, rq.n_forced, rq.flags};
+            auto it = g->graphs.find(key);
+            if (it == g->graphs.end()) {
+                hipGraph_t graph;
+                HIP_CHECK(hipStreamBeginCapture(g->st, hipStreamCaptureModeThreadLocal));
+                enqueue_decoder_pass(*g, B, 1, rq, out_cap);
+                HIP_CHECK(hipStreamEndCapture(g->st, &graph));
+                hipGraphExec_t exec;
+                HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+                HIP_CHECK(hipGraphDestroy(graph));
+                it = g->graphs.emplace(key, exec).first;
+            }
+            ex.push_back(it->second);
         }
         const bool early_exit = !(rq.flags & 4u);
         std::vector<int> hdone(B);
         for (int s = 1; s < rq.n_steps; ++s) {
-            HIP_CHECK(hipGraphLaunch(it->second, st_));
+            for (size_t i = 0; i < act.size(); ++i) HIP_CHECK(hipGraphLaunch(ex[i], act[i]->st));
             ++passes;
             if (early_exit && (s % 16) == 0) {
-                HIP_CHECK(hipMemcpyAsync(hdone.data(), done_, B * 4, hipMemcpyDeviceToHost, st_));
-                HIP_CHECK(hipStreamSynchronize(st_));
-                if (std::all_of(hdone.begin(), hdone.end(), [](int v) { return v != 0; })) break;
+                bool all = true;
+                for (DecGroup* g : act) {
+                    HIP_CHECK(hipMemcpyAsync(hdone.data(), g->done, g->B * 4, hipMemcpyDeviceToHost, g->st));
+                    HIP_CHECK(hipStreamSynchronize(g->st));
+                    all = all && std::all_of(hdone.begin(), hdone.begin() + g->B, [](int v) { return v != 0; });
+                }
+                if (all) break;
             }
         }
     }
     tm_.n_decode_passes = passes;
-    HIP_CHECK(hipMemcpyAsync(tokens, out_tok_, (size_t)B * out_cap * 4, hipMemcpyDeviceToHost, st_));
-    if (top1) HIP_CHECK(hipMemcpyAsync(top1, out_t1_, (size_t)B * out_cap * 4, hipMemcpyDeviceToHost, st_));
-    if (top2) HIP_CHECK(hipMemcpyAsync(top2, out_t2_, (size_t)B * out_cap * 4, hipMemcpyDeviceToHost, st_));
+    for (DecGroup* g : act) {
+        const size_t off = (size_t)g->b0 * out_cap, n = (size_t)g->B * out_cap * 4;
+        HIP_CHECK(hipMemcpyAsync(tokens + off, g->out_tok, n, hipMemcpyDeviceToHost, g->st));
+        if (top1) HIP_CHECK(hipMemcpyAsync(top1 + off, g->out_t1, n, hipMemcpyDeviceToHost, g->st));
+        if (top2) HIP_CHECK(hipMemcpyAsync(top2 + off, g->out_t2, n, hipMemcpyDeviceToHost, g->st));
+        HIP_CHECK(hipEventRecord(g->ev, g->st));
+        HIP_CHECK(hipStreamWaitEvent(st_, g->ev, 0));
+    }
 }
 
 void Engine::transcribe_device(const float* pcm_dev, int64_t stride, const int* n_samples, int B,
@@ -658,6 +708,86 @@ bool Engine::debug_weight_checksum(int tid, double* out2) {
     HIP_CHECK(hipMemcpyAsync(out2, scratch_, 16, hipMemcpyDeviceToHost, st_));
     HIP_CHECK(hipStreamSynchronize(st_));
     return true;
+}
+
+}  // namespace spt
+
+namespace spt {
+
+double Engine::probe(int kind, int iters, double* work, int* is_flops) {
+    select();
+    const int B = tm_.batch;
+    if (B < 1) throw std::runtime_error("probe needs a completed transcription call first");
+    if (iters < 1 || iters > 100000) throw std::runtime_error("iters out of range");
+    const int d = dm_.d, H = dm_.n_head, T = dm_.n_audio_ctx, ctx = dm_.n_text_ctx, V = dm_.n_vocab;
+    DecGroup& g = groups_[0];
+    const int Bg = g.B > 0 ? g.B : B;
+    std::function<void()> launch;
+    *is_flops = 0;
+    switch (kind) {
+        case 0:  // cross-attention of decoder layer 0 over this group's cross K/V
+            launch = [&] { dec_cross_attn(dt_, g.dq, ckv_, Bg, B, H, T, 1, g.dao, st_); };
+            *work = 2.0 * Bg * H * T * 64 * esz_;
+            break;
+        case 1:
+            launch = [&] { dec_self_attn(dt_, g.dq, g.skv, Bg, H, ctx, 1, g.ds, g.dao, st_); };
+            {
+                DecState h{};
+                HIP_CHECK(hipMemcpy(&h, g.ds, sizeof(h), hipMemcpyDeviceToHost));
+                *work = 2.0 * Bg * H * (h.pos0 + 1) * 64 * esz_;
+            }
+            break;
+        case 2: {
+            launch = [&] {
+                GemvArgs a{};
+                a.A = g.dx; a.lda = d; a.ln_w = lnf_w_; a.ln_b = lnf_b_; a.R = Bg;
+                a.W = tok_emb_; a.N = V; a.K = d; a.C = g.logits; a.ldc = V; a.st = g.ds;
+                a.suppress = suppress_; a.blank0 = a.blank1 = -1; a.part = g.part; a.n_tiles = (V + 15) / 16;
+                gemv(dt_, GV_LOGITS, a, st_);
+            };
+            *work = (double)V * d * esz_;
+            break;
+        }
+        case 3: {
+            launch = [&] {
+                GemvArgs a{};
+                a.A = g.dx; a.lda = d; a.ln_w = dec_[0].ln3_w; a.ln_b = dec_[0].ln3_b; a.R = Bg;
+                a.W = dec_[0].fc1_w; a.N = 4 * d; a.K = d; a.bias = dec_[0].fc1_b; a.C = g.dff; a.ldc = 4 * d;
+                gemv(dt_, GV_BIAS_GELU, a, st_);
+            };
+            *work = 4.0 * d * d * esz_;
+            break;
+        }
+        case 4: {
+            launch = [&] {
+                GemmArgs a{};
+                a.A = xn_; a.lda = d; a.W = enc_[0].fc1_w; a.ldw = d; a.M = B * T; a.N = 4 * d; a.K = d;
+                a.bias = enc_[0].fc1_b; a.C = ff_; a.ldc = 4 * d;
+                gemm_nt(dt_, EPI_BIAS_GELU, a, 1, st_);
+            };
+            *work = 2.0 * B * T * 4.0 * d * d;
+            *is_flops = 1;
+            break;
+        }
+        case 5:
+            launch = [&] { enc_attention(dt_, qkv_, B, T, H, ao_, st_); };
+            *work = 4.0 * B * H * (double)T * T * 64;
+            *is_flops = 1;
+            break;
+        default:
+            throw std::runtime_error("unknown probe kind");
+    }
+    if (n_groups_ > 1 || dm_.n_enc < 1) {
+        if (kind >= 4 && dm_.n_enc < 1) throw std::runtime_error("model has no encoder layers");
+    }
+    launch();  // warm
+    HIP_CHECK(hipEventRecord(ev_[0], st_));
+    for (int i = 0; i < iters; ++i) launch();
+    HIP_CHECK(hipEventRecord(ev_[1], st_));
+    HIP_CHECK(hipEventSynchronize(ev_[1]));
+    float ms;
+    HIP_CHECK(hipEventElapsedTime(&ms, ev_[0], ev_[1]));
+    return ms * 1000.0 / iters;
 }
 
 }  // namespace spt

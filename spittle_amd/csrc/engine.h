@@ -62,8 +62,38 @@ public:
     void debug_mel(const float* pcm_host, int n, float* out_host);
     void debug_encode(const float* mel_host, float* out_host);
     bool debug_weight_checksum(int tid, double* out2);
+    // re-launch one hot-path kernel on the last call's buffers; returns avg us per launch
+    double probe(int kind, int iters, double* work, int* is_flops);
 
 private:
+    struct GraphKey {
+        int B, out_cap, n_forced;
+        uint32_t flags;
+        bool operator<(const GraphKey& o) const {
+            if (B != o.B) return B < o.B;
+            if (out_cap != o.out_cap) return out_cap < o.out_cap;
+            if (n_forced != o.n_forced) return n_forced < o.n_forced;
+            return flags < o.flags;
+        }
+    };
+    // An independent slice of the batch decoded on its own stream: its kernels fill
+    // the launch gaps of the other group's latency-bound decoder chain.
+    struct DecGroup {
+        hipStream_t st = nullptr;
+        hipEvent_t ev = nullptr;
+        int b0 = 0, B = 0;
+        float* dx = nullptr;
+        void *dq = nullptr, *dao = nullptr, *dff = nullptr;
+        void* skv = nullptr;          // self K/V [L][2][B][H][ctx][64]
+        float* logits = nullptr;
+        void* part = nullptr;         // logits top-2 partials [B][V/16]
+        unsigned* arrive = nullptr;
+        int *tok_in = nullptr, *out_tok = nullptr, *done = nullptr, *forced = nullptr;
+        float *out_t1 = nullptr, *out_t2 = nullptr;
+        DecState* ds = nullptr;
+        std::map<GraphKey, hipGraphExec_t> graphs;
+    };
+
     void select() const;
     void alloc_weights();
     void generate_weights();
@@ -74,13 +104,14 @@ private:
     void run_encoder(int B);
     void run_cross_kv(int B);
     void run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1, float* top2);
-    void enqueue_decoder_pass(int B, int Tq, const DecodeRequest& rq, int out_cap);
+    void enqueue_decoder_pass(DecGroup& g, int B_total, int Tq, const DecodeRequest& rq, int out_cap);
 
     ModelDims dm_;
     int dt_, dev_, max_batch_;
     uint64_t seed_;
     int esz_;     // bytes per weight / activation element
     int cp_;      // padded mel channels (conv1 K = 3 * cp_)
+    int n_groups_ = 1;  // SPT_DECODE_GROUPS=2 splits the batch over two streams
     hipStream_t st_ = nullptr;
     std::vector<hipEvent_t> ev_;
 
@@ -115,31 +146,10 @@ private:
     float* x_ = nullptr;
     void *xn_ = nullptr, *qkv_ = nullptr, *ao_ = nullptr, *ff_ = nullptr, *enc_out_ = nullptr;
     void* ckv_ = nullptr;   // cross K/V [L][2][B][H][1500][64]
-    void* skv_ = nullptr;   // self K/V  [L][2][B][H][ctx][64]
-    float* dx_ = nullptr;
-    void *dq_ = nullptr, *dao_ = nullptr, *dff_ = nullptr;
-    float* part_ = nullptr;     // logits top-2 partials [B][V/16]
-    unsigned* arrive_ = nullptr;
-    float* logits_ = nullptr;
-    int *tok_in_ = nullptr, *out_tok_ = nullptr, *done_ = nullptr, *forced_ = nullptr;
-    float *out_t1_ = nullptr, *out_t2_ = nullptr;
     uint32_t* suppress_ = nullptr;
-    DecState* ds_ = nullptr;
     double* scratch_ = nullptr;
-    int n_split_ = 4;
+    std::vector<DecGroup> groups_;
 
-    // ---- graphs (generation step, keyed by batch / decode configuration)
-    struct GraphKey {
-        int B, out_cap, n_forced;
-        uint32_t flags;
-        bool operator<(const GraphKey& o) const {
-            if (B != o.B) return B < o.B;
-            if (out_cap != o.out_cap) return out_cap < o.out_cap;
-            if (n_forced != o.n_forced) return n_forced < o.n_forced;
-            return flags < o.flags;
-        }
-    };
-    std::map<GraphKey, hipGraphExec_t> graphs_;
     std::vector<uint32_t> host_suppress_;
     uint32_t suppress_flags_ = ~0u;
 

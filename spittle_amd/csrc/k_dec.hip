@@ -71,13 +71,12 @@ __device__ __forceinline__ TopP top_shfl(TopP t, int mask) {
 
 // NWV waves; CT column tiles of 16 per workgroup; KSPLIT = NWV / CT waves share a tile
 // and split its K.  Each wave keeps up to MAXJ super-steps of weights in flight.
-template <typename T, int MODE, bool LN, int RG, int NWV, int CT>
+template <typename T, int MODE, bool LN, int RG, int NWV, int CT, int MAXJ>
 __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
     constexpr int KS = GV<T>::KS;
     constexpr int EPL = KS / 4;          // elements per lane per super-step (64 bytes)
     constexpr int CPE = 16 / sizeof(T);  // elements per 16-byte chunk
     constexpr int KSPLIT = NWV / CT;
-    constexpr int MAXJ = 4;
     typedef typename GV<T>::frag frag;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -227,7 +226,7 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
                 t = top_merge(t, top_shfl(t, 2));
                 t = top_merge(t, top_shfl(t, 4));
                 t = top_merge(t, top_shfl(t, 8));
-                if (fr == 0 && row < a.R) ((TopP*)a.part)[(size_t)row * a.n_tiles + tile] = t;
+                if (fr == 0 && row < a.R && tile < a.n_tiles) ((TopP*)a.part)[(size_t)row * a.n_tiles + tile] = t;
             }
         }
         return;
@@ -265,26 +264,57 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
     }
 }
 
-template <typename T, int MODE, bool LN, int RG, int NWV, int CT>
+template <typename T, int MODE, bool LN, int RG, int NWV, int CT, int MAXJ>
+void gemv_attr() {
+    const int red = NWV * RG * 64 * (int)sizeof(f32x4);
+    HIP_CHECK(hipFuncSetAttribute((const void*)gemv_kernel<T, MODE, LN, RG, NWV, CT, MAXJ>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, GV_LDS_BYTES + red));
+}
+
+template <typename T, int MODE, bool LN, int RG, int NWV, int CT, int MAXJ>
 void gemv_launch_cfg(const GemvArgs& a, hipStream_t st) {
     const int red = NWV * RG * 64 * (int)sizeof(f32x4);
     const int lds = (LN ? gv_img_bytes(a.R, a.K, sizeof(T)) : 0) + (NWV / CT > 1 ? red : 0);
-    static bool attr_set = false;  // allow > 64 KiB of dynamic LDS (one-time, per instantiation)
-    if (!attr_set) {
-        HIP_CHECK(hipFuncSetAttribute((const void*)gemv_kernel<T, MODE, LN, RG, NWV, CT>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, GV_LDS_BYTES + red));
-        attr_set = true;
-    }
-    hipLaunchKernelGGL((gemv_kernel<T, MODE, LN, RG, NWV, CT>), dim3(cdiv(a.N, 16 * CT)), dim3(64 * NWV), lds, st,
-                       a);
+    hipLaunchKernelGGL((gemv_kernel<T, MODE, LN, RG, NWV, CT, MAXJ>), dim3(cdiv(a.N, 16 * CT)), dim3(64 * NWV), lds,
+                       st, a);
+    SPT_LAUNCH_CHECK();
+}
+
+// geometry per shape (nss = super-steps of K): every wave's whole K slice in flight
+// at once where registers allow, and at most one workgroup round on 256 CUs
+#define SPT_GV_CONFIGS(X)   \
+    X(4, 4, 4)  /* logits: 4 column tiles x 1 wave each */ \
+    X(8, 1, 1)  /* nss <= 8  */ \
+    X(8, 1, 2)  /* nss <= 16 */ \
+    X(16, 1, 3) /* nss <= 48 */
+
+// > 64 KiB of dynamic LDS must be enabled per kernel, outside any stream capture
+template <typename T, int MODE, bool LN>
+void gemv_attr_all() {
+#define SPT_ATTR(NWV, CT, MAXJ)                        \
+    gemv_attr<T, MODE, LN, 1, NWV, CT, MAXJ>();         \
+    gemv_attr<T, MODE, LN, 2, NWV, CT, MAXJ>();         \
+    gemv_attr<T, MODE, LN, 4, NWV, CT, MAXJ>();
+    SPT_GV_CONFIGS(SPT_ATTR)
+#undef SPT_ATTR
+}
+template <typename T>
+void gemv_attr_modes() {
+    gemv_attr_all<T, GV_BIAS, true>(); gemv_attr_all<T, GV_BIAS, false>();
+    gemv_attr_all<T, GV_BIAS_GELU, true>(); gemv_attr_all<T, GV_BIAS_GELU, false>();
+    gemv_attr_all<T, GV_BIAS_RESID, true>(); gemv_attr_all<T, GV_BIAS_RESID, false>();
+    gemv_attr_all<T, GV_QKV_CACHE, true>(); gemv_attr_all<T, GV_QKV_CACHE, false>();
+    gemv_attr_all<T, GV_LOGITS, true>(); gemv_attr_all<T, GV_LOGITS, false>();
 }
 
 template <typename T, int MODE, bool LN, int RG>
 void gemv_launch_rg(const GemvArgs& a, hipStream_t st) {
-    // wide weight streams (logits): 64 columns x 8 waves per workgroup; the rest:
-    // 16 columns x 8 waves, each wave holding up to 4 super-steps of its K slice in flight
-    if (a.N >= 16384) gemv_launch_cfg<T, MODE, LN, RG, 8, 4>(a, st);
-    else gemv_launch_cfg<T, MODE, LN, RG, 8, 1>(a, st);
+    const int nss = a.K / GV<T>::KS;
+    if (a.N >= 16384) gemv_launch_cfg<T, MODE, LN, RG, 4, 4, 4>(a, st);
+    else if (nss <= 8) gemv_launch_cfg<T, MODE, LN, RG, 8, 1, 1>(a, st);
+    else if (nss <= 16) gemv_launch_cfg<T, MODE, LN, RG, 8, 1, 2>(a, st);
+    else if (nss <= 48) gemv_launch_cfg<T, MODE, LN, RG, 16, 1, 3>(a, st);
+    else throw std::runtime_error("gemv: K too large");
 }
 
 template <typename T, int MODE>
@@ -321,11 +351,13 @@ template <> struct KVChunk<float> {
 };
 
 // q rows: q + (b*Tq + t)*q_ld + h*64; K/V rows of (b, h): base + ((kv*B + b)*H + h)*ctx*64
-template <typename T, int NQ>
+// CAUSAL: self-attention over the cache (keys 0..pos0+t); else cross-attention (all keys)
+template <typename T, int NQ, bool CAUSAL>
 __global__ __launch_bounds__(64 * AW) void dec_attn_kernel(const T* __restrict__ q, int q_ld,
                                                            const T* __restrict__ kv, int B, int H, int ctx,
-                                                           int n_keys_static, int causal, int Tq,
+                                                           int n_keys_static, int Tq,
                                                            const DecState* __restrict__ ds, T* __restrict__ out) {
+    constexpr bool causal = CAUSAL;
     __shared__ float s_m[AW][NQ], s_l[AW][NQ];
     __shared__ float s_o[AW][NQ][64];
     const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
@@ -458,14 +490,25 @@ __global__ __launch_bounds__(64 * AW) void dec_attn_kernel(const T* __restrict__
 }
 
 template <typename T>
-void dec_attn_launch(const T* q, const T* kv, int B, int H, int ctx, int n_keys, int causal, int Tq,
+void dec_attn_launch(const T* q, const T* kv, int nseq, int B_layout, int H, int ctx, int n_keys, int causal, int Tq,
                      const DecState* ds, T* out, hipStream_t st) {
-    if (Tq == 1)
-        hipLaunchKernelGGL((dec_attn_kernel<T, 1>), dim3(B * H), dim3(64 * AW), 0, st, q, H * 64, kv, B, H, ctx, n_keys,
-                           causal, Tq, ds, out);
-    else
-        hipLaunchKernelGGL((dec_attn_kernel<T, 4>), dim3(B * H), dim3(64 * AW), 0, st, q, H * 64, kv, B, H, ctx, n_keys,
-                           causal, Tq, ds, out);
+    const dim3 grid(nseq * H), blk(64 * AW);
+    if (causal) {
+        if (Tq == 1)
+            hipLaunchKernelGGL((dec_attn_kernel<T, 1, true>), grid, blk, 0, st, q, H * 64, kv, B_layout, H, ctx, n_keys,
+                               Tq, ds, out);
+        else
+            hipLaunchKernelGGL((dec_attn_kernel<T, 4, true>), grid, blk, 0, st, q, H * 64, kv, B_layout, H, ctx, n_keys,
+                               Tq, ds, out);
+    } else {
+        if (Tq == 1)
+            hipLaunchKernelGGL((dec_attn_kernel<T, 1, false>), grid, blk, 0, st, q, H * 64, kv, B_layout, H, ctx, n_keys,
+                               Tq, ds, out);
+        else
+            hipLaunchKernelGGL((dec_attn_kernel<T, 4, false>), grid, blk, 0, st, q, H * 64, kv, B_layout, H, ctx, n_keys,
+                               Tq, ds, out);
+    }
+    SPT_LAUNCH_CHECK();
 }
 
 // ------------------------------------------------------------------ finalize
@@ -530,6 +573,11 @@ __global__ void reset_kernel(DecState* ds, unsigned* arrive) {
 
 }  // namespace
 
+void gemv_prepare(int dtype) {
+    if (dtype == DT_BF16) gemv_attr_modes<bf16>();
+    else gemv_attr_modes<float>();
+}
+
 void gemv(int dtype, int mode, const GemvArgs& a, hipStream_t st) {
     if (a.R > 64 || a.R <= 0) throw std::runtime_error("gemv: rows must be in 1..64");
     if (a.K % (dtype == DT_BF16 ? 128 : 64)) throw std::runtime_error("gemv: K alignment");
@@ -558,20 +606,20 @@ void dec_self_attn(int dtype, const void* q, const void* cache, int B, int H, in
                    void* out, hipStream_t st) {
     if (Tq < 1 || Tq > 4) throw std::runtime_error("dec_self_attn: 1..4 queries per sequence");
     if (dtype == DT_BF16)
-        dec_attn_launch<bf16>((const bf16*)q, (const bf16*)cache, B, H, ctx, 0, 1, Tq, ds, (bf16*)out, st);
+        dec_attn_launch<bf16>((const bf16*)q, (const bf16*)cache, B, B, H, ctx, 0, 1, Tq, ds, (bf16*)out, st);
     else
-        dec_attn_launch<float>((const float*)q, (const float*)cache, B, H, ctx, 0, 1, Tq, ds, (float*)out, st);
+        dec_attn_launch<float>((const float*)q, (const float*)cache, B, B, H, ctx, 0, 1, Tq, ds, (float*)out, st);
 }
 
-void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int H, int T_enc, int Tq, int n_split, float* part,
-                    void* out, hipStream_t st) {
-    (void)n_split;
-    (void)part;
+void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int B_layout, int H, int T_enc, int Tq, void* out,
+                    hipStream_t st) {
     if (Tq < 1 || Tq > 4) throw std::runtime_error("dec_cross_attn: 1..4 queries per sequence");
     if (dtype == DT_BF16)
-        dec_attn_launch<bf16>((const bf16*)q, (const bf16*)kv, B, H, T_enc, T_enc, 0, Tq, nullptr, (bf16*)out, st);
+        dec_attn_launch<bf16>((const bf16*)q, (const bf16*)kv, B, B_layout, H, T_enc, T_enc, 0, Tq, nullptr, (bf16*)out,
+                              st);
     else
-        dec_attn_launch<float>((const float*)q, (const float*)kv, B, H, T_enc, T_enc, 0, Tq, nullptr, (float*)out, st);
+        dec_attn_launch<float>((const float*)q, (const float*)kv, B, B_layout, H, T_enc, T_enc, 0, Tq, nullptr,
+                               (float*)out, st);
 }
 
 void dec_finalize(int dtype, const FinalizeArgs& a, int B, hipStream_t st) {

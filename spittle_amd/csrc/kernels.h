@@ -83,6 +83,8 @@ struct GemvArgs {
     void* part; int n_tiles;
 };
 void gemv(int dtype, int mode, const GemvArgs& a, hipStream_t st);
+// one-time per-process kernel attributes (call before any stream capture)
+void gemv_prepare(int dtype);
 
 // x[b*Tq + t] = tok_emb[tok[b*Tq+t]] + pos_emb[pos0 + t]
 void dec_embed(int dtype, const int* tok, int R, int Tq, int d, const void* tok_emb,
@@ -91,8 +93,9 @@ void dec_embed(int dtype, const int* tok, int R, int Tq, int d, const void* tok_
 void dec_self_attn(int dtype, const void* q, const void* cache, int B, int H, int ctx, int Tq,
                    const DecState* ds, void* out, hipStream_t st);
 // cross attention over T_enc keys, split over key chunks; partials then combine
-void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int H, int T_enc, int Tq,
-                    int n_split, float* part, void* out, hipStream_t st);
+// kv: [2][B_layout][H][T_enc][64] (already offset to the first of the B sequences)
+void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int B_layout, int H, int T_enc, int Tq,
+                    void* out, hipStream_t st);
 
 struct FinalizeArgs {
     const void* part; int n_tiles;        // logits top-2 partials [B][n_tiles]

@@ -216,6 +216,14 @@ class WhisperEngine:
                                                out.ctypes.data_as(C.POINTER(C.c_float))))
         return out
 
+    def probe(self, kernel: str, iters: int = 50) -> dict:
+        """Time one hot-path kernel (HIP events, engine stream) on the last call's buffers."""
+        self._need()
+        us, work, fl = C.c_double(), C.c_double(), C.c_int32()
+        self._check(self._lib.spt_probe_kernel(self._ctx, L.PROBES[kernel], int(iters), C.byref(us), C.byref(work),
+                                               C.byref(fl)))
+        return {"avg_us": us.value, "work": work.value, "work_is_flops": bool(fl.value)}
+
     def weight_checksum(self, tensor_id: int):
         self._need()
         o = (C.c_double * 2)()
