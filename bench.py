@@ -131,11 +131,13 @@ def main():
     dev = torch.device("cuda", local)
 
     from spittle_amd import WhisperEngine, WhisperInferenceParams, WhisperModelParams
+    from spittle_amd.dist import max_over_ranks, shard_range
     from spittle_amd.synth import synth_audio
 
     B = args.batch
-    # this rank's shard of the global utterance list
-    pcm = np.stack([synth_audio(rank * B + i) for i in range(B)])
+    # this rank's shard of the global utterance list (B per GPU: weak scaling)
+    lo, hi = shard_range(world * B, world, rank)
+    pcm = np.stack([synth_audio(i) for i in range(lo, hi)])
     pcm_dev = torch.from_numpy(pcm).to(dev)
     torch.cuda.synchronize()
 
@@ -162,10 +164,7 @@ def main():
         res = step()
     barrier()
     dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = max_over_ranks(dt, device=dev)
     assert all(len(r.tokens) == args.decode_steps for r in res)
     phases = eng.timings()
 
