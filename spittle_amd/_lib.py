@@ -25,7 +25,7 @@ EXPORTS = [
     "spt_debug_encode", "spt_debug_weight_checksum", "spt_probe_kernel",
 ]
 PROBES = {"dec_cross_attn": 0, "dec_self_attn": 1, "dec_logits": 2, "dec_fc1": 3, "enc_fc1_gemm": 4,
-          "enc_attn": 5}
+          "enc_attn": 5, "dec_pass": 6}
 
 
 class ModelParams(C.Structure):
@@ -63,9 +63,12 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise ImportError(f"spittle_amd: HIP library not built: {LIB_PATH} (run `make -C spittle_amd/csrc`)")
-    L = C.CDLL(LIB_PATH)
+    path = LIB_PATH
+    if os.environ.get("SPT_DEBUG_LIB"):  # bounds-checked developer build (make -C spittle_amd/csrc dbg)
+        path = os.path.join(os.path.dirname(LIB_PATH), "libspittle_hip_dbg.so")
+    if not os.path.exists(path):
+        raise ImportError(f"spittle_amd: HIP library not built: {path} (run `make -C spittle_amd/csrc`)")
+    L = C.CDLL(path)
     vp, fp = C.c_void_p, C.POINTER(C.c_float)
     L.spt_version.restype = C.c_char_p
     L.spt_default_model_params.argtypes = [C.POINTER(ModelParams)]

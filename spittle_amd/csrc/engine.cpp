@@ -9,6 +9,8 @@
 // protocol of BASELINE.md.
 #include "engine.h"
 
+#include <cstdio>
+
 #include <math.h>
 #include <string.h>
 
@@ -134,7 +136,42 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     generate_weights();
     upload_tables();
     alloc_workspace();
+    setup_persist();
     HIP_CHECK(hipStreamSynchronize(st_));
+}
+
+// The persistent pass needs every workgroup co-resident (one per CU); it is used only
+// where its shape checks pass and a single decode stream owns the device. EXPERIMENTAL:
+// opt-in with SPT_PERSIST=1 (an unexplained device fault in long runs is under study).
+void Engine::setup_persist() {
+    const char* env = getenv("SPT_PERSIST");
+    if (dt_ != DT_BF16 || n_groups_ != 1 || !env || env[0] != '1') return;
+    hipDeviceProp_t prop;
+    HIP_CHECK(hipGetDeviceProperties(&prop, dev_));
+    n_cu_ = prop.multiProcessorCount;
+    if (n_cu_ < 1 || n_cu_ > 1024) return;
+    // key splits depend on the device and model only, never on the batch (batch invariance)
+    s_cross_ = std::max(1, std::min(64, n_cu_ * 8 / (8 * dm_.n_head)));
+    s_self_ = 8;
+    std::vector<PersistLayer> pl(dm_.n_dec);
+    for (int l = 0; l < dm_.n_dec; ++l) {
+        const DecL& e = dec_[l];
+        PersistLayer& q = pl[l];
+        q.qkv_w = (const uint16_t*)e.qkv_w; q.so_w = (const uint16_t*)e.so_w; q.cq_w = (const uint16_t*)e.cq_w;
+        q.co_w = (const uint16_t*)e.co_w; q.fc1_w = (const uint16_t*)e.fc1_w; q.fc2_w = (const uint16_t*)e.fc2_w;
+        q.qkv_b = e.qkv_b; q.so_b = e.so_b; q.cq_b = e.cq_b; q.co_b = e.co_b; q.fc1_b = e.fc1_b; q.fc2_b = e.fc2_b;
+        q.ln1_w = e.ln1_w; q.ln1_b = e.ln1_b; q.ln2_w = e.ln2_w; q.ln2_b = e.ln2_b; q.ln3_w = e.ln3_w; q.ln3_b = e.ln3_b;
+    }
+    HIP_CHECK(hipMemcpy(players_, pl.data(), pl.size() * sizeof(PersistLayer), hipMemcpyHostToDevice));
+    persist_prepare();
+    persist_ = true;
+}
+
+bool Engine::persist_ok(int B, int Tq) const {
+    if (!persist_ || Tq != 1) return false;
+    PersistArgs a{};
+    a.B = B; a.d = dm_.d; a.H = dm_.n_head; a.S_self = s_self_; a.S_cross = s_cross_;
+    return persist_check(a, n_cu_) == nullptr;
 }
 
 Engine::~Engine() {
@@ -378,7 +415,13 @@ void Engine::alloc_workspace() {
             g.done = (int*)c.take(B * 4);
             g.forced = (int*)c.take(B * ctx * 4);
             g.ds = (DecState*)c.take(sizeof(DecState));
+            g.xpart = (float*)c.take(B * H * 64 * 66 * 4);
+            g.xcnt = (unsigned*)c.take(2 * B * H * 4);
+            g.flags = (unsigned*)c.take(1024 * 4);
+            g.abort_flag = (unsigned*)c.take(64);
+            g.pargs = (PersistArgs*)c.take(sizeof(PersistArgs));
         }
+        players_ = (PersistLayer*)c.take(L * sizeof(PersistLayer));
         if (!pass) {
             abytes_ = c.off;
             if (hipMalloc(&aarena_, abytes_) != hipSuccess) {
@@ -456,7 +499,9 @@ void Engine::enqueue_decoder_pass(DecGroup& g, int B_total, int Tq, const Decode
     hipStream_t st = g.st;
     // g.dx already holds this pass's input embeddings (dec_embed for the prompt pass,
     // dec_finalize of the previous pass afterwards)
-    for (int l = 0; l < dm_.n_dec; ++l) {
+    const bool persist = Tq == 1 && persist_ok(B, 1);
+    if (persist) dec_persist(g.hargs, g.pargs, n_cu_, st);  // every layer in one launch
+    for (int l = 0; l < (persist ? 0 : dm_.n_dec); ++l) {
         const DecL& e = dec_[l];
         void* skv_l = (char*)g.skv + self_layer * l * esz_;
         // this group's sequences inside the [2][B_total][H][T][64] cross K/V of layer l
@@ -499,7 +544,7 @@ void Engine::enqueue_decoder_pass(DecGroup& g, int B_total, int Tq, const Decode
     gemv(dt_, GV_LOGITS, a, st);
     FinalizeArgs f{};
     f.part = g.part; f.n_tiles = n_tiles;
-    f.eot = sp.eot; f.ignore_eot = (rq.flags & 4u) ? 1 : 0;
+    f.eot = sp.eot; f.ignore_eot = (rq.flags & 4u) ? 1 : 0; f.n_vocab = dm_.n_vocab;
     f.forced = rq.n_forced > 0 ? g.forced : nullptr; f.forced_len = rq.n_forced;
     f.next_tok = g.tok_in; f.out_tok = g.out_tok; f.out_top1 = g.out_t1; f.out_top2 = g.out_t2; f.out_cap = out_cap;
     f.done = g.done;
@@ -558,14 +603,44 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         fill_f32(g.out_t1, (int64_t)g.B * out_cap, -INFINITY, g.st);
         fill_f32(g.out_t2, (int64_t)g.B * out_cap, -INFINITY, g.st);
         dec_reset(g.ds, g.arrive, g.st);
+        if (persist_ok(g.B, 1)) {  // arguments of this call's persistent passes
+            const int d = dm_.d, H = dm_.n_head, ctx = dm_.n_text_ctx, T = dm_.n_audio_ctx;
+            PersistArgs& pa = g.hargs;
+            pa = PersistArgs{};
+            pa.layers = players_; pa.n_layers = dm_.n_dec;
+            pa.B = g.B; pa.d = d; pa.H = H; pa.ctx = ctx; pa.T_enc = T; pa.B_layout = B;
+            pa.S_self = s_self_; pa.S_cross = s_cross_;
+            pa.x = g.dx; pa.q = (uint16_t*)g.dq; pa.ao = (uint16_t*)g.dao; pa.ff = (uint16_t*)g.dff;
+            pa.skv = (uint16_t*)g.skv; pa.self_layer = (int64_t)2 * g.B * H * ctx * 64;
+            pa.ckv = (const uint16_t*)ckv_ + (int64_t)g.b0 * H * T * 64; pa.cross_layer = (int64_t)2 * B * H * T * 64;
+            pa.xpart = g.xpart; pa.xcnt = g.xcnt; pa.flags = g.flags; pa.abort_flag = g.abort_flag; pa.ds = g.ds;
+            pa.ws_lo = aarena_; pa.ws_hi = aarena_ + abytes_; pa.wt_lo = warena_; pa.wt_hi = warena_ + wbytes_;
+            HIP_CHECK(hipMemcpyAsync(g.pargs, &pa, sizeof(PersistArgs), hipMemcpyHostToDevice, g.st));
+            persist_reset(pa, n_cu_, g.st);
+        }
         dec_embed(dt_, g.tok_in, g.B * Tq, Tq, dm_.d, tok_emb_, dec_pos_, g.ds, g.dx, g.st);
         enqueue_decoder_pass(g, B, Tq, rq, out_cap);  // prompt pass produces token 0
     }
     int passes = 1;
     static const bool no_graph = getenv("SPT_NO_GRAPH") != nullptr;  // eager passes (profilers, debugging)
+    static const bool sync_debug = getenv("SPT_DEBUG_SYNC") != nullptr;  // per-pass sync + state check
     if (rq.n_steps > 1 && no_graph) {
         for (int s = 1; s < rq.n_steps; ++s, ++passes)
-            for (DecGroup* g : act) enqueue_decoder_pass(*g, B, 1, rq, out_cap);
+            for (DecGroup* g : act) {
+                enqueue_decoder_pass(*g, B, 1, rq, out_cap);
+                if (!sync_debug) continue;
+                const hipError_t e = hipStreamSynchronize(g->st);
+                DecState h{};
+                unsigned ab = 0;
+                if (e == hipSuccess) {
+                    HIP_CHECK(hipMemcpy(&h, g->ds, sizeof(h), hipMemcpyDeviceToHost));
+                    HIP_CHECK(hipMemcpy(&ab, g->abort_flag, 4, hipMemcpyDeviceToHost));
+                }
+                if (e != hipSuccess || ab || h.step != s + 1 || (s % 16) == 0)
+                    fprintf(stderr, "[spt] pass %d: %s step=%d pos0=%d abort=%u\n", s, hipGetErrorString(e), h.step,
+                            h.pos0, ab);
+                if (e != hipSuccess) throw HipError(std::string("pass failed: ") + hipGetErrorString(e));
+            }
     } else if (rq.n_steps > 1) {
         std::vector<hipGraphExec_t> ex;
         for (DecGroup* g : act) {
@@ -607,6 +682,21 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         if (top2) HIP_CHECK(hipMemcpyAsync(top2 + off, g->out_t2, n, hipMemcpyDeviceToHost, g->st));
         HIP_CHECK(hipEventRecord(g->ev, g->st));
         HIP_CHECK(hipStreamWaitEvent(st_, g->ev, 0));
+        if (persist_ok(g->B, 1)) {
+            unsigned ab = 0;
+            HIP_CHECK(hipMemcpyAsync(&ab, g->abort_flag, 4, hipMemcpyDeviceToHost, g->st));
+            HIP_CHECK(hipStreamSynchronize(g->st));
+            if (ab == 3) {
+                unsigned w[4];
+                HIP_CHECK(hipMemcpy(w, g->abort_flag, 16, hipMemcpyDeviceToHost));
+                char msg[160];
+                snprintf(msg, sizeof msg, "persistent decoder: out-of-arena access at site %u, address 0x%08x%08x",
+                         w[1], w[3], w[2]);
+                throw std::runtime_error(msg);
+            }
+            if (ab == 2) throw std::runtime_error("persistent decoder: invalid decode state (pos/step)");
+            if (ab) throw std::runtime_error("persistent decoder pass timed out waiting for a phase (results invalid)");
+        }
     }
 }
 
@@ -774,6 +864,19 @@ double Engine::probe(int kind, int iters, double* work, int* is_flops) {
             *work = 4.0 * B * H * (double)T * T * 64;
             *is_flops = 1;
             break;
+        case 6: {  // the persistent decoder pass (flags reset first: each launch synchronises for real)
+            if (!persist_ok(Bg, 1)) throw std::runtime_error("persistent decoder pass not active for this engine");
+            launch = [&] {
+                persist_reset(g.hargs, n_cu_, st_);
+                dec_persist(g.hargs, g.pargs, n_cu_, st_);
+            };
+            DecState h{};
+            HIP_CHECK(hipMemcpy(&h, g.ds, sizeof(h), hipMemcpyDeviceToHost));
+            // weights streamed once per pass + cross K/V + self K/V read
+            const double wl = 14.0 * d * d * esz_;
+            *work = dm_.n_dec * (wl + 2.0 * Bg * H * T * 64 * esz_ + 2.0 * Bg * H * (h.pos0 + 1) * 64 * esz_);
+            break;
+        }
         default:
             throw std::runtime_error("unknown probe kind");
     }

@@ -530,6 +530,11 @@ __global__ __launch_bounds__(256) void finalize_kernel(FinalizeArgs a) {
     __syncthreads();
     if (tid == 0) {
         for (int w = 1; w < 4; ++w) t = top_merge(t, s_top[w]);
+        // non-finite logits leave no valid winner: record the sentinel, never index with it
+        if (t.i1 < 0 || t.i1 >= a.n_vocab) {
+            t.i1 = -2;
+            t.v1 = t.v2 = __builtin_nanf("");
+        }
         int nxt = a.eot;
         if (step < a.out_cap) {
             const int oi = b * a.out_cap + step;
@@ -544,6 +549,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(FinalizeArgs a) {
                 nxt = t.i1;
                 if (a.forced && step < a.forced_len) nxt = a.forced[b * a.forced_len + step];
                 if (!a.ignore_eot && t.i1 == a.eot) a.done[b] = 1;
+                if (nxt < 0 || nxt >= a.n_vocab) nxt = a.eot;
             }
         }
         a.next_tok[b] = nxt;
