@@ -122,6 +122,9 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     cp_ = ((dm_.n_mels + 63) / 64) * 64;
     if ((3 * cp_ * esz_) % 128) cp_ = ((dm_.n_mels + 127) / 128) * 128;
     if (const char* g = getenv("SPT_DECODE_GROUPS")) n_groups_ = std::max(1, std::min(2, atoi(g)));
+    // cross-workgroup K split of the small decoder GEMVs: measured slower on MI355X (the
+    // last-arriver release/acquire costs more than the extra CUs gain), opt-in only
+    kz_split_ = getenv("SPT_GEMV_KSPLIT") != nullptr;
     select();
     HIP_CHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     ev_.resize(8);
@@ -136,6 +139,7 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     generate_weights();
     upload_tables();
     alloc_workspace();
+    for (auto& g : groups_) HIP_CHECK(hipMemsetAsync(g.kcnt, 0, kGemvMaxTiles * 4, st_));
     setup_persist();
     HIP_CHECK(hipStreamSynchronize(st_));
 }
@@ -415,6 +419,8 @@ void Engine::alloc_workspace() {
             g.done = (int*)c.take(B * 4);
             g.forced = (int*)c.take(B * ctx * 4);
             g.ds = (DecState*)c.take(sizeof(DecState));
+            g.kpart = (float*)c.take(kGemvPartBytes);
+            g.kcnt = (unsigned*)c.take(kGemvMaxTiles * 4);
             g.xpart = (float*)c.take(B * H * 64 * 66 * 4);
             g.xcnt = (unsigned*)c.take(2 * B * H * 4);
             g.flags = (unsigned*)c.take(1024 * 4);
@@ -510,26 +516,32 @@ void Engine::enqueue_decoder_pass(DecGroup& g, int B_total, int Tq, const Decode
         a.A = g.dx; a.lda = d; a.ln_w = e.ln1_w; a.ln_b = e.ln1_b; a.R = R;
         a.W = e.qkv_w; a.N = 3 * d; a.K = d; a.bias = e.qkv_b; a.C = g.dq; a.ldc = d;
         a.cache = skv_l; a.cache_B = B; a.cache_H = H; a.cache_ctx = ctx; a.Tq = Tq; a.st = g.ds;
+        if (kz_split_) { a.kpart = g.kpart; a.kcnt = g.kcnt; }
         gemv(dt_, GV_QKV_CACHE, a, st);
         dec_self_attn(dt_, g.dq, skv_l, B, H, ctx, Tq, g.ds, g.dao, st);
         a = GemvArgs{};
         a.A = g.dao; a.lda = d; a.R = R; a.W = e.so_w; a.N = d; a.K = d; a.bias = e.so_b; a.C = g.dx; a.ldc = d;
+        if (kz_split_) { a.kpart = g.kpart; a.kcnt = g.kcnt; }
         gemv(dt_, GV_BIAS_RESID, a, st);
         a = GemvArgs{};
         a.A = g.dx; a.lda = d; a.ln_w = e.ln2_w; a.ln_b = e.ln2_b; a.R = R;
         a.W = e.cq_w; a.N = d; a.K = d; a.bias = e.cq_b; a.C = g.dq; a.ldc = d;
+        if (kz_split_) { a.kpart = g.kpart; a.kcnt = g.kcnt; }
         gemv(dt_, GV_BIAS, a, st);
         dec_cross_attn(dt_, g.dq, ckv_l, B, B_total, H, T, Tq, g.dao, st);
         a = GemvArgs{};
         a.A = g.dao; a.lda = d; a.R = R; a.W = e.co_w; a.N = d; a.K = d; a.bias = e.co_b; a.C = g.dx; a.ldc = d;
+        if (kz_split_) { a.kpart = g.kpart; a.kcnt = g.kcnt; }
         gemv(dt_, GV_BIAS_RESID, a, st);
         a = GemvArgs{};
         a.A = g.dx; a.lda = d; a.ln_w = e.ln3_w; a.ln_b = e.ln3_b; a.R = R;
         a.W = e.fc1_w; a.N = 4 * d; a.K = d; a.bias = e.fc1_b; a.C = g.dff; a.ldc = 4 * d;
+        if (kz_split_) { a.kpart = g.kpart; a.kcnt = g.kcnt; }
         gemv(dt_, GV_BIAS_GELU, a, st);
         a = GemvArgs{};
         a.A = g.dff; a.lda = 4 * d; a.R = R; a.W = e.fc2_w; a.N = d; a.K = 4 * d; a.bias = e.fc2_b; a.C = g.dx;
         a.ldc = d;
+        if (kz_split_) { a.kpart = g.kpart; a.kcnt = g.kcnt; }
         gemv(dt_, GV_BIAS_RESID, a, st);
     }
     const Specials sp = specials_for(dm_.n_vocab);

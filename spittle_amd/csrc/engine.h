@@ -91,6 +91,8 @@ private:
         int *tok_in = nullptr, *out_tok = nullptr, *done = nullptr, *forced = nullptr;
         float *out_t1 = nullptr, *out_t2 = nullptr;
         DecState* ds = nullptr;
+        float* kpart = nullptr;       // GEMV cross-workgroup K-split partials
+        unsigned* kcnt = nullptr;     // ... and per-tile arrival counters
         // persistent decoder pass (k_persist.hip)
         float* xpart = nullptr;       // attention split partials
         unsigned* xcnt = nullptr;     // split tickets [2][B*H]
@@ -119,6 +121,7 @@ private:
     int esz_;     // bytes per weight / activation element
     int cp_;      // padded mel channels (conv1 K = 3 * cp_)
     int n_groups_ = 1;  // SPT_DECODE_GROUPS=2 splits the batch over two streams
+    bool kz_split_ = false;  // SPT_GEMV_KSPLIT: cross-workgroup K split of decoder GEMVs
     // persistent decoder pass: one workgroup per CU (SPT_PERSIST=0 disables)
     bool persist_ = false;
     int n_cu_ = 0, s_self_ = 8, s_cross_ = 12;

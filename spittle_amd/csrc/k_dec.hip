@@ -20,6 +20,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <algorithm>
+
 namespace spt {
 
 namespace {
@@ -86,20 +88,36 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
     const int n0 = tile * 16;
     const int K = a.K;
     const int lds_ld = K + CPE;  // padded row stride (elements): rows land 4 banks apart
-    const int nss = K / KS;
+    // K split across the grid's y dimension: this workgroup owns super-steps [ss0, ss1)
+    const int kz = blockIdx.y, kzc = gridDim.y;
+    const int nss_all = K / KS, per = (nss_all + kzc - 1) / kzc;
+    const int ss0 = kz * per, ss1 = min(nss_all, ss0 + per);
     const T* wrow = (const T*)a.W + (size_t)min(n0 + fr, a.N - 1) * K + fq * EPL;
 
     frag w[MAXJ][4];
     auto load_chunk = [&](int j0) {
 #pragma unroll
         for (int j = 0; j < MAXJ; ++j) {
-            const int ss = ks + (j0 + j) * KSPLIT;
-            if (ss < nss) {
+            const int ss = ss0 + ks + (j0 + j) * KSPLIT;
+            if (ss < ss1) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) w[j][i] = *(const frag*)(wrow + (size_t)ss * KS + i * CPE);
             }
         }
     };
+    // LayerNorm input rows are fetched BEFORE the weight stream: loads retire in issue
+    // order, so the prologue then waits only for its own row, not for the weights
+    float4 x0[6];
+    if constexpr (LN) {
+        if (wid < a.R) {
+            const float* xr = (const float*)a.A + (size_t)wid * a.lda + a.a_row0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const int k = lane * 4 + 256 * i;
+                if (k < K) x0[i] = *(const float4*)(xr + k);
+            }
+        }
+    }
     load_chunk(0);  // the first weight fetch overlaps the LayerNorm prologue
 
     if constexpr (LN) {
@@ -112,7 +130,7 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
             for (int i = 0; i < 6; ++i) {
                 const int k = lane * 4 + 256 * i;
                 if (k < K) {
-                    v[i] = *(const float4*)(xr + k);
+                    v[i] = r == wid ? x0[i] : *(const float4*)(xr + k);
                     s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
                 }
             }
@@ -150,8 +168,8 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
     auto compute_chunk = [&](int j0) {
 #pragma unroll
         for (int j = 0; j < MAXJ; ++j) {
-            const int ss = ks + (j0 + j) * KSPLIT;
-            if (ss >= nss) break;
+            const int ss = ss0 + ks + (j0 + j) * KSPLIT;
+            if (ss >= ss1) break;
             const int kb = ss * KS + fq * EPL;
 #pragma unroll
             for (int g = 0; g < RG; ++g) {
@@ -183,7 +201,7 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
             }
         }
     };
-    for (int j0 = 0; ks + j0 * KSPLIT < nss; j0 += MAXJ) {
+    for (int j0 = 0; ss0 + ks + j0 * KSPLIT < ss1; j0 += MAXJ) {
         if (j0 > 0) load_chunk(j0);
         compute_chunk(j0);
     }
@@ -202,6 +220,28 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
 #pragma unroll
             for (int s = 1; s < KSPLIT; ++s) v += red[(((s * CT) + ct) * RG + g) * 64 + lane];
             acc[g] = v;
+        }
+    }
+    if constexpr (MODE != GV_LOGITS) {
+        // cross-workgroup K split: partials to global, the last arriver of the tile sums
+        // them in split order (deterministic) and runs the epilogue
+        if (kzc > 1) {
+            f32x4* kp = (f32x4*)a.kpart + (size_t)tile * kzc * RG * 64;
+#pragma unroll
+            for (int g = 0; g < RG; ++g) kp[(kz * RG + g) * 64 + lane] = acc[g];
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            unsigned t = 0;
+            if (lane == 0) t = __hip_atomic_fetch_add(a.kcnt + tile, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            t = __shfl(t, 0, 64);
+            if (t != (unsigned)kzc - 1) return;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#pragma unroll
+            for (int g = 0; g < RG; ++g) {
+                f32x4 v = kp[g * 64 + lane];
+                for (int z = 1; z < kzc; ++z) v += kp[(z * RG + g) * 64 + lane];
+                acc[g] = v;
+            }
+            if (lane == 0) __hip_atomic_store(a.kcnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     const int n = n0 + fr;
@@ -275,8 +315,8 @@ template <typename T, int MODE, bool LN, int RG, int NWV, int CT, int MAXJ>
 void gemv_launch_cfg(const GemvArgs& a, hipStream_t st) {
     const int red = NWV * RG * 64 * (int)sizeof(f32x4);
     const int lds = (LN ? gv_img_bytes(a.R, a.K, sizeof(T)) : 0) + (NWV / CT > 1 ? red : 0);
-    hipLaunchKernelGGL((gemv_kernel<T, MODE, LN, RG, NWV, CT, MAXJ>), dim3(cdiv(a.N, 16 * CT)), dim3(64 * NWV), lds,
-                       st, a);
+    hipLaunchKernelGGL((gemv_kernel<T, MODE, LN, RG, NWV, CT, MAXJ>), dim3(cdiv(a.N, 16 * CT), a.ksplit),
+                       dim3(64 * NWV), lds, st, a);
     SPT_LAUNCH_CHECK();
 }
 
@@ -309,7 +349,7 @@ void gemv_attr_modes() {
 
 template <typename T, int MODE, bool LN, int RG>
 void gemv_launch_rg(const GemvArgs& a, hipStream_t st) {
-    const int nss = a.K / GV<T>::KS;
+    const int nss = cdiv(a.K / GV<T>::KS, a.ksplit);  // super-steps per workgroup
     if (a.N >= 16384) gemv_launch_cfg<T, MODE, LN, RG, 4, 4, 4>(a, st);
     else if (nss <= 8) gemv_launch_cfg<T, MODE, LN, RG, 8, 1, 1>(a, st);
     else if (nss <= 16) gemv_launch_cfg<T, MODE, LN, RG, 8, 1, 2>(a, st);
@@ -584,9 +624,19 @@ void gemv_prepare(int dtype) {
     else gemv_attr_modes<float>();
 }
 
-void gemv(int dtype, int mode, const GemvArgs& a, hipStream_t st) {
-    if (a.R > 64 || a.R <= 0) throw std::runtime_error("gemv: rows must be in 1..64");
-    if (a.K % (dtype == DT_BF16 ? 128 : 64)) throw std::runtime_error("gemv: K alignment");
+void gemv(int dtype, int mode, const GemvArgs& a_in, hipStream_t st) {
+    if (a_in.R > 64 || a_in.R <= 0) throw std::runtime_error("gemv: rows must be in 1..64");
+    const int ks = dtype == DT_BF16 ? 128 : 64;
+    if (a_in.K % ks) throw std::runtime_error("gemv: K alignment");
+    GemvArgs a = a_in;
+    // fill the chip: fewer than ~256 column-tile workgroups -> split K across workgroups
+    // (depends on N and K only, so results never depend on the batch)
+    a.ksplit = 1;
+    if (mode != GV_LOGITS && a.kpart && a.kcnt) {
+        const int nwg = cdiv(a.N, 16), nss = a.K / ks;
+        a.ksplit = std::max(1, std::min(std::min(256 / nwg, kGemvMaxKSplit), nss));
+        if (a.N / 16 > kGemvMaxTiles) a.ksplit = 1;
+    }
 #define SPT_GV(T, M) \
     case M: gemv_launch<T, M>(a, st); return;
     if (dtype == DT_BF16) {

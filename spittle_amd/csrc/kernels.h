@@ -81,7 +81,13 @@ struct GemvArgs {
     // GV_LOGITS: suppression + per-16-column-tile top-2 partials [R][n_tiles] (16 B each)
     const uint32_t* suppress; int blank0, blank1;
     void* part; int n_tiles;
+    // optional cross-workgroup K split (non-logits modes): partials [tiles][split][rows/16][64]
+    // f32x4 and one arrival counter per column tile (zero between launches)
+    float* kpart; unsigned* kcnt;
+    int ksplit;                           // set by gemv()
 };
+constexpr int kGemvMaxKSplit = 4, kGemvMaxTiles = 512;
+constexpr int64_t kGemvPartBytes = (int64_t)kGemvMaxTiles * kGemvMaxKSplit * 4 * 64 * 16;
 void gemv(int dtype, int mode, const GemvArgs& a, hipStream_t st);
 // one-time per-process kernel attributes (call before any stream capture)
 void gemv_prepare(int dtype);
