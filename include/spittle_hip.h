@@ -132,8 +132,7 @@ typedef enum {
     SPT_PROBE_DEC_LOGITS = 2,      /* final LayerNorm + logits + top-2 partials */
     SPT_PROBE_DEC_FC1 = 3,         /* decoder LayerNorm + fc1 + GELU (weight stream) */
     SPT_PROBE_ENC_FC1_GEMM = 4,    /* encoder fc1 GEMM + bias + GELU */
-    SPT_PROBE_ENC_ATTN = 5,        /* encoder flash attention, one layer */
-    SPT_PROBE_DEC_PASS = 6         /* one whole persistent decoder pass (all layers, bf16) */
+    SPT_PROBE_ENC_ATTN = 5         /* encoder flash attention, one layer */
 } spt_probe_kind;
 spt_status spt_probe_kernel(spt_ctx* ctx, int32_t kind, int32_t iters, double* avg_us, double* work,
                             int32_t* work_is_flops);

@@ -25,7 +25,7 @@ EXPORTS = [
     "spt_debug_encode", "spt_debug_weight_checksum", "spt_probe_kernel",
 ]
 PROBES = {"dec_cross_attn": 0, "dec_self_attn": 1, "dec_logits": 2, "dec_fc1": 3, "enc_fc1_gemm": 4,
-          "enc_attn": 5, "dec_pass": 6}
+          "enc_attn": 5}
 
 
 class ModelParams(C.Structure):

@@ -122,9 +122,9 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     cp_ = ((dm_.n_mels + 63) / 64) * 64;
     if ((3 * cp_ * esz_) % 128) cp_ = ((dm_.n_mels + 127) / 128) * 128;
     if (const char* g = getenv("SPT_DECODE_GROUPS")) n_groups_ = std::max(1, std::min(2, atoi(g)));
-    // cross-workgroup K split of the small decoder GEMVs: measured slower on MI355X (the
-    // last-arriver release/acquire costs more than the extra CUs gain), opt-in only
-    kz_split_ = getenv("SPT_GEMV_KSPLIT") != nullptr;
+    // cross-attention key split / waves per workgroup: fixed per engine (never per batch)
+    if (const char* v = getenv("SPT_XATTN_SPLIT")) xsplit_ = std::max(1, std::min(kAttnMaxSplit, atoi(v)));
+    if (const char* v = getenv("SPT_XATTN_WAVES")) xwaves_ = atoi(v) == 16 ? 16 : 8;
     select();
     HIP_CHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     ev_.resize(8);
@@ -139,43 +139,7 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     generate_weights();
     upload_tables();
     alloc_workspace();
-    for (auto& g : groups_) HIP_CHECK(hipMemsetAsync(g.kcnt, 0, kGemvMaxTiles * 4, st_));
-    setup_persist();
     HIP_CHECK(hipStreamSynchronize(st_));
-}
-
-// The persistent pass needs every workgroup co-resident (one per CU); it is used only
-// where its shape checks pass and a single decode stream owns the device. EXPERIMENTAL:
-// opt-in with SPT_PERSIST=1 (an unexplained device fault in long runs is under study).
-void Engine::setup_persist() {
-    const char* env = getenv("SPT_PERSIST");
-    if (dt_ != DT_BF16 || n_groups_ != 1 || !env || env[0] != '1') return;
-    hipDeviceProp_t prop;
-    HIP_CHECK(hipGetDeviceProperties(&prop, dev_));
-    n_cu_ = prop.multiProcessorCount;
-    if (n_cu_ < 1 || n_cu_ > 1024) return;
-    // key splits depend on the device and model only, never on the batch (batch invariance)
-    s_cross_ = std::max(1, std::min(64, n_cu_ * 8 / (8 * dm_.n_head)));
-    s_self_ = 8;
-    std::vector<PersistLayer> pl(dm_.n_dec);
-    for (int l = 0; l < dm_.n_dec; ++l) {
-        const DecL& e = dec_[l];
-        PersistLayer& q = pl[l];
-        q.qkv_w = (const uint16_t*)e.qkv_w; q.so_w = (const uint16_t*)e.so_w; q.cq_w = (const uint16_t*)e.cq_w;
-        q.co_w = (const uint16_t*)e.co_w; q.fc1_w = (const uint16_t*)e.fc1_w; q.fc2_w = (const uint16_t*)e.fc2_w;
-        q.qkv_b = e.qkv_b; q.so_b = e.so_b; q.cq_b = e.cq_b; q.co_b = e.co_b; q.fc1_b = e.fc1_b; q.fc2_b = e.fc2_b;
-        q.ln1_w = e.ln1_w; q.ln1_b = e.ln1_b; q.ln2_w = e.ln2_w; q.ln2_b = e.ln2_b; q.ln3_w = e.ln3_w; q.ln3_b = e.ln3_b;
-    }
-    HIP_CHECK(hipMemcpy(players_, pl.data(), pl.size() * sizeof(PersistLayer), hipMemcpyHostToDevice));
-    persist_prepare();
-    persist_ = true;
-}
-
-bool Engine::persist_ok(int B, int Tq) const {
-    if (!persist_ || Tq != 1) return false;
-    PersistArgs a{};
-    a.B = B; a.d = dm_.d; a.H = dm_.n_head; a.S_self = s_self_; a.S_cross = s_cross_;
-    return persist_check(a, n_cu_) == nullptr;
 }
 
 Engine::~Engine() {
@@ -419,15 +383,9 @@ void Engine::alloc_workspace() {
             g.done = (int*)c.take(B * 4);
             g.forced = (int*)c.take(B * ctx * 4);
             g.ds = (DecState*)c.take(sizeof(DecState));
-            g.kpart = (float*)c.take(kGemvPartBytes);
-            g.kcnt = (unsigned*)c.take(kGemvMaxTiles * 4);
-            g.xpart = (float*)c.take(B * H * 64 * 66 * 4);
-            g.xcnt = (unsigned*)c.take(2 * B * H * 4);
-            g.flags = (unsigned*)c.take(1024 * 4);
-            g.abort_flag = (unsigned*)c.take(64);
-            g.pargs = (PersistArgs*)c.take(sizeof(PersistArgs));
+            g.xpart = (float*)c.take((int64_t)B * H * kAttnMaxSplit * 4 * 66 * 4);
+            g.xcnt = (unsigned*)c.take(B * H * 4);
         }
-        players_ = (PersistLayer*)c.take(L * sizeof(PersistLayer));
         if (!pass) {
             abytes_ = c.off;
             if (hipMalloc(&aarena_, abytes_) != hipSuccess) {
@@ -505,9 +463,7 @@ void Engine::enqueue_decoder_pass(DecGroup& g, int B_total, int Tq, const Decode
     hipStream_t st = g.st;
     // g.dx already holds this pass's input embeddings (dec_embed for the prompt pass,
     // dec_finalize of the previous pass afterwards)
-    const bool persist = Tq == 1 && persist_ok(B, 1);
-    if (persist) dec_persist(g.hargs, g.pargs, n_cu_, st);  // every layer in one launch
-    for (int l = 0; l < (persist ? 0 : dm_.n_dec); ++l) {
+    for (int l = 0; l < dm_.n_dec; ++l) {
         const DecL& e = dec_[l];
         void* skv_l = (char*)g.skv + self_layer * l * esz_;
         // this group's sequences inside the [2][B_total][H][T][64] cross K/V of layer l
@@ -516,32 +472,28 @@ void Engine::enqueue_decoder_pass(DecGroup& g, int B_total, int Tq, const Decode
         a.A = g.dx; a.lda = d; a.ln_w = e.ln1_w; a.ln_b = e.ln1_b; a.R = R;
         a.W = e.qkv_w; a.N = 3 * d; a.K = d; a.bias = e.qkv_b; a.C = g.dq; a.ldc = d;
         a.cache = skv_l; a.cache_B = B; a.cache_H = H; a.cache_ctx = ctx; a.Tq = Tq; a.st = g.ds;
-        if (kz_split_) { a.kpart = g.kpart; a.kcnt = g.kcnt; }
         gemv(dt_, GV_QKV_CACHE, a, st);
         dec_self_attn(dt_, g.dq, skv_l, B, H, ctx, Tq, g.ds, g.dao, st);
         a = GemvArgs{};
         a.A = g.dao; a.lda = d; a.R = R; a.W = e.so_w; a.N = d; a.K = d; a.bias = e.so_b; a.C = g.dx; a.ldc = d;
-        if (kz_split_) { a.kpart = g.kpart; a.kcnt = g.kcnt; }
         gemv(dt_, GV_BIAS_RESID, a, st);
         a = GemvArgs{};
         a.A = g.dx; a.lda = d; a.ln_w = e.ln2_w; a.ln_b = e.ln2_b; a.R = R;
         a.W = e.cq_w; a.N = d; a.K = d; a.bias = e.cq_b; a.C = g.dq; a.ldc = d;
-        if (kz_split_) { a.kpart = g.kpart; a.kcnt = g.kcnt; }
         gemv(dt_, GV_BIAS, a, st);
-        dec_cross_attn(dt_, g.dq, ckv_l, B, B_total, H, T, Tq, g.dao, st);
+        AttnSplit xs;
+        xs.splits = xsplit_; xs.waves = xwaves_; xs.xpart = g.xpart; xs.xcnt = g.xcnt;
+        dec_cross_attn(dt_, g.dq, ckv_l, B, B_total, H, T, Tq, g.dao, xs, st);
         a = GemvArgs{};
         a.A = g.dao; a.lda = d; a.R = R; a.W = e.co_w; a.N = d; a.K = d; a.bias = e.co_b; a.C = g.dx; a.ldc = d;
-        if (kz_split_) { a.kpart = g.kpart; a.kcnt = g.kcnt; }
         gemv(dt_, GV_BIAS_RESID, a, st);
         a = GemvArgs{};
         a.A = g.dx; a.lda = d; a.ln_w = e.ln3_w; a.ln_b = e.ln3_b; a.R = R;
         a.W = e.fc1_w; a.N = 4 * d; a.K = d; a.bias = e.fc1_b; a.C = g.dff; a.ldc = 4 * d;
-        if (kz_split_) { a.kpart = g.kpart; a.kcnt = g.kcnt; }
         gemv(dt_, GV_BIAS_GELU, a, st);
         a = GemvArgs{};
         a.A = g.dff; a.lda = 4 * d; a.R = R; a.W = e.fc2_w; a.N = d; a.K = 4 * d; a.bias = e.fc2_b; a.C = g.dx;
         a.ldc = d;
-        if (kz_split_) { a.kpart = g.kpart; a.kcnt = g.kcnt; }
         gemv(dt_, GV_BIAS_RESID, a, st);
     }
     const Specials sp = specials_for(dm_.n_vocab);
@@ -615,21 +567,6 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         fill_f32(g.out_t1, (int64_t)g.B * out_cap, -INFINITY, g.st);
         fill_f32(g.out_t2, (int64_t)g.B * out_cap, -INFINITY, g.st);
         dec_reset(g.ds, g.arrive, g.st);
-        if (persist_ok(g.B, 1)) {  // arguments of this call's persistent passes
-            const int d = dm_.d, H = dm_.n_head, ctx = dm_.n_text_ctx, T = dm_.n_audio_ctx;
-            PersistArgs& pa = g.hargs;
-            pa = PersistArgs{};
-            pa.layers = players_; pa.n_layers = dm_.n_dec;
-            pa.B = g.B; pa.d = d; pa.H = H; pa.ctx = ctx; pa.T_enc = T; pa.B_layout = B;
-            pa.S_self = s_self_; pa.S_cross = s_cross_;
-            pa.x = g.dx; pa.q = (uint16_t*)g.dq; pa.ao = (uint16_t*)g.dao; pa.ff = (uint16_t*)g.dff;
-            pa.skv = (uint16_t*)g.skv; pa.self_layer = (int64_t)2 * g.B * H * ctx * 64;
-            pa.ckv = (const uint16_t*)ckv_ + (int64_t)g.b0 * H * T * 64; pa.cross_layer = (int64_t)2 * B * H * T * 64;
-            pa.xpart = g.xpart; pa.xcnt = g.xcnt; pa.flags = g.flags; pa.abort_flag = g.abort_flag; pa.ds = g.ds;
-            pa.ws_lo = aarena_; pa.ws_hi = aarena_ + abytes_; pa.wt_lo = warena_; pa.wt_hi = warena_ + wbytes_;
-            HIP_CHECK(hipMemcpyAsync(g.pargs, &pa, sizeof(PersistArgs), hipMemcpyHostToDevice, g.st));
-            persist_reset(pa, n_cu_, g.st);
-        }
         dec_embed(dt_, g.tok_in, g.B * Tq, Tq, dm_.d, tok_emb_, dec_pos_, g.ds, g.dx, g.st);
         enqueue_decoder_pass(g, B, Tq, rq, out_cap);  // prompt pass produces token 0
     }
@@ -643,14 +580,9 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
                 if (!sync_debug) continue;
                 const hipError_t e = hipStreamSynchronize(g->st);
                 DecState h{};
-                unsigned ab = 0;
-                if (e == hipSuccess) {
-                    HIP_CHECK(hipMemcpy(&h, g->ds, sizeof(h), hipMemcpyDeviceToHost));
-                    HIP_CHECK(hipMemcpy(&ab, g->abort_flag, 4, hipMemcpyDeviceToHost));
-                }
-                if (e != hipSuccess || ab || h.step != s + 1 || (s % 16) == 0)
-                    fprintf(stderr, "[spt] pass %d: %s step=%d pos0=%d abort=%u\n", s, hipGetErrorString(e), h.step,
-                            h.pos0, ab);
+                if (e == hipSuccess) HIP_CHECK(hipMemcpy(&h, g->ds, sizeof(h), hipMemcpyDeviceToHost));
+                if (e != hipSuccess || h.step != s + 1 || (s % 16) == 0)
+                    fprintf(stderr, "[spt] pass %d: %s step=%d pos0=%d\n", s, hipGetErrorString(e), h.step, h.pos0);
                 if (e != hipSuccess) throw HipError(std::string("pass failed: ") + hipGetErrorString(e));
             }
     } else if (rq.n_steps > 1) {
@@ -694,21 +626,6 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         if (top2) HIP_CHECK(hipMemcpyAsync(top2 + off, g->out_t2, n, hipMemcpyDeviceToHost, g->st));
         HIP_CHECK(hipEventRecord(g->ev, g->st));
         HIP_CHECK(hipStreamWaitEvent(st_, g->ev, 0));
-        if (persist_ok(g->B, 1)) {
-            unsigned ab = 0;
-            HIP_CHECK(hipMemcpyAsync(&ab, g->abort_flag, 4, hipMemcpyDeviceToHost, g->st));
-            HIP_CHECK(hipStreamSynchronize(g->st));
-            if (ab == 3) {
-                unsigned w[4];
-                HIP_CHECK(hipMemcpy(w, g->abort_flag, 16, hipMemcpyDeviceToHost));
-                char msg[160];
-                snprintf(msg, sizeof msg, "persistent decoder: out-of-arena access at site %u, address 0x%08x%08x",
-                         w[1], w[3], w[2]);
-                throw std::runtime_error(msg);
-            }
-            if (ab == 2) throw std::runtime_error("persistent decoder: invalid decode state (pos/step)");
-            if (ab) throw std::runtime_error("persistent decoder pass timed out waiting for a phase (results invalid)");
-        }
     }
 }
 
@@ -828,7 +745,11 @@ double Engine::probe(int kind, int iters, double* work, int* is_flops) {
     *is_flops = 0;
     switch (kind) {
         case 0:  // cross-attention of decoder layer 0 over this group's cross K/V
-            launch = [&] { dec_cross_attn(dt_, g.dq, ckv_, Bg, B, H, T, 1, g.dao, st_); };
+            launch = [&] {
+                AttnSplit xs;
+                xs.splits = xsplit_; xs.waves = xwaves_; xs.xpart = g.xpart; xs.xcnt = g.xcnt;
+                dec_cross_attn(dt_, g.dq, ckv_, Bg, B, H, T, 1, g.dao, xs, st_);
+            };
             *work = 2.0 * Bg * H * T * 64 * esz_;
             break;
         case 1:
@@ -876,19 +797,6 @@ double Engine::probe(int kind, int iters, double* work, int* is_flops) {
             *work = 4.0 * B * H * (double)T * T * 64;
             *is_flops = 1;
             break;
-        case 6: {  // the persistent decoder pass (flags reset first: each launch synchronises for real)
-            if (!persist_ok(Bg, 1)) throw std::runtime_error("persistent decoder pass not active for this engine");
-            launch = [&] {
-                persist_reset(g.hargs, n_cu_, st_);
-                dec_persist(g.hargs, g.pargs, n_cu_, st_);
-            };
-            DecState h{};
-            HIP_CHECK(hipMemcpy(&h, g.ds, sizeof(h), hipMemcpyDeviceToHost));
-            // weights streamed once per pass + cross K/V + self K/V read
-            const double wl = 14.0 * d * d * esz_;
-            *work = dm_.n_dec * (wl + 2.0 * Bg * H * T * 64 * esz_ + 2.0 * Bg * H * (h.pos0 + 1) * 64 * esz_);
-            break;
-        }
         default:
             throw std::runtime_error("unknown probe kind");
     }

@@ -91,15 +91,8 @@ private:
         int *tok_in = nullptr, *out_tok = nullptr, *done = nullptr, *forced = nullptr;
         float *out_t1 = nullptr, *out_t2 = nullptr;
         DecState* ds = nullptr;
-        float* kpart = nullptr;       // GEMV cross-workgroup K-split partials
-        unsigned* kcnt = nullptr;     // ... and per-tile arrival counters
-        // persistent decoder pass (k_persist.hip)
-        float* xpart = nullptr;       // attention split partials
-        unsigned* xcnt = nullptr;     // split tickets [2][B*H]
-        unsigned* flags = nullptr;    // per-workgroup phase flags
-        unsigned* abort_flag = nullptr;
-        PersistArgs* pargs = nullptr; // device copy of the launch arguments
-        PersistArgs hargs{};          // host copy
+        float* xpart = nullptr;       // cross-attention key-split partials
+        unsigned* xcnt = nullptr;     // ... and their arrival tickets [B*H]
         std::map<GraphKey, hipGraphExec_t> graphs;
     };
 
@@ -120,14 +113,8 @@ private:
     uint64_t seed_;
     int esz_;     // bytes per weight / activation element
     int cp_;      // padded mel channels (conv1 K = 3 * cp_)
+    int xsplit_ = 1, xwaves_ = 8;  // cross-attention key split, waves per workgroup
     int n_groups_ = 1;  // SPT_DECODE_GROUPS=2 splits the batch over two streams
-    bool kz_split_ = false;  // SPT_GEMV_KSPLIT: cross-workgroup K split of decoder GEMVs
-    // persistent decoder pass: one workgroup per CU (SPT_PERSIST=0 disables)
-    bool persist_ = false;
-    int n_cu_ = 0, s_self_ = 8, s_cross_ = 12;
-    PersistLayer* players_ = nullptr;
-    bool persist_ok(int B, int Tq) const;
-    void setup_persist();
     hipStream_t st_ = nullptr;
     std::vector<hipEvent_t> ev_;
 

@@ -71,6 +71,20 @@ __device__ __forceinline__ TopP top_shfl(TopP t, int mask) {
     return u;
 }
 
+// weight loads: default cache policy. Non-temporal (SPT_GV_NT=1) measured slower on MI355X
+// (r1 ubench: logits 36.8 -> 58.6 us, one decoder layer 59.6 -> 76.9 us)
+#ifndef SPT_GV_NT
+#define SPT_GV_NT 0
+#endif
+template <typename F>
+__device__ __forceinline__ F load_w(const F* p) {
+#if SPT_GV_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+
 // NWV waves; CT column tiles of 16 per workgroup; KSPLIT = NWV / CT waves share a tile
 // and split its K.  Each wave keeps up to MAXJ super-steps of weights in flight.
 template <typename T, int MODE, bool LN, int RG, int NWV, int CT, int MAXJ>
@@ -101,7 +115,7 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
             const int ss = ss0 + ks + (j0 + j) * KSPLIT;
             if (ss < ss1) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) w[j][i] = *(const frag*)(wrow + (size_t)ss * KS + i * CPE);
+                for (int i = 0; i < 4; ++i) w[j][i] = load_w((const frag*)(wrow + (size_t)ss * KS + i * CPE));
             }
         }
     };
@@ -220,28 +234,6 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
 #pragma unroll
             for (int s = 1; s < KSPLIT; ++s) v += red[(((s * CT) + ct) * RG + g) * 64 + lane];
             acc[g] = v;
-        }
-    }
-    if constexpr (MODE != GV_LOGITS) {
-        // cross-workgroup K split: partials to global, the last arriver of the tile sums
-        // them in split order (deterministic) and runs the epilogue
-        if (kzc > 1) {
-            f32x4* kp = (f32x4*)a.kpart + (size_t)tile * kzc * RG * 64;
-#pragma unroll
-            for (int g = 0; g < RG; ++g) kp[(kz * RG + g) * 64 + lane] = acc[g];
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            unsigned t = 0;
-            if (lane == 0) t = __hip_atomic_fetch_add(a.kcnt + tile, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-            t = __shfl(t, 0, 64);
-            if (t != (unsigned)kzc - 1) return;
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#pragma unroll
-            for (int g = 0; g < RG; ++g) {
-                f32x4 v = kp[g * 64 + lane];
-                for (int z = 1; z < kzc; ++z) v += kp[(z * RG + g) * 64 + lane];
-                acc[g] = v;
-            }
-            if (lane == 0) __hip_atomic_store(a.kcnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     const int n = n0 + fr;
@@ -375,7 +367,6 @@ void gemv_launch(const GemvArgs& a, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------ attention (decode)
-constexpr int AW = 8;                 // waves per (b, h) workgroup
 constexpr float kLog2Scale = 0.125f * 1.4426950408889634f;
 
 template <typename T> struct KVChunk;  // 8 dims of one key row per lane
@@ -391,15 +382,20 @@ template <> struct KVChunk<float> {
 };
 
 // q rows: q + (b*Tq + t)*q_ld + h*64; K/V rows of (b, h): base + ((kv*B + b)*H + h)*ctx*64
-// CAUSAL: self-attention over the cache (keys 0..pos0+t); else cross-attention (all keys)
-template <typename T, int NQ, bool CAUSAL>
-__global__ __launch_bounds__(64 * AW) void dec_attn_kernel(const T* __restrict__ q, int q_ld,
-                                                           const T* __restrict__ kv, int B, int H, int ctx,
-                                                           int n_keys_static, int Tq,
-                                                           const DecState* __restrict__ ds, T* __restrict__ out) {
+// CAUSAL: self-attention over the cache (keys 0..pos0+t); else cross-attention (all keys).
+// SPLIT: the keys of one (b, h) are cut into gridDim.y chunks, one workgroup each; every chunk
+// publishes its (m, l, o[64]) with write-through (sc1) stores, and the chunk whose arrival
+// ticket comes last merges them in chunk order (deterministic) and writes the output row.
+template <typename T, int NQ, bool CAUSAL, int AWV, bool SPLIT>
+__global__ __launch_bounds__(64 * AWV) void dec_attn_kernel(const T* __restrict__ q, int q_ld,
+                                                            const T* __restrict__ kv, int B, int H, int ctx,
+                                                            int n_keys_static, int Tq,
+                                                            const DecState* __restrict__ ds, T* __restrict__ out,
+                                                            float* __restrict__ xpart, unsigned* __restrict__ xcnt) {
     constexpr bool causal = CAUSAL;
-    __shared__ float s_m[AW][NQ], s_l[AW][NQ];
-    __shared__ float s_o[AW][NQ][64];
+    __shared__ float s_m[AWV][NQ], s_l[AWV][NQ];
+    __shared__ float s_o[AWV][NQ][64];
+    __shared__ int s_last;
     const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int slot = lane >> 3, g = lane & 7;  // key slot within a group of 8, dim group (8 dims)
@@ -425,7 +421,10 @@ __global__ __launch_bounds__(64 * AW) void dec_attn_kernel(const T* __restrict__
     // NI groups of 8 keys per block; raw K/V chunks ping-pong so the next block streams in
     constexpr int NI = (sizeof(T) == 2) ? (NQ == 1 ? 8 : 4) : (NQ == 1 ? 4 : 2);
     constexpr int KB = 8 * NI;
-    const int nblk = cdiv(n_keys, KB);
+    const int nblk_all = cdiv(n_keys, KB);
+    const int S = SPLIT ? (int)gridDim.y : 1, sp = SPLIT ? (int)blockIdx.y : 0;
+    const int per = cdiv(nblk_all, S);
+    const int blk0 = sp * per, nblk = min(nblk_all, blk0 + per);
     KVChunk<T> kA[NI], vA[NI], kB[NI], vB[NI];
     auto load_blk = [&](KVChunk<T>(&kc)[NI], KVChunk<T>(&vc)[NI], int blk) {
 #pragma unroll
@@ -473,15 +472,15 @@ __global__ __launch_bounds__(64 * AW) void dec_attn_kernel(const T* __restrict__
             m[t] = mn;
         }
     };
-    int blk = wid;
+    int blk = blk0 + wid;
     if (blk < nblk) load_blk(kA, vA, blk);
     while (blk < nblk) {
-        int nb = blk + AW;
+        int nb = blk + AWV;
         if (nb < nblk) load_blk(kB, vB, nb);
         process(kA, vA, blk * KB);
         blk = nb;
         if (blk >= nblk) break;
-        nb = blk + AW;
+        nb = blk + AWV;
         if (nb < nblk) load_blk(kA, vA, nb);
         process(kB, vB, blk * KB);
         blk = nb;
@@ -512,43 +511,87 @@ __global__ __launch_bounds__(64 * AW) void dec_attn_kernel(const T* __restrict__
     }
     __syncthreads();
     // workgroup merge: thread (t, e)
+    float M = -INFINITY, L = 0.f, O = 0.f;
+    const int t = tid >> 6, e = tid & 63;
     if (tid < 64 * Tq) {
-        const int t = tid >> 6, e = tid & 63;
-        float M = -INFINITY;
 #pragma unroll
-        for (int w = 0; w < AW; ++w) M = fmaxf(M, s_m[w][t]);
-        float L = 0.f, O = 0.f;
+        for (int w = 0; w < AWV; ++w) M = fmaxf(M, s_m[w][t]);
 #pragma unroll
-        for (int w = 0; w < AW; ++w) {
+        for (int w = 0; w < AWV; ++w) {
             if (s_m[w][t] == -INFINITY) continue;
             const float f = exp2f(s_m[w][t] - M);
             L += s_l[w][t] * f;
             O += s_o[w][t][e] * f;
         }
-        out[(size_t)(b * Tq + t) * (H * 64) + h * 64 + e] = from_f<T>(O / L);
     }
+    if constexpr (SPLIT) {
+        // publish this chunk: [bh][S][NQ][66] = {o[64], m, l}, write-through stores
+        float* pp = xpart + (((size_t)bh * S + sp) * NQ) * 66;
+        if (tid < 64 * Tq) {
+            __hip_atomic_store(pp + t * 66 + e, O, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (e == 0) {
+                __hip_atomic_store(pp + t * 66 + 64, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(pp + t * 66 + 65, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            const unsigned prev = __hip_atomic_fetch_add(xcnt + bh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = prev == (unsigned)S - 1;
+            if (last) __hip_atomic_store(xcnt + bh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = last;
+        }
+        __syncthreads();
+        if (!s_last) return;
+        if (tid < 64 * Tq) {
+            const float* pb = xpart + ((size_t)bh * S * NQ) * 66;
+            M = -INFINITY;
+            for (int c = 0; c < S; ++c)
+                M = fmaxf(M, __hip_atomic_load(pb + (c * NQ + t) * 66 + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            L = 0.f;
+            O = 0.f;
+            for (int c = 0; c < S; ++c) {
+                const float mc = __hip_atomic_load(pb + (c * NQ + t) * 66 + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (mc == -INFINITY) continue;
+                const float f = exp2f(mc - M);
+                L += __hip_atomic_load(pb + (c * NQ + t) * 66 + 65, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * f;
+                O += __hip_atomic_load(pb + (c * NQ + t) * 66 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * f;
+            }
+        }
+    }
+    if (tid < 64 * Tq) out[(size_t)(b * Tq + t) * (H * 64) + h * 64 + e] = from_f<T>(O / L);
+}
+
+template <typename T, int NQ, bool CAUSAL, int AWV, bool SPLIT>
+void dec_attn_cfg(const T* q, const T* kv, int nseq, int B_layout, int H, int ctx, int n_keys, int Tq,
+                  const DecState* ds, T* out, int S, float* xpart, unsigned* xcnt, hipStream_t st) {
+    hipLaunchKernelGGL((dec_attn_kernel<T, NQ, CAUSAL, AWV, SPLIT>), dim3(nseq * H, S), dim3(64 * AWV), 0, st, q,
+                       H * 64, kv, B_layout, H, ctx, n_keys, Tq, ds, out, xpart, xcnt);
+    SPT_LAUNCH_CHECK();
 }
 
 template <typename T>
 void dec_attn_launch(const T* q, const T* kv, int nseq, int B_layout, int H, int ctx, int n_keys, int causal, int Tq,
-                     const DecState* ds, T* out, hipStream_t st) {
-    const dim3 grid(nseq * H), blk(64 * AW);
+                     const DecState* ds, T* out, const AttnSplit& sp, hipStream_t st) {
     if (causal) {
-        if (Tq == 1)
-            hipLaunchKernelGGL((dec_attn_kernel<T, 1, true>), grid, blk, 0, st, q, H * 64, kv, B_layout, H, ctx, n_keys,
-                               Tq, ds, out);
-        else
-            hipLaunchKernelGGL((dec_attn_kernel<T, 4, true>), grid, blk, 0, st, q, H * 64, kv, B_layout, H, ctx, n_keys,
-                               Tq, ds, out);
-    } else {
-        if (Tq == 1)
-            hipLaunchKernelGGL((dec_attn_kernel<T, 1, false>), grid, blk, 0, st, q, H * 64, kv, B_layout, H, ctx, n_keys,
-                               Tq, ds, out);
-        else
-            hipLaunchKernelGGL((dec_attn_kernel<T, 4, false>), grid, blk, 0, st, q, H * 64, kv, B_layout, H, ctx, n_keys,
-                               Tq, ds, out);
+        if (Tq == 1) dec_attn_cfg<T, 1, true, 8, false>(q, kv, nseq, B_layout, H, ctx, n_keys, Tq, ds, out, 1, nullptr, nullptr, st);
+        else dec_attn_cfg<T, 4, true, 8, false>(q, kv, nseq, B_layout, H, ctx, n_keys, Tq, ds, out, 1, nullptr, nullptr, st);
+        return;
     }
-    SPT_LAUNCH_CHECK();
+    const int S = (sp.xpart && sp.xcnt) ? std::max(1, std::min(sp.splits, kAttnMaxSplit)) : 1;
+    const int waves = sp.waves == 16 ? 16 : 8;
+#define SPT_XA(NQ_, AW_)                                                                                         \
+    if (S > 1) dec_attn_cfg<T, NQ_, false, AW_, true>(q, kv, nseq, B_layout, H, ctx, n_keys, Tq, ds, out, S,     \
+                                                      sp.xpart, sp.xcnt, st);                                   \
+    else dec_attn_cfg<T, NQ_, false, AW_, false>(q, kv, nseq, B_layout, H, ctx, n_keys, Tq, ds, out, 1, nullptr, \
+                                                 nullptr, st);
+    if (Tq == 1) {
+        if (waves == 16) { SPT_XA(1, 16) } else { SPT_XA(1, 8) }
+    } else {
+        SPT_XA(4, 8)
+    }
+#undef SPT_XA
 }
 
 // ------------------------------------------------------------------ finalize
@@ -629,14 +672,7 @@ void gemv(int dtype, int mode, const GemvArgs& a_in, hipStream_t st) {
     const int ks = dtype == DT_BF16 ? 128 : 64;
     if (a_in.K % ks) throw std::runtime_error("gemv: K alignment");
     GemvArgs a = a_in;
-    // fill the chip: fewer than ~256 column-tile workgroups -> split K across workgroups
-    // (depends on N and K only, so results never depend on the batch)
     a.ksplit = 1;
-    if (mode != GV_LOGITS && a.kpart && a.kcnt) {
-        const int nwg = cdiv(a.N, 16), nss = a.K / ks;
-        a.ksplit = std::max(1, std::min(std::min(256 / nwg, kGemvMaxKSplit), nss));
-        if (a.N / 16 > kGemvMaxTiles) a.ksplit = 1;
-    }
 #define SPT_GV(T, M) \
     case M: gemv_launch<T, M>(a, st); return;
     if (dtype == DT_BF16) {
@@ -662,20 +698,21 @@ void dec_self_attn(int dtype, const void* q, const void* cache, int B, int H, in
                    void* out, hipStream_t st) {
     if (Tq < 1 || Tq > 4) throw std::runtime_error("dec_self_attn: 1..4 queries per sequence");
     if (dtype == DT_BF16)
-        dec_attn_launch<bf16>((const bf16*)q, (const bf16*)cache, B, B, H, ctx, 0, 1, Tq, ds, (bf16*)out, st);
+        dec_attn_launch<bf16>((const bf16*)q, (const bf16*)cache, B, B, H, ctx, 0, 1, Tq, ds, (bf16*)out, AttnSplit{}, st);
     else
-        dec_attn_launch<float>((const float*)q, (const float*)cache, B, B, H, ctx, 0, 1, Tq, ds, (float*)out, st);
+        dec_attn_launch<float>((const float*)q, (const float*)cache, B, B, H, ctx, 0, 1, Tq, ds, (float*)out, AttnSplit{},
+                               st);
 }
 
 void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int B_layout, int H, int T_enc, int Tq, void* out,
-                    hipStream_t st) {
+                    const AttnSplit& sp, hipStream_t st) {
     if (Tq < 1 || Tq > 4) throw std::runtime_error("dec_cross_attn: 1..4 queries per sequence");
     if (dtype == DT_BF16)
         dec_attn_launch<bf16>((const bf16*)q, (const bf16*)kv, B, B_layout, H, T_enc, T_enc, 0, Tq, nullptr, (bf16*)out,
-                              st);
+                              sp, st);
     else
         dec_attn_launch<float>((const float*)q, (const float*)kv, B, B_layout, H, T_enc, T_enc, 0, Tq, nullptr,
-                               (float*)out, st);
+                               (float*)out, sp, st);
 }
 
 void dec_finalize(int dtype, const FinalizeArgs& a, int B, hipStream_t st) {

@@ -81,13 +81,8 @@ struct GemvArgs {
     // GV_LOGITS: suppression + per-16-column-tile top-2 partials [R][n_tiles] (16 B each)
     const uint32_t* suppress; int blank0, blank1;
     void* part; int n_tiles;
-    // optional cross-workgroup K split (non-logits modes): partials [tiles][split][rows/16][64]
-    // f32x4 and one arrival counter per column tile (zero between launches)
-    float* kpart; unsigned* kcnt;
     int ksplit;                           // set by gemv()
 };
-constexpr int kGemvMaxKSplit = 4, kGemvMaxTiles = 512;
-constexpr int64_t kGemvPartBytes = (int64_t)kGemvMaxTiles * kGemvMaxKSplit * 4 * 64 * 16;
 void gemv(int dtype, int mode, const GemvArgs& a, hipStream_t st);
 // one-time per-process kernel attributes (call before any stream capture)
 void gemv_prepare(int dtype);
@@ -100,8 +95,12 @@ void dec_self_attn(int dtype, const void* q, const void* cache, int B, int H, in
                    const DecState* ds, void* out, hipStream_t st);
 // cross attention over T_enc keys, split over key chunks; partials then combine
 // kv: [2][B_layout][H][T_enc][64] (already offset to the first of the B sequences)
+// split: keys of each (b, h) over `splits` workgroups (partials [B*H][splits][Tq][66] f32 in
+// xpart, arrival tickets [B*H] in xcnt, zero before the first launch); waves per workgroup 8 or 16
+struct AttnSplit { int splits = 1; int waves = 8; float* xpart = nullptr; unsigned* xcnt = nullptr; };
+constexpr int kAttnMaxSplit = 8;
 void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int B_layout, int H, int T_enc, int Tq,
-                    void* out, hipStream_t st);
+                    void* out, const AttnSplit& split, hipStream_t st);
 
 struct FinalizeArgs {
     const void* part; int n_tiles;        // logits top-2 partials [B][n_tiles]
@@ -117,35 +116,5 @@ struct FinalizeArgs {
 // argmax reduce + record + next-token embed + step advance (replaces embed/argmax/advance)
 void dec_finalize(int dtype, const FinalizeArgs& a, int B, hipStream_t st);
 void dec_reset(DecState* ds, unsigned* arrive, hipStream_t st);
-
-// ------------------------------------------------------------------ persistent decoder pass (k_persist.hip)
-// bf16 weights; one token per sequence (Tq = 1); 1..16 sequences
-struct PersistLayer {
-    const uint16_t *qkv_w, *so_w, *cq_w, *co_w, *fc1_w, *fc2_w;
-    const float *qkv_b, *so_b, *cq_b, *co_b, *fc1_b, *fc2_b;
-    const float *ln1_w, *ln1_b, *ln2_w, *ln2_b, *ln3_w, *ln3_b;
-};
-struct PersistArgs {
-    const PersistLayer* layers; int n_layers;   // device array
-    int B, d, H, ctx, T_enc, B_layout;          // pos / step come from ds
-    int S_self, S_cross;                        // key splits (fixed per model: batch-invariant)
-    float* x;                                   // residual stream [B][d] (in/out)
-    uint16_t *q, *ao, *ff;                      // [B][d], [B][d], [B][4d]
-    uint16_t* skv; int64_t self_layer;          // self K/V [L][2][B][H][ctx][64]
-    const uint16_t* ckv; int64_t cross_layer;   // cross K/V of the first sequence, layer stride
-    float* xpart;                               // attention split partials [B*H*max(S)][66]
-    unsigned* xcnt;                             // split tickets [2][B*H] (self, cross)
-    unsigned* flags;                            // per-workgroup phase flags [G]
-    unsigned* abort_flag;                       // nonzero: a wait timed out, results invalid
-    const DecState* ds;
-    const char *ws_lo, *ws_hi, *wt_lo, *wt_hi;  // arenas (bounds checks of SPT_PERSIST_DEBUG builds)
-};
-int persist_lds_bytes(int R, int d);
-// nullptr if the shape is supported with G workgroups, else the reason
-const char* persist_check(const PersistArgs& a, int G);
-void persist_prepare();
-// a: host copy (launch geometry); a_dev: the same struct in device memory (read by the kernel)
-void dec_persist(const PersistArgs& a, const PersistArgs* a_dev, int G, hipStream_t st);
-void persist_reset(const PersistArgs& a, int G, hipStream_t st);
 
 }  // namespace spt

@@ -1,9 +1,10 @@
 // ubench.cpp -- kernel microbenchmarks (developer tool, not part of the C ABI).
 // Times the library's launchers with HIP events, back-to-back launches on one stream.
 //   ubench gemv  N K R mode ln dtype     mode: 0 bias 1 gelu 2 resid 3 qkv 4 logits
-//   ubench attn  B H ctx nkeys causal Tq dtype
+//   ubench attn  B H ctx nkeys causal Tq dtype [splits waves]
 //   ubench gemm  M N K epi dtype
-//   ubench layer B dtype                 one large-v3 decoder layer (8 launches)
+//   ubench layer B dtype [xsplits xwaves] one large-v3 decoder layer (8 launches)
+//   ubench layer2 B dtype [...]          two such chains on two streams
 //   ubench null
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -106,7 +107,14 @@ int main(int argc, char** argv) {
         HIP_CHECK(hipMemcpy(ds, &h, sizeof(h), hipMemcpyHostToDevice));
         double us;
         if (causal) us = time_us(st, iters, [&] { dec_self_attn(dt, q, kv, B, H, ctx, Tq, ds, out, st); });
-        else us = time_us(st, iters, [&] { dec_cross_attn(dt, q, kv, B, B, H, ctx, Tq, out, st); });
+        else {
+            AttnSplit xs;
+            xs.splits = ai(9, 1); xs.waves = ai(10, 8);
+            xs.xpart = (float*)dalloc((size_t)B * H * kAttnMaxSplit * 4 * 66 * 4);
+            xs.xcnt = (unsigned*)dalloc((size_t)B * H * 4);
+            us = time_us(st, iters, [&] { dec_cross_attn(dt, q, kv, B, B, H, ctx, Tq, out, xs, st); });
+            printf("  (splits=%d waves=%d) ", xs.splits, xs.waves);
+        }
         const double bytes = 2.0 * B * H * nk * 64 * esz;
         printf("attn B=%d H=%d nk=%d causal=%d Tq=%d dt=%d : %.2f us  %.0f GB/s\n", B, H, nk, causal, Tq, dt, us,
                bytes / us / 1e3);
@@ -126,8 +134,11 @@ int main(int argc, char** argv) {
                2.0 * M * N * K / us / 1e6);
         return 0;
     }
-    if (what == "layer") {
+    if (what == "layer" || what == "layer2") {
+        // layer: one large-v3 decoder layer chain at batch B
+        // layer2: two independent chains of batch B on two streams (can they overlap?)
         const int B = ai(2, 8), dt = ai(3, DT_BF16), d = 1280, H = 20, ctx = 448, T = 1500;
+        const int xsplits = ai(4, 1), xwaves = ai(5, 8);
         gemv_prepare(dt);
         const int esz = dt == DT_BF16 ? 2 : 4;
         void* wqkv = drand((size_t)3 * d * d, dt, 1, -4);
@@ -139,50 +150,100 @@ int main(int argc, char** argv) {
         float* b4 = frand(4 * d, 7, -5);
         float* lnw = frand(d, 8, -3);
         float* lnb = frand(d, 9, -4);
-        float* x = frand((size_t)B * d, 10, 0);
-        void* q = dalloc((size_t)B * d * esz);
-        void* ao = dalloc((size_t)B * d * esz);
-        void* ff = dalloc((size_t)B * 4 * d * esz);
-        void* skv = drand((size_t)2 * B * H * ctx * 64, dt, 11, 0);
-        void* ckv = drand((size_t)2 * B * H * T * 64, dt, 12, 0);
-        DecState h{128, 0};
-        HIP_CHECK(hipMemcpy(ds, &h, sizeof(h), hipMemcpyHostToDevice));
-        auto layer = [&] {
-            GemvArgs a{};
-            a.A = x; a.lda = d; a.ln_w = lnw; a.ln_b = lnb; a.R = B; a.W = wqkv; a.N = 3 * d; a.K = d; a.bias = b4;
-            a.C = q; a.ldc = d; a.cache = skv; a.cache_B = B; a.cache_H = H; a.cache_ctx = ctx; a.Tq = 1; a.st = ds;
-            gemv(dt, GV_QKV_CACHE, a, st);
-            dec_self_attn(dt, q, skv, B, H, ctx, 1, ds, ao, st);
-            a = GemvArgs{};
-            a.A = ao; a.lda = d; a.R = B; a.W = wo; a.N = d; a.K = d; a.bias = b4; a.C = x; a.ldc = d;
-            gemv(dt, GV_BIAS_RESID, a, st);
-            a = GemvArgs{};
-            a.A = x; a.lda = d; a.ln_w = lnw; a.ln_b = lnb; a.R = B; a.W = wq; a.N = d; a.K = d; a.bias = b4; a.C = q;
-            a.ldc = d;
-            gemv(dt, GV_BIAS, a, st);
-            dec_cross_attn(dt, q, ckv, B, B, H, T, 1, ao, st);
-            a = GemvArgs{};
-            a.A = ao; a.lda = d; a.R = B; a.W = wco; a.N = d; a.K = d; a.bias = b4; a.C = x; a.ldc = d;
-            gemv(dt, GV_BIAS_RESID, a, st);
-            a = GemvArgs{};
-            a.A = x; a.lda = d; a.ln_w = lnw; a.ln_b = lnb; a.R = B; a.W = w1; a.N = 4 * d; a.K = d; a.bias = b4;
-            a.C = ff; a.ldc = 4 * d;
-            gemv(dt, GV_BIAS_GELU, a, st);
-            a = GemvArgs{};
-            a.A = ff; a.lda = 4 * d; a.R = B; a.W = w2; a.N = d; a.K = 4 * d; a.bias = b4; a.C = x; a.ldc = d;
-            gemv(dt, GV_BIAS_RESID, a, st);
+        struct Chain { float* x; void *q, *ao, *ff, *skv, *ckv; DecState* ds; AttnSplit xs; };
+        auto mk = [&](uint32_t s) {
+            Chain c;
+            c.x = frand((size_t)B * d, 10 + s, 0);
+            c.q = dalloc((size_t)B * d * esz);
+            c.ao = dalloc((size_t)B * d * esz);
+            c.ff = dalloc((size_t)B * 4 * d * esz);
+            c.skv = drand((size_t)2 * B * H * ctx * 64, dt, 11 + s, 0);
+            c.ckv = drand((size_t)2 * B * H * T * 64, dt, 12 + s, 0);
+            c.ds = (DecState*)dalloc(64);
+            c.xs.splits = xsplits; c.xs.waves = xwaves;
+            c.xs.xpart = (float*)dalloc((size_t)B * H * kAttnMaxSplit * 4 * 66 * 4);
+            c.xs.xcnt = (unsigned*)dalloc((size_t)B * H * 4);
+            DecState h{128, 0};
+            HIP_CHECK(hipMemcpy(c.ds, &h, sizeof(h), hipMemcpyHostToDevice));
+            return c;
         };
-        const double eager = time_us(st, 50, layer);
-        hipGraph_t g;
-        HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-        for (int i = 0; i < 8; ++i) layer();
-        HIP_CHECK(hipStreamEndCapture(st, &g));
-        hipGraphExec_t ge;
-        HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
-        const double graph = time_us(st, 20, [&] { HIP_CHECK(hipGraphLaunch(ge, st)); }) / 8;
+        auto layer = [&](const Chain& c, hipStream_t s) {
+            GemvArgs a{};
+            a.A = c.x; a.lda = d; a.ln_w = lnw; a.ln_b = lnb; a.R = B; a.W = wqkv; a.N = 3 * d; a.K = d; a.bias = b4;
+            a.C = c.q; a.ldc = d; a.cache = c.skv; a.cache_B = B; a.cache_H = H; a.cache_ctx = ctx; a.Tq = 1; a.st = c.ds;
+            gemv(dt, GV_QKV_CACHE, a, s);
+            dec_self_attn(dt, c.q, c.skv, B, H, ctx, 1, c.ds, c.ao, s);
+            a = GemvArgs{};
+            a.A = c.ao; a.lda = d; a.R = B; a.W = wo; a.N = d; a.K = d; a.bias = b4; a.C = c.x; a.ldc = d;
+            gemv(dt, GV_BIAS_RESID, a, s);
+            a = GemvArgs{};
+            a.A = c.x; a.lda = d; a.ln_w = lnw; a.ln_b = lnb; a.R = B; a.W = wq; a.N = d; a.K = d; a.bias = b4;
+            a.C = c.q; a.ldc = d;
+            gemv(dt, GV_BIAS, a, s);
+            dec_cross_attn(dt, c.q, c.ckv, B, B, H, T, 1, c.ao, c.xs, s);
+            a = GemvArgs{};
+            a.A = c.ao; a.lda = d; a.R = B; a.W = wco; a.N = d; a.K = d; a.bias = b4; a.C = c.x; a.ldc = d;
+            gemv(dt, GV_BIAS_RESID, a, s);
+            a = GemvArgs{};
+            a.A = c.x; a.lda = d; a.ln_w = lnw; a.ln_b = lnb; a.R = B; a.W = w1; a.N = 4 * d; a.K = d; a.bias = b4;
+            a.C = c.ff; a.ldc = 4 * d;
+            gemv(dt, GV_BIAS_GELU, a, s);
+            a = GemvArgs{};
+            a.A = c.ff; a.lda = 4 * d; a.R = B; a.W = w2; a.N = d; a.K = 4 * d; a.bias = b4; a.C = c.x; a.ldc = d;
+            gemv(dt, GV_BIAS_RESID, a, s);
+        };
         const double bytes = (14.0 * d * d) * esz + 2.0 * B * H * (T + 129) * 64 * esz;
-        printf("layer B=%d dt=%d : eager %.2f us  graph %.2f us  (%.0f GB/s at graph)\n", B, dt, eager, graph,
-               bytes / graph / 1e3);
+        Chain c0 = mk(0);
+        if (what == "layer") {
+            const double eager = time_us(st, 50, [&] { layer(c0, st); });
+            hipGraph_t g;
+            HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+            for (int i = 0; i < 8; ++i) layer(c0, st);
+            HIP_CHECK(hipStreamEndCapture(st, &g));
+            hipGraphExec_t ge;
+            HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+            const double graph = time_us(st, 20, [&] { HIP_CHECK(hipGraphLaunch(ge, st)); }) / 8;
+            printf("layer B=%d dt=%d : eager %.2f us  graph %.2f us  (%.0f GB/s at graph)\n", B, dt, eager, graph,
+                   bytes / graph / 1e3);
+            return 0;
+        }
+        Chain c1 = mk(100);
+        hipStream_t s2;
+        HIP_CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+        hipEvent_t fork, join;
+        HIP_CHECK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+        // sequential: both chains on one stream; concurrent: second chain on s2
+        const double seq = time_us(st, 50, [&] { layer(c0, st); layer(c1, st); });
+        const double conc = time_us(st, 50, [&] {
+            HIP_CHECK(hipEventRecord(fork, st));
+            HIP_CHECK(hipStreamWaitEvent(s2, fork, 0));
+            layer(c0, st);
+            layer(c1, s2);
+            HIP_CHECK(hipEventRecord(join, s2));
+            HIP_CHECK(hipStreamWaitEvent(st, join, 0));
+        });
+        // graphs: one graph per stream, 8 layers each, launched on both streams at once
+        hipGraphExec_t ge[2];
+        hipStream_t ss[2] = {st, s2};
+        Chain* cc[2] = {&c0, &c1};
+        for (int k = 0; k < 2; ++k) {
+            hipGraph_t g;
+            HIP_CHECK(hipStreamBeginCapture(ss[k], hipStreamCaptureModeThreadLocal));
+            for (int i = 0; i < 8; ++i) layer(*cc[k], ss[k]);
+            HIP_CHECK(hipStreamEndCapture(ss[k], &g));
+            HIP_CHECK(hipGraphInstantiate(&ge[k], g, nullptr, nullptr, 0));
+        }
+        const double gconc = time_us(st, 20, [&] {
+            HIP_CHECK(hipEventRecord(fork, st));
+            HIP_CHECK(hipStreamWaitEvent(s2, fork, 0));
+            HIP_CHECK(hipGraphLaunch(ge[0], st));
+            HIP_CHECK(hipGraphLaunch(ge[1], s2));
+            HIP_CHECK(hipEventRecord(join, s2));
+            HIP_CHECK(hipStreamWaitEvent(st, join, 0));
+        }) / 8;
+        printf("layer2 B=%d x2 dt=%d : sequential %.2f us  two-stream eager %.2f us  two-stream graphs %.2f us (per layer pair)\n",
+               B, dt, seq, conc, gconc);
         return 0;
     }
     fprintf(stderr, "unknown bench %s\n", what.c_str());
