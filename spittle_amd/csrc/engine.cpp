@@ -123,8 +123,9 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     if ((3 * cp_ * esz_) % 128) cp_ = ((dm_.n_mels + 127) / 128) * 128;
     if (const char* g = getenv("SPT_DECODE_GROUPS")) n_groups_ = std::max(1, std::min(2, atoi(g)));
     // cross-attention key split / waves per workgroup: fixed per engine (never per batch)
-    if (const char* v = getenv("SPT_XATTN_SPLIT")) xsplit_ = std::max(1, std::min(kAttnMaxSplit, atoi(v)));
-    if (const char* v = getenv("SPT_XATTN_WAVES")) xwaves_ = atoi(v) == 16 ? 16 : 8;
+    // projection K splits (self-out: 2, fc2: 4; fixed per engine, never per batch). The pending-
+    // slab count a LayerNorm prologue sums is a kernel template constant: 2 after the self-out
+    // projection, 4 after fc2.
     select();
     HIP_CHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     ev_.resize(8);
@@ -383,9 +384,10 @@ void Engine::alloc_workspace() {
             g.done = (int*)c.take(B * 4);
             g.forced = (int*)c.take(B * ctx * 4);
             g.ds = (DecState*)c.take(sizeof(DecState));
-            g.xpart = (float*)c.take((int64_t)B * H * kAttnMaxSplit * 4 * 66 * 4);
-            g.xcnt = (unsigned*)c.take(B * H * 4);
+            g.dx2 = (float*)c.take(R * d * 4);
+            g.pend = (float*)c.take((int64_t)kMaxPend * R * d * 4);
         }
+        zero_ = (float*)c.take(R * d * 4);  // never written: the "no pending slab" operand
         if (!pass) {
             abytes_ = c.off;
             if (hipMalloc(&aarena_, abytes_) != hipSuccess) {
@@ -457,55 +459,90 @@ void Engine::run_cross_kv(int B) {
     gemm_nt(dt_, EPI_KVSPLIT, g, 1, st_);
 }
 
+// One decoder pass: 8 launches per layer.  The residual stream is f32 rows; the self-attention
+// output projection and fc2 split K over 2 / 4 workgroups and leave their results as pending
+// partial slabs, which the next LayerNorm prologue sums (x + slabs, fixed order) and writes to
+// the other x buffer: no read-modify-write of the residual there and 2-4x the workgroups on
+// the N = d projections (r1 ubench: self-out 4.8 -> 3.2 us, fc2 10.2 -> 5.7 us).  The cross-
+// attention output projection keeps the read-modify-write residual add, because slabs there
+// would land on the 320-workgroup fc1 LayerNorm prologue (+1.2 us per slab measured).
 void Engine::enqueue_decoder_pass(DecGroup& g, int B_total, int Tq, const DecodeRequest& rq, int out_cap) {
     const int d = dm_.d, H = dm_.n_head, ctx = dm_.n_text_ctx, T = dm_.n_audio_ctx, B = g.B, R = B * Tq;
     const int64_t self_layer = (int64_t)2 * B * H * ctx * 64, cross_layer = (int64_t)2 * B_total * H * T * 64;
+    const int ks = dt_ == DT_BF16 ? 128 : 64;
     hipStream_t st = g.st;
-    // g.dx already holds this pass's input embeddings (dec_embed for the prompt pass,
-    // dec_finalize of the previous pass afterwards)
+    float* xc = g.dx;   // current residual rows (dec_embed / dec_finalize wrote this pass's input here)
+    float* xo = g.dx2;  // the other buffer
+    int np = 0;         // pending slabs in g.pend
+    auto ln_input = [&](GemvArgs& a) {  // LayerNorm prologue over xc + the pending slabs
+        a.A = xc;
+        for (int p = 0; p < kMaxPend; ++p) a.pend[p] = p < np ? g.pend + (int64_t)p * R * d : zero_;
+        a.n_pend = np;
+        a.x_out = np > 0 ? xo : nullptr;
+    };
+    auto consumed = [&] {
+        if (np > 0) std::swap(xc, xo);
+        np = 0;
+    };
+    auto partial = [&](GemvArgs& a, int split) {  // a K-split projection producing pending slabs
+        a.C = g.pend; a.ldc = d; a.c_split = (int64_t)R * d;
+        a.ksplit = split;
+        if (a.K / ks < split) throw std::runtime_error("decoder projection too narrow for its K split");
+        np = split;
+    };
     for (int l = 0; l < dm_.n_dec; ++l) {
         const DecL& e = dec_[l];
         void* skv_l = (char*)g.skv + self_layer * l * esz_;
         // this group's sequences inside the [2][B_total][H][T][64] cross K/V of layer l
         const void* ckv_l = (const char*)ckv_ + (cross_layer * l + (int64_t)g.b0 * H * T * 64) * esz_;
+        // LN1 + QKV projection + self K/V append
         GemvArgs a{};
-        a.A = g.dx; a.lda = d; a.ln_w = e.ln1_w; a.ln_b = e.ln1_b; a.R = R;
+        ln_input(a); a.lda = d; a.ln_w = e.ln1_w; a.ln_b = e.ln1_b; a.R = R;
         a.W = e.qkv_w; a.N = 3 * d; a.K = d; a.bias = e.qkv_b; a.C = g.dq; a.ldc = d;
         a.cache = skv_l; a.cache_B = B; a.cache_H = H; a.cache_ctx = ctx; a.Tq = Tq; a.st = g.ds;
-        gemv(dt_, GV_QKV_CACHE, a, st);
+        gemv(dt_, GV_QKV_CACHE, A_LN, a, st);
+        consumed();
         dec_self_attn(dt_, g.dq, skv_l, B, H, ctx, Tq, g.ds, g.dao, st);
+        // self-attention output projection -> pending slabs
         a = GemvArgs{};
-        a.A = g.dao; a.lda = d; a.R = R; a.W = e.so_w; a.N = d; a.K = d; a.bias = e.so_b; a.C = g.dx; a.ldc = d;
-        gemv(dt_, GV_BIAS_RESID, a, st);
+        a.A = g.dao; a.lda = d; a.R = R; a.W = e.so_w; a.N = d; a.K = d; a.bias = e.so_b;
+        partial(a, so_split_);
+        gemv(dt_, GV_PARTIAL, A_DIRECT, a, st);
+        // LN2 + cross-Q projection
         a = GemvArgs{};
-        a.A = g.dx; a.lda = d; a.ln_w = e.ln2_w; a.ln_b = e.ln2_b; a.R = R;
+        ln_input(a); a.lda = d; a.ln_w = e.ln2_w; a.ln_b = e.ln2_b; a.R = R;
         a.W = e.cq_w; a.N = d; a.K = d; a.bias = e.cq_b; a.C = g.dq; a.ldc = d;
-        gemv(dt_, GV_BIAS, a, st);
-        AttnSplit xs;
-        xs.splits = xsplit_; xs.waves = xwaves_; xs.xpart = g.xpart; xs.xcnt = g.xcnt;
-        dec_cross_attn(dt_, g.dq, ckv_l, B, B_total, H, T, Tq, g.dao, xs, st);
+        gemv(dt_, GV_BIAS, A_LN, a, st);
+        consumed();
+        dec_cross_attn(dt_, g.dq, ckv_l, B, B_total, H, T, Tq, g.dao, st);
+        // cross output projection, residual add in place
         a = GemvArgs{};
-        a.A = g.dao; a.lda = d; a.R = R; a.W = e.co_w; a.N = d; a.K = d; a.bias = e.co_b; a.C = g.dx; a.ldc = d;
-        gemv(dt_, GV_BIAS_RESID, a, st);
+        a.A = g.dao; a.lda = d; a.R = R; a.W = e.co_w; a.N = d; a.K = d; a.bias = e.co_b; a.C = xc; a.ldc = d;
+        gemv(dt_, GV_BIAS_RESID, A_DIRECT, a, st);
+        // LN3 + fc1 + GELU
         a = GemvArgs{};
-        a.A = g.dx; a.lda = d; a.ln_w = e.ln3_w; a.ln_b = e.ln3_b; a.R = R;
+        ln_input(a); a.lda = d; a.ln_w = e.ln3_w; a.ln_b = e.ln3_b; a.R = R;
         a.W = e.fc1_w; a.N = 4 * d; a.K = d; a.bias = e.fc1_b; a.C = g.dff; a.ldc = 4 * d;
-        gemv(dt_, GV_BIAS_GELU, a, st);
+        gemv(dt_, GV_BIAS_GELU, A_LN, a, st);
+        consumed();
+        // fc2 -> pending slabs
         a = GemvArgs{};
-        a.A = g.dff; a.lda = 4 * d; a.R = R; a.W = e.fc2_w; a.N = d; a.K = 4 * d; a.bias = e.fc2_b; a.C = g.dx;
-        a.ldc = d;
-        gemv(dt_, GV_BIAS_RESID, a, st);
+        a.A = g.dff; a.lda = 4 * d; a.R = R; a.W = e.fc2_w; a.N = d; a.K = 4 * d; a.bias = e.fc2_b;
+        partial(a, fc2_split_);
+        gemv(dt_, GV_PARTIAL, A_DIRECT, a, st);
     }
     const Specials sp = specials_for(dm_.n_vocab);
     const int n_tiles = (dm_.n_vocab + 15) / 16;
     GemvArgs a{};
-    a.A = g.dx; a.lda = Tq * d; a.a_row0 = (Tq - 1) * d; a.ln_w = lnf_w_; a.ln_b = lnf_b_; a.R = B;
+    ln_input(a);  // final LayerNorm of the last token of each sequence; the combined rows are not needed
+    a.x_out = nullptr;
+    a.lda = Tq * d; a.a_row0 = (Tq - 1) * d; a.ln_w = lnf_w_; a.ln_b = lnf_b_; a.R = B;
     a.W = tok_emb_; a.N = dm_.n_vocab; a.K = d; a.C = g.logits; a.ldc = dm_.n_vocab; a.st = g.ds;
     a.suppress = suppress_;
     a.blank0 = (rq.flags & 1u) ? sp.eot : -1;
     a.blank1 = (rq.flags & 1u) ? 220 : -1;
     a.part = g.part; a.n_tiles = n_tiles;
-    gemv(dt_, GV_LOGITS, a, st);
+    gemv(dt_, GV_LOGITS, A_LN, a, st);
     FinalizeArgs f{};
     f.part = g.part; f.n_tiles = n_tiles;
     f.eot = sp.eot; f.ignore_eot = (rq.flags & 4u) ? 1 : 0; f.n_vocab = dm_.n_vocab;
@@ -745,11 +782,7 @@ double Engine::probe(int kind, int iters, double* work, int* is_flops) {
     *is_flops = 0;
     switch (kind) {
         case 0:  // cross-attention of decoder layer 0 over this group's cross K/V
-            launch = [&] {
-                AttnSplit xs;
-                xs.splits = xsplit_; xs.waves = xwaves_; xs.xpart = g.xpart; xs.xcnt = g.xcnt;
-                dec_cross_attn(dt_, g.dq, ckv_, Bg, B, H, T, 1, g.dao, xs, st_);
-            };
+            launch = [&] { dec_cross_attn(dt_, g.dq, ckv_, Bg, B, H, T, 1, g.dao, st_); };
             *work = 2.0 * Bg * H * T * 64 * esz_;
             break;
         case 1:
@@ -764,9 +797,10 @@ double Engine::probe(int kind, int iters, double* work, int* is_flops) {
             launch = [&] {
                 GemvArgs a{};
                 a.A = g.dx; a.lda = d; a.ln_w = lnf_w_; a.ln_b = lnf_b_; a.R = Bg;
+                for (int p = 0; p < kMaxPend; ++p) a.pend[p] = zero_;
                 a.W = tok_emb_; a.N = V; a.K = d; a.C = g.logits; a.ldc = V; a.st = g.ds;
                 a.suppress = suppress_; a.blank0 = a.blank1 = -1; a.part = g.part; a.n_tiles = (V + 15) / 16;
-                gemv(dt_, GV_LOGITS, a, st_);
+                gemv(dt_, GV_LOGITS, A_LN, a, st_);
             };
             *work = (double)V * d * esz_;
             break;
@@ -775,8 +809,9 @@ double Engine::probe(int kind, int iters, double* work, int* is_flops) {
             launch = [&] {
                 GemvArgs a{};
                 a.A = g.dx; a.lda = d; a.ln_w = dec_[0].ln3_w; a.ln_b = dec_[0].ln3_b; a.R = Bg;
+                for (int p = 0; p < kMaxPend; ++p) a.pend[p] = zero_;
                 a.W = dec_[0].fc1_w; a.N = 4 * d; a.K = d; a.bias = dec_[0].fc1_b; a.C = g.dff; a.ldc = 4 * d;
-                gemv(dt_, GV_BIAS_GELU, a, st_);
+                gemv(dt_, GV_BIAS_GELU, A_LN, a, st_);
             };
             *work = 4.0 * d * d * esz_;
             break;

@@ -91,8 +91,8 @@ private:
         int *tok_in = nullptr, *out_tok = nullptr, *done = nullptr, *forced = nullptr;
         float *out_t1 = nullptr, *out_t2 = nullptr;
         DecState* ds = nullptr;
-        float* xpart = nullptr;       // cross-attention key-split partials
-        unsigned* xcnt = nullptr;     // ... and their arrival tickets [B*H]
+        float* dx2 = nullptr;         // second residual buffer (ping-pong with dx)
+        float* pend = nullptr;        // pending partial slabs [kMaxPend][R][d]
         std::map<GraphKey, hipGraphExec_t> graphs;
     };
 
@@ -113,7 +113,7 @@ private:
     uint64_t seed_;
     int esz_;     // bytes per weight / activation element
     int cp_;      // padded mel channels (conv1 K = 3 * cp_)
-    int xsplit_ = 1, xwaves_ = 8;  // cross-attention key split, waves per workgroup
+    static constexpr int so_split_ = 2, fc2_split_ = 4;  // K splits of the self-out / fc2 projections
     int n_groups_ = 1;  // SPT_DECODE_GROUPS=2 splits the batch over two streams
     hipStream_t st_ = nullptr;
     std::vector<hipEvent_t> ev_;
@@ -151,6 +151,7 @@ private:
     void* ckv_ = nullptr;   // cross K/V [L][2][B][H][1500][64]
     uint32_t* suppress_ = nullptr;
     double* scratch_ = nullptr;
+    float* zero_ = nullptr;  // [R][d] zeros: the operand of an unused pending slab
     std::vector<DecGroup> groups_;
 
     std::vector<uint32_t> host_suppress_;

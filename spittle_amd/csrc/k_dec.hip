@@ -87,12 +87,25 @@ __device__ __forceinline__ F load_w(const F* p) {
 
 // NWV waves; CT column tiles of 16 per workgroup; KSPLIT = NWV / CT waves share a tile
 // and split its K.  Each wave keeps up to MAXJ super-steps of weights in flight.
-template <typename T, int MODE, bool LN, int RG, int NWV, int CT, int MAXJ>
+// blockIdx.y splits K across workgroups (GV_PARTIAL only: each split writes its own
+// partial slab, summed in split order by the consumer's A_LN prologue).
+// ASRC selects the A operand:
+//   A_DIRECT  activation rows [R][lda] of type T read straight into MFMA fragments;
+//   A_LN      LayerNorm of the f32 residual rows x + pend[0..np-1] (the pending partial slabs
+//             of the previous GV_PARTIAL launch), staged as a bank-padded LDS image;
+//             workgroup (0, 0) also writes the combined rows to x_out.
+// kernel-side A source codes: A_DIRECT, or LN_SRC(np) = A_LN with np pending slabs (0, 2, 4)
+constexpr int LN_SRC(int np) { return 16 + np; }
+constexpr bool is_ln(int asrc) { return asrc >= 16; }
+constexpr int ln_np(int asrc) { return asrc - 16; }
+
+template <typename T, int MODE, int ASRC, int RG, int NWV, int CT, int MAXJ>
 __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
     constexpr int KS = GV<T>::KS;
     constexpr int EPL = KS / 4;          // elements per lane per super-step (64 bytes)
     constexpr int CPE = 16 / sizeof(T);  // elements per 16-byte chunk
     constexpr int KSPLIT = NWV / CT;
+    constexpr bool IMG = ASRC != A_DIRECT;
     typedef typename GV<T>::frag frag;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -119,32 +132,54 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
             }
         }
     };
-    // LayerNorm input rows are fetched BEFORE the weight stream: loads retire in issue
-    // order, so the prologue then waits only for its own row, not for the weights
-    float4 x0[6];
-    if constexpr (LN) {
+    // LayerNorm input rows (x and the pending slabs) are fetched BEFORE the weight stream:
+    // loads retire in issue order, so the prologue then waits only for its own row.  The slab
+    // count is a template constant: loads under a runtime select are serialised by hipcc.
+    constexpr int NP = is_ln(ASRC) ? ln_np(ASRC) : 0;
+    float4 x0[NP + 1][6];
+    if constexpr (is_ln(ASRC)) {
         if (wid < a.R) {
-            const float* xr = (const float*)a.A + (size_t)wid * a.lda + a.a_row0;
+            const size_t ro = (size_t)wid * a.lda + a.a_row0;
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
                 const int k = lane * 4 + 256 * i;
-                if (k < K) x0[i] = *(const float4*)(xr + k);
+                if (k < K) {
+                    x0[0][i] = *(const float4*)((const float*)a.A + ro + k);
+#pragma unroll
+                    for (int p = 0; p < NP; ++p) x0[p + 1][i] = *(const float4*)(a.pend[p] + ro + k);
+                }
             }
         }
     }
-    load_chunk(0);  // the first weight fetch overlaps the LayerNorm prologue
+    load_chunk(0);  // the first weight fetch overlaps the prologue
 
-    if constexpr (LN) {
+    if constexpr (is_ln(ASRC)) {
         T* img = (T*)smem;
+        const bool wr_x = a.x_out && blockIdx.x == 0 && blockIdx.y == 0;
         for (int r = wid; r < a.R; r += NWV) {
-            const float* xr = (const float*)a.A + (size_t)r * a.lda + a.a_row0;
+            const size_t ro = (size_t)r * a.lda + a.a_row0;
             float4 v[6];
             float s = 0.f;
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
                 const int k = lane * 4 + 256 * i;
                 if (k < K) {
-                    v[i] = r == wid ? x0[i] : *(const float4*)(xr + k);
+                    float4 u[NP + 1];
+                    if (r == wid) {
+#pragma unroll
+                        for (int p = 0; p <= NP; ++p) u[p] = x0[p][i];
+                    } else {
+                        u[0] = *(const float4*)((const float*)a.A + ro + k);
+#pragma unroll
+                        for (int p = 0; p < NP; ++p) u[p + 1] = *(const float4*)(a.pend[p] + ro + k);
+                    }
+                    // x + p0 + p1 + ..., always in this order (deterministic)
+                    v[i] = u[0];
+#pragma unroll
+                    for (int p = 1; p <= NP; ++p) {
+                        v[i].x += u[p].x; v[i].y += u[p].y; v[i].z += u[p].z; v[i].w += u[p].w;
+                    }
+                    if (wr_x) *(float4*)(a.x_out + ro + k) = v[i];
                     s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
                 }
             }
@@ -192,7 +227,7 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
                 if (row < a.R) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
-                        if constexpr (LN)
+                        if constexpr (IMG)
                             af[i] = *(const frag*)((const T*)smem + (size_t)row * lds_ld + kb + i * CPE);
                         else
                             af[i] = *(const frag*)((const T*)a.A + (size_t)row * a.lda + a.a_row0 + kb + i * CPE);
@@ -222,8 +257,8 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
 
     // cross-wave K reduction (waves sharing a column tile)
     if constexpr (KSPLIT > 1) {
-        f32x4* red = (f32x4*)(smem + (LN ? gv_img_bytes(a.R, K, sizeof(T)) : 0));
-        if (LN) __syncthreads();  // the LN image region is not reused, but keep waves in step
+        f32x4* red = (f32x4*)(smem + (IMG ? gv_img_bytes(a.R, K, sizeof(T)) : 0));
+        if (IMG) __syncthreads();  // the image region is not reused, but keep waves in step
 #pragma unroll
         for (int g = 0; g < RG; ++g) red[(wid * RG + g) * 64 + lane] = acc[g];
         __syncthreads();
@@ -264,7 +299,7 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
         return;
     }
     if (n >= a.N) return;
-    const float bv = a.bias ? a.bias[n] : 0.0f;
+    const float bv = (a.bias && kz == 0) ? a.bias[n] : 0.0f;
 #pragma unroll
     for (int g = 0; g < RG; ++g) {
 #pragma unroll
@@ -276,6 +311,8 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
                 ((T*)a.C)[(size_t)row * a.ldc + n] = from_f<T>(y);
             } else if constexpr (MODE == GV_BIAS_GELU) {
                 ((T*)a.C)[(size_t)row * a.ldc + n] = from_f<T>(gelu_tanh(y));
+            } else if constexpr (MODE == GV_PARTIAL) {
+                ((float*)a.C + (size_t)kz * a.c_split)[(size_t)row * a.ldc + n] = y;
             } else if constexpr (MODE == GV_BIAS_RESID) {
                 ((float*)a.C)[(size_t)row * a.ldc + n] += y;
             } else if constexpr (MODE == GV_QKV_CACHE) {
@@ -296,77 +333,88 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
     }
 }
 
-template <typename T, int MODE, bool LN, int RG, int NWV, int CT, int MAXJ>
+template <typename T, int MODE, int ASRC, int RG, int NWV, int CT, int MAXJ>
 void gemv_attr() {
     const int red = NWV * RG * 64 * (int)sizeof(f32x4);
-    HIP_CHECK(hipFuncSetAttribute((const void*)gemv_kernel<T, MODE, LN, RG, NWV, CT, MAXJ>,
+    HIP_CHECK(hipFuncSetAttribute((const void*)gemv_kernel<T, MODE, ASRC, RG, NWV, CT, MAXJ>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, GV_LDS_BYTES + red));
 }
 
-template <typename T, int MODE, bool LN, int RG, int NWV, int CT, int MAXJ>
+template <typename T, int MODE, int ASRC, int RG, int NWV, int CT, int MAXJ>
 void gemv_launch_cfg(const GemvArgs& a, hipStream_t st) {
     const int red = NWV * RG * 64 * (int)sizeof(f32x4);
-    const int lds = (LN ? gv_img_bytes(a.R, a.K, sizeof(T)) : 0) + (NWV / CT > 1 ? red : 0);
-    hipLaunchKernelGGL((gemv_kernel<T, MODE, LN, RG, NWV, CT, MAXJ>), dim3(cdiv(a.N, 16 * CT), a.ksplit),
+    const int lds = (ASRC != A_DIRECT ? gv_img_bytes(a.R, a.K, sizeof(T)) : 0) + (NWV / CT > 1 ? red : 0);
+    hipLaunchKernelGGL((gemv_kernel<T, MODE, ASRC, RG, NWV, CT, MAXJ>), dim3(cdiv(a.N, 16 * CT), a.ksplit),
                        dim3(64 * NWV), lds, st, a);
     SPT_LAUNCH_CHECK();
 }
 
-// geometry per shape (nss = super-steps of K): every wave's whole K slice in flight
-// at once where registers allow, and at most one workgroup round on 256 CUs
+// geometry per shape (nss = super-steps of K per workgroup): every wave's whole K slice in
+// flight at once where registers allow; logits: 4 column tiles x 1 wave each (4, 4, 4)
 #define SPT_GV_CONFIGS(X)   \
-    X(4, 4, 4)  /* logits: 4 column tiles x 1 wave each */ \
-    X(8, 1, 1)  /* nss <= 8  */ \
+    X(4, 1, 2)  /* nss <= 8  */ \
     X(8, 1, 2)  /* nss <= 16 */ \
     X(16, 1, 3) /* nss <= 48 */
 
+// the (mode, A source) pairs the decoder uses
+#define SPT_GV_PAIRS(X)                 \
+    X(GV_QKV_CACHE, LN_SRC(0))          \
+    X(GV_QKV_CACHE, LN_SRC(4))          \
+    X(GV_BIAS, LN_SRC(2))               \
+    X(GV_BIAS_GELU, LN_SRC(0))          \
+    X(GV_LOGITS, LN_SRC(0))             \
+    X(GV_LOGITS, LN_SRC(4))             \
+    X(GV_PARTIAL, A_DIRECT)             \
+    X(GV_BIAS_RESID, A_DIRECT)
+
 // > 64 KiB of dynamic LDS must be enabled per kernel, outside any stream capture
-template <typename T, int MODE, bool LN>
+template <typename T, int MODE, int ASRC>
 void gemv_attr_all() {
-#define SPT_ATTR(NWV, CT, MAXJ)                        \
-    gemv_attr<T, MODE, LN, 1, NWV, CT, MAXJ>();         \
-    gemv_attr<T, MODE, LN, 2, NWV, CT, MAXJ>();         \
-    gemv_attr<T, MODE, LN, 4, NWV, CT, MAXJ>();
-    SPT_GV_CONFIGS(SPT_ATTR)
+#define SPT_ATTR(NWV, CT, MAXJ)                          \
+    gemv_attr<T, MODE, ASRC, 1, NWV, CT, MAXJ>();         \
+    gemv_attr<T, MODE, ASRC, 2, NWV, CT, MAXJ>();         \
+    gemv_attr<T, MODE, ASRC, 4, NWV, CT, MAXJ>();
+    if constexpr (MODE == GV_LOGITS) {
+        SPT_ATTR(4, 4, 4)
+    } else if constexpr (ASRC == A_DIRECT) {
+        SPT_GV_CONFIGS(SPT_ATTR)
+    } else {
+        SPT_ATTR(4, 1, 2)
+        SPT_ATTR(8, 1, 2)
+    }
 #undef SPT_ATTR
 }
 template <typename T>
 void gemv_attr_modes() {
-    gemv_attr_all<T, GV_BIAS, true>(); gemv_attr_all<T, GV_BIAS, false>();
-    gemv_attr_all<T, GV_BIAS_GELU, true>(); gemv_attr_all<T, GV_BIAS_GELU, false>();
-    gemv_attr_all<T, GV_BIAS_RESID, true>(); gemv_attr_all<T, GV_BIAS_RESID, false>();
-    gemv_attr_all<T, GV_QKV_CACHE, true>(); gemv_attr_all<T, GV_QKV_CACHE, false>();
-    gemv_attr_all<T, GV_LOGITS, true>(); gemv_attr_all<T, GV_LOGITS, false>();
+#define SPT_PAIR(M, S) gemv_attr_all<T, M, S>();
+    SPT_GV_PAIRS(SPT_PAIR)
+#undef SPT_PAIR
 }
 
-template <typename T, int MODE, bool LN, int RG>
+template <typename T, int MODE, int ASRC, int RG>
 void gemv_launch_rg(const GemvArgs& a, hipStream_t st) {
     const int nss = cdiv(a.K / GV<T>::KS, a.ksplit);  // super-steps per workgroup
-    if (a.N >= 16384) gemv_launch_cfg<T, MODE, LN, RG, 4, 4, 4>(a, st);
-    else if (nss <= 8) gemv_launch_cfg<T, MODE, LN, RG, 8, 1, 1>(a, st);
-    else if (nss <= 16) gemv_launch_cfg<T, MODE, LN, RG, 8, 1, 2>(a, st);
-    else if (nss <= 48) gemv_launch_cfg<T, MODE, LN, RG, 16, 1, 3>(a, st);
-    else throw std::runtime_error("gemv: K too large");
-}
-
-template <typename T, int MODE>
-void gemv_launch(const GemvArgs& a, hipStream_t st) {
-    const bool ln = a.ln_w != nullptr;
-    if (ln && (gv_img_bytes(a.R, a.K, sizeof(T)) > GV_LDS_BYTES || a.K > 1536))
-        throw std::runtime_error("gemv: LayerNorm image exceeds LDS budget");
-    if (a.R <= 16) {
-        if (ln) gemv_launch_rg<T, MODE, true, 1>(a, st);
-        else gemv_launch_rg<T, MODE, false, 1>(a, st);
-    } else if (a.R <= 32) {
-        if (ln) gemv_launch_rg<T, MODE, true, 2>(a, st);
-        else gemv_launch_rg<T, MODE, false, 2>(a, st);
+    if constexpr (MODE == GV_LOGITS) {
+        gemv_launch_cfg<T, MODE, ASRC, RG, 4, 4, 4>(a, st);
     } else {
-        if (ln) gemv_launch_rg<T, MODE, true, 4>(a, st);
-        else gemv_launch_rg<T, MODE, false, 4>(a, st);
+        if (nss <= 8) gemv_launch_cfg<T, MODE, ASRC, RG, 4, 1, 2>(a, st);
+        else if (nss <= 16) gemv_launch_cfg<T, MODE, ASRC, RG, 8, 1, 2>(a, st);
+        else if constexpr (ASRC == A_DIRECT) {  // 16 waves: no room for a staged A image's registers
+            if (nss <= 48) gemv_launch_cfg<T, MODE, ASRC, RG, 16, 1, 3>(a, st);
+            else throw std::runtime_error("gemv: K too large");
+        } else throw std::runtime_error("gemv: K too large for a staged A operand");
     }
 }
 
+template <typename T, int MODE, int ASRC>
+void gemv_launch(const GemvArgs& a, hipStream_t st) {
+    if (a.R <= 16) gemv_launch_rg<T, MODE, ASRC, 1>(a, st);
+    else if (a.R <= 32) gemv_launch_rg<T, MODE, ASRC, 2>(a, st);
+    else gemv_launch_rg<T, MODE, ASRC, 4>(a, st);
+}
+
 // ------------------------------------------------------------------ attention (decode)
+constexpr int AW = 8;  // waves per attention workgroup
 constexpr float kLog2Scale = 0.125f * 1.4426950408889634f;
 
 template <typename T> struct KVChunk;  // 8 dims of one key row per lane
@@ -381,60 +429,42 @@ template <> struct KVChunk<float> {
     __device__ __forceinline__ float at(int e) const { return e < 4 ? a[e] : b[e - 4]; }
 };
 
-// q rows: q + (b*Tq + t)*q_ld + h*64; K/V rows of (b, h): base + ((kv*B + b)*H + h)*ctx*64
-// CAUSAL: self-attention over the cache (keys 0..pos0+t); else cross-attention (all keys).
-// SPLIT: the keys of one (b, h) are cut into gridDim.y chunks, one workgroup each; every chunk
-// publishes its (m, l, o[64]) with write-through (sc1) stores, and the chunk whose arrival
-// ticket comes last merges them in chunk order (deterministic) and writes the output row.
-template <typename T, int NQ, bool CAUSAL, int AWV, bool SPLIT>
-__global__ __launch_bounds__(64 * AWV) void dec_attn_kernel(const T* __restrict__ q, int q_ld,
-                                                            const T* __restrict__ kv, int B, int H, int ctx,
-                                                            int n_keys_static, int Tq,
-                                                            const DecState* __restrict__ ds, T* __restrict__ out,
-                                                            float* __restrict__ xpart, unsigned* __restrict__ xcnt) {
-    constexpr bool causal = CAUSAL;
-    __shared__ float s_m[AWV][NQ], s_l[AWV][NQ];
-    __shared__ float s_o[AWV][NQ][64];
-    __shared__ int s_last;
-    const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int slot = lane >> 3, g = lane & 7;  // key slot within a group of 8, dim group (8 dims)
-    const int pos0 = causal ? ds->pos0 : 0;
-    const int n_keys = causal ? pos0 + Tq : n_keys_static;
-    const T* Kb = kv + (((size_t)0 * B + b) * H + h) * (size_t)ctx * 64 + 8 * g;
-    const T* Vb = kv + (((size_t)1 * B + b) * H + h) * (size_t)ctx * 64 + 8 * g;
-
-    float qv[NQ][8], m[NQ], l[NQ], o[NQ][8];
-    int lim[NQ];
-#pragma unroll
-    for (int t = 0; t < NQ; ++t) {
-        const int tt = t < Tq ? t : Tq - 1;
-        const T* qr = q + (size_t)(b * Tq + tt) * q_ld + h * 64 + 8 * g;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) qv[t][e] = to_f<T>(qr[e]) * kLog2Scale;
-        m[t] = -INFINITY;
-        l[t] = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[t][e] = 0.f;
-        lim[t] = causal ? pos0 + tt + 1 : n_keys;
-    }
-    // NI groups of 8 keys per block; raw K/V chunks ping-pong so the next block streams in
-    constexpr int NI = (sizeof(T) == 2) ? (NQ == 1 ? 8 : 4) : (NQ == 1 ? 4 : 2);
-    constexpr int KB = 8 * NI;
-    const int nblk_all = cdiv(n_keys, KB);
-    const int S = SPLIT ? (int)gridDim.y : 1, sp = SPLIT ? (int)blockIdx.y : 0;
-    const int per = cdiv(nblk_all, S);
-    const int blk0 = sp * per, nblk = min(nblk_all, blk0 + per);
+// One wave's share of flash-decoding over key blocks [blk0, nblk) of one (b, h): 8 lanes per
+// key (8 dims each, fully coalesced 16-byte sweeps of the K/V rows), online softmax in exp2
+// space; raw K/V chunks ping-pong so the next block streams in during the current one.
+// qv is pre-scaled by log2(e)/8.  Leaves (m, l, o) per query in the calling lanes.
+template <typename T, int NQ>
+struct AttnWave {
+    static constexpr int NI = (sizeof(T) == 2) ? (NQ == 1 ? 8 : 4) : (NQ == 1 ? 4 : 2);
+    static constexpr int KB = 8 * NI;  // keys per block
     KVChunk<T> kA[NI], vA[NI], kB[NI], vB[NI];
-    auto load_blk = [&](KVChunk<T>(&kc)[NI], KVChunk<T>(&vc)[NI], int blk) {
+    float m[NQ], l[NQ], o[NQ][8];
+    const T *Kb, *Vb;
+    int n_keys, slot;
+
+    __device__ __forceinline__ void init(const T* K, const T* V, int nk, int lane) {
+        slot = lane >> 3;
+        Kb = K;
+        Vb = V;
+        n_keys = nk;
+#pragma unroll
+        for (int t = 0; t < NQ; ++t) {
+            m[t] = -INFINITY;
+            l[t] = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[t][e] = 0.f;
+        }
+    }
+    __device__ __forceinline__ void load_blk(KVChunk<T> (&kc)[NI], KVChunk<T> (&vc)[NI], int blk) {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             const int key = min(blk * KB + 8 * i + slot, n_keys - 1);
             kc[i].load(Kb + (size_t)key * 64);
             vc[i].load(Vb + (size_t)key * 64);
         }
-    };
-    auto process = [&](const KVChunk<T>(&kc)[NI], const KVChunk<T>(&vc)[NI], int kbase) {
+    }
+    __device__ __forceinline__ void process(const KVChunk<T> (&kc)[NI], const KVChunk<T> (&vc)[NI], int kbase,
+                                            const float (&qv)[NQ][8], const int (&lim)[NQ], int Tq) {
 #pragma unroll
         for (int t = 0; t < NQ; ++t) {
             if (t >= Tq) break;
@@ -471,127 +501,141 @@ __global__ __launch_bounds__(64 * AWV) void dec_attn_kernel(const T* __restrict_
             l[t] = l[t] * alpha + ls;
             m[t] = mn;
         }
-    };
-    int blk = blk0 + wid;
-    if (blk < nblk) load_blk(kA, vA, blk);
-    while (blk < nblk) {
-        int nb = blk + AWV;
-        if (nb < nblk) load_blk(kB, vB, nb);
-        process(kA, vA, blk * KB);
-        blk = nb;
-        if (blk >= nblk) break;
-        nb = blk + AWV;
-        if (nb < nblk) load_blk(kA, vA, nb);
-        process(kB, vB, blk * KB);
-        blk = nb;
     }
-    // wave merge: sum l and o over the 8 key slots (m is wave-uniform)
+    // blocks blk0 + w, blk0 + w + AW, ... below nblk; the first block may already be in flight
+    __device__ __forceinline__ void run(int blk, int nblk, bool first_loaded, const float (&qv)[NQ][8],
+                                        const int (&lim)[NQ], int Tq) {
+        if (blk < nblk && !first_loaded) load_blk(kA, vA, blk);
+        while (blk < nblk) {
+            int nb = blk + AW;
+            if (nb < nblk) load_blk(kB, vB, nb);
+            process(kA, vA, blk * KB, qv, lim, Tq);
+            blk = nb;
+            if (blk >= nblk) break;
+            nb = blk + AW;
+            if (nb < nblk) load_blk(kA, vA, nb);
+            process(kB, vB, blk * KB, qv, lim, Tq);
+            blk = nb;
+        }
+    }
+    // sum l and o over the 8 key slots of the wave (m is wave-uniform) into LDS
+    __device__ __forceinline__ void to_lds(float (*s_m)[NQ], float (*s_l)[NQ], float (*s_o)[NQ][64], int wid,
+                                           int lane) {
+        const int g = lane & 7;
+#pragma unroll
+        for (int t = 0; t < NQ; ++t) {
+            float lt = l[t];
+            lt += __shfl_xor(lt, 8, 64);
+            lt += __shfl_xor(lt, 16, 64);
+            lt += __shfl_xor(lt, 32, 64);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                float v = o[t][e];
+                v += __shfl_xor(v, 8, 64);
+                v += __shfl_xor(v, 16, 64);
+                v += __shfl_xor(v, 32, 64);
+                o[t][e] = v;
+            }
+            if (lane < 8) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) s_o[wid][t][8 * g + e] = o[t][e];
+            }
+            if (lane == 0) {
+                s_m[wid][t] = m[t];
+                s_l[wid][t] = lt;
+            }
+        }
+    }
+};
+
+// workgroup merge of the AW waves' (m, l, o) for query t, element e -> (M, L, O)
+template <int NQ>
+__device__ __forceinline__ void attn_merge(const float (*s_m)[NQ], const float (*s_l)[NQ], const float (*s_o)[NQ][64],
+                                           int t, int e, float& M, float& L, float& O) {
+    M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < AW; ++w) M = fmaxf(M, s_m[w][t]);
+    L = 0.f;
+    O = 0.f;
+#pragma unroll
+    for (int w = 0; w < AW; ++w) {
+        if (s_m[w][t] == -INFINITY) continue;
+        const float f = exp2f(s_m[w][t] - M);
+        L += s_l[w][t] * f;
+        O += s_o[w][t][e] * f;
+    }
+}
+
+// Self-attention over the cache (keys 0..pos0+t), one workgroup per (b, h).
+// q rows: q + (b*Tq + t)*q_ld + h*64; K/V rows of (b, h): base + ((kv*B + b)*H + h)*ctx*64.
+template <typename T, int NQ>
+__global__ __launch_bounds__(64 * AW) void self_attn_kernel(const T* __restrict__ q, int q_ld,
+                                                            const T* __restrict__ kv, int B, int H, int ctx, int Tq,
+                                                            const DecState* __restrict__ ds, T* __restrict__ out) {
+    __shared__ float s_m[AW][NQ], s_l[AW][NQ];
+    __shared__ float s_o[AW][NQ][64];
+    const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane & 7;
+    const int pos0 = ds->pos0;
+    const int n_keys = pos0 + Tq;
+    AttnWave<T, NQ> aw;
+    aw.init(kv + (((size_t)0 * B + b) * H + h) * (size_t)ctx * 64 + 8 * g,
+            kv + (((size_t)1 * B + b) * H + h) * (size_t)ctx * 64 + 8 * g, n_keys, lane);
+    float qv[NQ][8];
+    int lim[NQ];
 #pragma unroll
     for (int t = 0; t < NQ; ++t) {
-        float lt = l[t];
-        lt += __shfl_xor(lt, 8, 64);
-        lt += __shfl_xor(lt, 16, 64);
-        lt += __shfl_xor(lt, 32, 64);
+        const int tt = t < Tq ? t : Tq - 1;
+        const T* qr = q + (size_t)(b * Tq + tt) * q_ld + h * 64 + 8 * g;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            float v = o[t][e];
-            v += __shfl_xor(v, 8, 64);
-            v += __shfl_xor(v, 16, 64);
-            v += __shfl_xor(v, 32, 64);
-            o[t][e] = v;
-        }
-        if (lane < 8) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) s_o[wid][t][8 * g + e] = o[t][e];
-        }
-        if (lane == 0) {
-            s_m[wid][t] = m[t];
-            s_l[wid][t] = lt;
-        }
+        for (int e = 0; e < 8; ++e) qv[t][e] = to_f<T>(qr[e]) * kLog2Scale;
+        lim[t] = pos0 + tt + 1;
     }
+    aw.run(wid, cdiv(n_keys, AttnWave<T, NQ>::KB), false, qv, lim, Tq);
+    aw.to_lds(s_m, s_l, s_o, wid, lane);
     __syncthreads();
-    // workgroup merge: thread (t, e)
-    float M = -INFINITY, L = 0.f, O = 0.f;
-    const int t = tid >> 6, e = tid & 63;
     if (tid < 64 * Tq) {
-#pragma unroll
-        for (int w = 0; w < AWV; ++w) M = fmaxf(M, s_m[w][t]);
-#pragma unroll
-        for (int w = 0; w < AWV; ++w) {
-            if (s_m[w][t] == -INFINITY) continue;
-            const float f = exp2f(s_m[w][t] - M);
-            L += s_l[w][t] * f;
-            O += s_o[w][t][e] * f;
-        }
+        const int t = tid >> 6, e = tid & 63;
+        float M, L, O;
+        attn_merge<NQ>(s_m, s_l, s_o, t, e, M, L, O);
+        out[(size_t)(b * Tq + t) * (H * 64) + h * 64 + e] = from_f<T>(O / L);
     }
-    if constexpr (SPLIT) {
-        // publish this chunk: [bh][S][NQ][66] = {o[64], m, l}, write-through stores
-        float* pp = xpart + (((size_t)bh * S + sp) * NQ) * 66;
-        if (tid < 64 * Tq) {
-            __hip_atomic_store(pp + t * 66 + e, O, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (e == 0) {
-                __hip_atomic_store(pp + t * 66 + 64, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(pp + t * 66 + 65, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-            const unsigned prev = __hip_atomic_fetch_add(xcnt + bh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int last = prev == (unsigned)S - 1;
-            if (last) __hip_atomic_store(xcnt + bh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_last = last;
-        }
-        __syncthreads();
-        if (!s_last) return;
-        if (tid < 64 * Tq) {
-            const float* pb = xpart + ((size_t)bh * S * NQ) * 66;
-            M = -INFINITY;
-            for (int c = 0; c < S; ++c)
-                M = fmaxf(M, __hip_atomic_load(pb + (c * NQ + t) * 66 + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            L = 0.f;
-            O = 0.f;
-            for (int c = 0; c < S; ++c) {
-                const float mc = __hip_atomic_load(pb + (c * NQ + t) * 66 + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (mc == -INFINITY) continue;
-                const float f = exp2f(mc - M);
-                L += __hip_atomic_load(pb + (c * NQ + t) * 66 + 65, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * f;
-                O += __hip_atomic_load(pb + (c * NQ + t) * 66 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * f;
-            }
-        }
-    }
-    if (tid < 64 * Tq) out[(size_t)(b * Tq + t) * (H * 64) + h * 64 + e] = from_f<T>(O / L);
 }
 
-template <typename T, int NQ, bool CAUSAL, int AWV, bool SPLIT>
-void dec_attn_cfg(const T* q, const T* kv, int nseq, int B_layout, int H, int ctx, int n_keys, int Tq,
-                  const DecState* ds, T* out, int S, float* xpart, unsigned* xcnt, hipStream_t st) {
-    hipLaunchKernelGGL((dec_attn_kernel<T, NQ, CAUSAL, AWV, SPLIT>), dim3(nseq * H, S), dim3(64 * AWV), 0, st, q,
-                       H * 64, kv, B_layout, H, ctx, n_keys, Tq, ds, out, xpart, xcnt);
-    SPT_LAUNCH_CHECK();
-}
-
-template <typename T>
-void dec_attn_launch(const T* q, const T* kv, int nseq, int B_layout, int H, int ctx, int n_keys, int causal, int Tq,
-                     const DecState* ds, T* out, const AttnSplit& sp, hipStream_t st) {
-    if (causal) {
-        if (Tq == 1) dec_attn_cfg<T, 1, true, 8, false>(q, kv, nseq, B_layout, H, ctx, n_keys, Tq, ds, out, 1, nullptr, nullptr, st);
-        else dec_attn_cfg<T, 4, true, 8, false>(q, kv, nseq, B_layout, H, ctx, n_keys, Tq, ds, out, 1, nullptr, nullptr, st);
-        return;
+// Cross-attention over the cached encoder K/V (all T_enc keys), one workgroup per (b, h).
+// kv: [2][B_layout][H][T_enc][64] at the group's first sequence.  (A fused LayerNorm + cross-Q
+// projection prologue and key-chunk splits were measured slower on MI355X: r1
+// exp_fused_xattn_pending_slabs.txt.)
+template <typename T, int NQ>
+__global__ __launch_bounds__(64 * AW) void cross_attn_kernel(const T* __restrict__ q, const T* __restrict__ kv,
+                                                             int B_layout, int H, int T_enc, int Tq,
+                                                             T* __restrict__ out) {
+    __shared__ float s_m[AW][NQ], s_l[AW][NQ];
+    __shared__ float s_o[AW][NQ][64];
+    const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane & 7;
+    const size_t kvo = ((size_t)b * H + h) * (size_t)T_enc * 64 + 8 * g;
+    AttnWave<T, NQ> aw;
+    aw.init(kv + kvo, kv + (size_t)B_layout * H * T_enc * 64 + kvo, T_enc, lane);
+    float qv[NQ][8];
+    int lim[NQ];
+#pragma unroll
+    for (int t = 0; t < NQ; ++t) {
+        const int tt = t < Tq ? t : Tq - 1;
+        const T* qr = q + (size_t)(b * Tq + tt) * (H * 64) + h * 64 + 8 * g;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qv[t][e] = to_f<T>(qr[e]) * kLog2Scale;
+        lim[t] = T_enc;
     }
-    const int S = (sp.xpart && sp.xcnt) ? std::max(1, std::min(sp.splits, kAttnMaxSplit)) : 1;
-    const int waves = sp.waves == 16 ? 16 : 8;
-#define SPT_XA(NQ_, AW_)                                                                                         \
-    if (S > 1) dec_attn_cfg<T, NQ_, false, AW_, true>(q, kv, nseq, B_layout, H, ctx, n_keys, Tq, ds, out, S,     \
-                                                      sp.xpart, sp.xcnt, st);                                   \
-    else dec_attn_cfg<T, NQ_, false, AW_, false>(q, kv, nseq, B_layout, H, ctx, n_keys, Tq, ds, out, 1, nullptr, \
-                                                 nullptr, st);
-    if (Tq == 1) {
-        if (waves == 16) { SPT_XA(1, 16) } else { SPT_XA(1, 8) }
-    } else {
-        SPT_XA(4, 8)
+    aw.run(wid, cdiv(T_enc, AttnWave<T, NQ>::KB), false, qv, lim, Tq);
+    aw.to_lds(s_m, s_l, s_o, wid, lane);
+    __syncthreads();
+    if (tid < 64 * Tq) {
+        const int t = tid >> 6, e = tid & 63;
+        float M, L, O;
+        attn_merge<NQ>(s_m, s_l, s_o, t, e, M, L, O);
+        out[(size_t)(b * Tq + t) * (H * 64) + h * 64 + e] = from_f<T>(O / L);
     }
-#undef SPT_XA
 }
 
 // ------------------------------------------------------------------ finalize
@@ -667,23 +711,34 @@ void gemv_prepare(int dtype) {
     else gemv_attr_modes<float>();
 }
 
-void gemv(int dtype, int mode, const GemvArgs& a_in, hipStream_t st) {
+void gemv(int dtype, int mode, int asrc, const GemvArgs& a_in, hipStream_t st) {
     if (a_in.R > 64 || a_in.R <= 0) throw std::runtime_error("gemv: rows must be in 1..64");
     const int ks = dtype == DT_BF16 ? 128 : 64;
     if (a_in.K % ks) throw std::runtime_error("gemv: K alignment");
     GemvArgs a = a_in;
-    a.ksplit = 1;
-#define SPT_GV(T, M) \
-    case M: gemv_launch<T, M>(a, st); return;
-    if (dtype == DT_BF16) {
-        switch (mode) { SPT_GV(bf16, GV_BIAS) SPT_GV(bf16, GV_BIAS_GELU) SPT_GV(bf16, GV_BIAS_RESID)
-                        SPT_GV(bf16, GV_QKV_CACHE) SPT_GV(bf16, GV_LOGITS) }
-    } else {
-        switch (mode) { SPT_GV(float, GV_BIAS) SPT_GV(float, GV_BIAS_GELU) SPT_GV(float, GV_BIAS_RESID)
-                        SPT_GV(float, GV_QKV_CACHE) SPT_GV(float, GV_LOGITS) }
+    a.ksplit = std::max(1, a.ksplit);
+    if (a.ksplit > 1 && mode != GV_PARTIAL) throw std::runtime_error("gemv: K split needs partial outputs");
+    if (a.ksplit > a.K / ks) throw std::runtime_error("gemv: K split exceeds the super-steps");
+    const int esz = dtype == DT_BF16 ? 2 : 4;
+    if (asrc != A_DIRECT && gv_img_bytes(a.R, a.K, esz) > GV_LDS_BYTES)
+        throw std::runtime_error("gemv: A image exceeds the LDS budget");
+    if (asrc == A_LN && (a.K > 1536 || !a.ln_w || !a.ln_b))
+        throw std::runtime_error("gemv: LayerNorm prologue needs K <= 1536 and LN parameters");
+    if (asrc == A_LN && a.n_pend != 0 && a.n_pend != 2 && a.n_pend != 4)
+        throw std::runtime_error("gemv: pending slab count must be 0, 2 or 4");
+    if (asrc == A_LN)
+        for (int p = 0; p < 4; ++p)
+            if (!a.pend[p]) throw std::runtime_error("gemv: LayerNorm prologue needs 4 pending slabs (zero slab if none)");
+    const int code = asrc == A_LN ? LN_SRC(a.n_pend) : asrc;
+#define SPT_GV(M, S)                                                      \
+    if (mode == M && code == S) {                                         \
+        if (dtype == DT_BF16) gemv_launch<bf16, M, S>(a, st);             \
+        else gemv_launch<float, M, S>(a, st);                             \
+        return;                                                           \
     }
+    SPT_GV_PAIRS(SPT_GV)
 #undef SPT_GV
-    throw std::runtime_error("gemv: bad mode");
+    throw std::runtime_error("gemv: unsupported mode / A source");
 }
 
 void dec_embed(int dtype, const int* tok, int R, int Tq, int d, const void* tok_emb, const float* pos_emb,
@@ -697,22 +752,31 @@ void dec_embed(int dtype, const int* tok, int R, int Tq, int d, const void* tok_
 void dec_self_attn(int dtype, const void* q, const void* cache, int B, int H, int ctx, int Tq, const DecState* ds,
                    void* out, hipStream_t st) {
     if (Tq < 1 || Tq > 4) throw std::runtime_error("dec_self_attn: 1..4 queries per sequence");
-    if (dtype == DT_BF16)
-        dec_attn_launch<bf16>((const bf16*)q, (const bf16*)cache, B, B, H, ctx, 0, 1, Tq, ds, (bf16*)out, AttnSplit{}, st);
-    else
-        dec_attn_launch<float>((const float*)q, (const float*)cache, B, B, H, ctx, 0, 1, Tq, ds, (float*)out, AttnSplit{},
-                               st);
+    const dim3 grid(B * H), blk(64 * AW);
+#define SPT_SA(T, NQ) \
+    hipLaunchKernelGGL((self_attn_kernel<T, NQ>), grid, blk, 0, st, (const T*)q, H * 64, (const T*)cache, B, H, ctx, Tq, ds, (T*)out)
+    if (dtype == DT_BF16) {
+        if (Tq == 1) SPT_SA(bf16, 1); else SPT_SA(bf16, 4);
+    } else {
+        if (Tq == 1) SPT_SA(float, 1); else SPT_SA(float, 4);
+    }
+#undef SPT_SA
+    SPT_LAUNCH_CHECK();
 }
 
 void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int B_layout, int H, int T_enc, int Tq, void* out,
-                    const AttnSplit& sp, hipStream_t st) {
+                    hipStream_t st) {
     if (Tq < 1 || Tq > 4) throw std::runtime_error("dec_cross_attn: 1..4 queries per sequence");
-    if (dtype == DT_BF16)
-        dec_attn_launch<bf16>((const bf16*)q, (const bf16*)kv, B, B_layout, H, T_enc, T_enc, 0, Tq, nullptr, (bf16*)out,
-                              sp, st);
-    else
-        dec_attn_launch<float>((const float*)q, (const float*)kv, B, B_layout, H, T_enc, T_enc, 0, Tq, nullptr,
-                               (float*)out, sp, st);
+    const dim3 grid(B * H), blk(64 * AW);
+#define SPT_XA(T, NQ) \
+    hipLaunchKernelGGL((cross_attn_kernel<T, NQ>), grid, blk, 0, st, (const T*)q, (const T*)kv, B_layout, H, T_enc, Tq, (T*)out)
+    if (dtype == DT_BF16) {
+        if (Tq == 1) SPT_XA(bf16, 1); else SPT_XA(bf16, 4);
+    } else {
+        if (Tq == 1) SPT_XA(float, 1); else SPT_XA(float, 4);
+    }
+#undef SPT_XA
+    SPT_LAUNCH_CHECK();
 }
 
 void dec_finalize(int dtype, const FinalizeArgs& a, int B, hipStream_t st) {

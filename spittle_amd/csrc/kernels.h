@@ -66,24 +66,28 @@ struct DecState {        // device-resident step state
     int step;            // index of the token being produced
 };
 
-enum { GV_BIAS = 0, GV_BIAS_GELU = 1, GV_BIAS_RESID = 2, GV_QKV_CACHE = 3, GV_LOGITS = 4 };
+enum { GV_BIAS = 0, GV_BIAS_GELU = 1, GV_PARTIAL = 2, GV_QKV_CACHE = 3, GV_LOGITS = 4, GV_BIAS_RESID = 5 };
+enum { A_DIRECT = 0, A_LN = 1 };
 struct GemvArgs {
-    // A: either LN(x) of f32 rows (ln_w != nullptr) or a dtype activation
-    const void* A; int lda; int a_row0;   // row i of A at A + (i * lda + a_row0)
-    const float* ln_w; const float* ln_b; // fused pre-LayerNorm when non-null (A is f32 then)
+    // A rows: row i at A + (i * lda + a_row0); A_DIRECT: dtype activations; A_LN: f32 residual rows
+    const void* A; int lda; int a_row0;
+    const float* ln_w; const float* ln_b; // A_LN: LayerNorm of x + pend[0] + .. + pend[3]
+    const float* pend[4]; int n_pend;     // A_LN: pending partial slabs (same layout as A): n_pend = 0, 2 or 4
+    float* x_out;                         // A_LN: combined rows written here by workgroup (0, 0) (or nullptr)
     int R;                                // rows (<= 64)
     const void* W; int N, K;              // W [N][K]
     const float* bias;
-    void* C; int ldc;                     // output rows (GV_BIAS*, GV_LOGITS)
+    void* C; int ldc;                     // output rows (GV_BIAS*, GV_LOGITS, GV_PARTIAL; GV_BIAS_RESID: f32 C += ...)
+    int ksplit; int64_t c_split;          // GV_PARTIAL: K split over workgroups, slab s at C + s * c_split (f32)
     // GV_QKV_CACHE: q -> C, k/v -> cache [2][B][H][ctx][64] at position pos0 + t (row = b*Tq + t)
     void* cache; int cache_B, cache_H, cache_ctx, Tq;
     const DecState* st;
     // GV_LOGITS: suppression + per-16-column-tile top-2 partials [R][n_tiles] (16 B each)
     const uint32_t* suppress; int blank0, blank1;
     void* part; int n_tiles;
-    int ksplit;                           // set by gemv()
 };
-void gemv(int dtype, int mode, const GemvArgs& a, hipStream_t st);
+constexpr int kMaxPend = 4;
+void gemv(int dtype, int mode, int asrc, const GemvArgs& a, hipStream_t st);
 // one-time per-process kernel attributes (call before any stream capture)
 void gemv_prepare(int dtype);
 
@@ -93,14 +97,10 @@ void dec_embed(int dtype, const int* tok, int R, int Tq, int d, const void* tok_
 // self attention over the cache: q [R][d] (row b*Tq + t at position pos0 + t), keys 0..pos0+t
 void dec_self_attn(int dtype, const void* q, const void* cache, int B, int H, int ctx, int Tq,
                    const DecState* ds, void* out, hipStream_t st);
-// cross attention over T_enc keys, split over key chunks; partials then combine
+// cross attention over all T_enc cached encoder keys: q [R][d] -> out [R][d]
 // kv: [2][B_layout][H][T_enc][64] (already offset to the first of the B sequences)
-// split: keys of each (b, h) over `splits` workgroups (partials [B*H][splits][Tq][66] f32 in
-// xpart, arrival tickets [B*H] in xcnt, zero before the first launch); waves per workgroup 8 or 16
-struct AttnSplit { int splits = 1; int waves = 8; float* xpart = nullptr; unsigned* xcnt = nullptr; };
-constexpr int kAttnMaxSplit = 8;
 void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int B_layout, int H, int T_enc, int Tq,
-                    void* out, const AttnSplit& split, hipStream_t st);
+                    void* out, hipStream_t st);
 
 struct FinalizeArgs {
     const void* part; int n_tiles;        // logits top-2 partials [B][n_tiles]

@@ -1,9 +1,10 @@
 // ubench.cpp -- kernel microbenchmarks (developer tool, not part of the C ABI).
 // Times the library's launchers with HIP events, back-to-back launches on one stream.
-//   ubench gemv  N K R mode ln dtype     mode: 0 bias 1 gelu 2 resid 3 qkv 4 logits
-//   ubench attn  B H ctx nkeys causal Tq dtype [splits waves]
+//   ubench gemv  N K R mode ln dtype [ksplit npend]  mode: 0 bias 1 gelu 2 partial 3 qkv 4 logits 5 resid
+//   ubench attn  B H ctx nkeys Tq dtype   self-attention
+//   ubench xattn B T Tq dtype            cross-attention
 //   ubench gemm  M N K epi dtype
-//   ubench layer B dtype [xsplits xwaves] one large-v3 decoder layer (8 launches)
+//   ubench layer B dtype                 one large-v3 decoder layer (8 launches)
 //   ubench layer2 B dtype [...]          two such chains on two streams
 //   ubench null
 #include <hip/hip_runtime.h>
@@ -72,7 +73,8 @@ int main(int argc, char** argv) {
         return 0;
     }
     if (what == "gemv") {
-        const int N = ai(2, 1280), K = ai(3, 1280), R = ai(4, 8), mode = ai(5, 2), ln = ai(6, 0), dt = ai(7, DT_BF16);
+        const int N = ai(2, 1280), K = ai(3, 1280), R = ai(4, 8), mode = ai(5, 2), ln = ai(6, 0), dt = ai(7, DT_BF16),
+                  ksplit = ai(8, 1), npend = ai(9, 0);
         gemv_prepare(dt);
         const int esz = dt == DT_BF16 ? 2 : 4;
         void* W = drand((size_t)N * K, dt, 1, -5);
@@ -80,65 +82,54 @@ int main(int argc, char** argv) {
         float* lnw = frand(K, 3, -3);
         float* lnb = frand(K, 4, -4);
         void* A = ln ? (void*)frand((size_t)R * K, 5, 0) : drand((size_t)R * K, dt, 5, 0);
-        void* C = dalloc((size_t)R * N * 4 + 64);
+        float* zero = (float*)dalloc((size_t)4 * R * K * 4);
+        void* C = dalloc((size_t)4 * R * N * 4 + 64);
         void* cache = dalloc((size_t)2 * R * 20 * 448 * 64 * esz);
         uint32_t* sup = (uint32_t*)dalloc(N / 8 + 64);
         void* part = dalloc((size_t)R * ((N + 15) / 16) * 16 + 64);
         GemvArgs a{};
         a.A = A; a.lda = K; a.R = R; a.W = W; a.N = N; a.K = K; a.bias = bias; a.C = C; a.ldc = N;
         if (ln) { a.ln_w = lnw; a.ln_b = lnb; }
+        for (int p = 0; p < kMaxPend; ++p) a.pend[p] = zero + (size_t)p * R * K;
+        a.n_pend = npend;
         a.cache = cache; a.cache_B = R; a.cache_H = N / 3 / 64; a.cache_ctx = 448; a.Tq = 1; a.st = ds;
         a.suppress = sup; a.blank0 = a.blank1 = -1; a.part = part; a.n_tiles = (N + 15) / 16;
+        a.ksplit = ksplit; a.c_split = (int64_t)R * N;
         if (mode == GV_QKV_CACHE) a.ldc = N / 3;
-        const double us = time_us(st, iters, [&] { gemv(dt, mode, a, st); });
+        const double us = time_us(st, iters, [&] { gemv(dt, mode, ln ? A_LN : A_DIRECT, a, st); });
         const double bytes = (double)N * K * esz;
-        printf("gemv N=%d K=%d R=%d mode=%d ln=%d dt=%d : %.2f us  %.0f GB/s\n", N, K, R, mode, ln, dt, us,
-               bytes / us / 1e3);
+        printf("gemv N=%d K=%d R=%d mode=%d ln=%d dt=%d ksplit=%d npend=%d : %.2f us  %.0f GB/s\n", N, K, R, mode, ln, dt,
+               ksplit, npend, us, bytes / us / 1e3);
         return 0;
     }
-    if (what == "attn") {
-        const int B = ai(2, 8), H = ai(3, 20), ctx = ai(4, 1500), nk = ai(5, 1500), causal = ai(6, 0),
-                  Tq = ai(7, 1), dt = ai(8, DT_BF16);
+    if (what == "attn") {  // self-attention (causal) over nkeys cached keys
+        const int B = ai(2, 8), H = ai(3, 20), ctx = ai(4, 448), nk = ai(5, 132), Tq = ai(6, 1), dt = ai(7, DT_BF16);
         const int esz = dt == DT_BF16 ? 2 : 4;
         void* q = drand((size_t)B * Tq * H * 64, dt, 1, 0);
         void* kv = drand((size_t)2 * B * H * ctx * 64, dt, 2, 0);
         void* out = dalloc((size_t)B * Tq * H * 64 * esz);
         DecState h{nk - Tq, 0};
         HIP_CHECK(hipMemcpy(ds, &h, sizeof(h), hipMemcpyHostToDevice));
-        double us;
-        if (causal) us = time_us(st, iters, [&] { dec_self_attn(dt, q, kv, B, H, ctx, Tq, ds, out, st); });
-        else {
-            AttnSplit xs;
-            xs.splits = ai(9, 1); xs.waves = ai(10, 8);
-            xs.xpart = (float*)dalloc((size_t)B * H * kAttnMaxSplit * 4 * 66 * 4);
-            xs.xcnt = (unsigned*)dalloc((size_t)B * H * 4);
-            us = time_us(st, iters, [&] { dec_cross_attn(dt, q, kv, B, B, H, ctx, Tq, out, xs, st); });
-            printf("  (splits=%d waves=%d) ", xs.splits, xs.waves);
-        }
-        const double bytes = 2.0 * B * H * nk * 64 * esz;
-        printf("attn B=%d H=%d nk=%d causal=%d Tq=%d dt=%d : %.2f us  %.0f GB/s\n", B, H, nk, causal, Tq, dt, us,
-               bytes / us / 1e3);
+        const double us = time_us(st, iters, [&] { dec_self_attn(dt, q, kv, B, H, ctx, Tq, ds, out, st); });
+        printf("self-attn B=%d H=%d nk=%d Tq=%d dt=%d : %.2f us  %.0f GB/s\n", B, H, nk, Tq, dt, us,
+               2.0 * B * H * nk * 64 * esz / us / 1e3);
         return 0;
     }
-    if (what == "gemm") {
-        const int M = ai(2, 12000), N = ai(3, 5120), K = ai(4, 1280), epi = ai(5, 0), dt = ai(6, DT_BF16);
-        void* A = drand((size_t)M * K, dt, 1, -2);
-        void* W = drand((size_t)N * K, dt, 2, -5);
-        float* bias = frand(N, 3, -5);
-        void* C = dalloc((size_t)M * N * 4);
-        GemmArgs g{};
-        g.A = A; g.lda = K; g.W = W; g.ldw = K; g.M = M; g.N = N; g.K = K; g.bias = bias; g.C = C; g.ldc = N;
-        g.kv_B = M / 1500; g.kv_T = 1500; g.kv_H = 20;
-        const double us = time_us(st, 20, [&] { gemm_nt(dt, epi, g, 1, st); });
-        printf("gemm M=%d N=%d K=%d epi=%d dt=%d : %.2f us  %.1f TFLOP/s\n", M, N, K, epi, dt, us,
-               2.0 * M * N * K / us / 1e6);
+    if (what == "xattn") {  // cross-attention over T encoder keys
+        const int B = ai(2, 8), T = ai(3, 1500), Tq = ai(4, 1), dt = ai(5, DT_BF16), d = 1280, H = 20;
+        const int esz = dt == DT_BF16 ? 2 : 4;
+        void* q = drand((size_t)B * Tq * d, dt, 1, 0);
+        void* kv = drand((size_t)2 * B * H * T * 64, dt, 2, 0);
+        void* out = dalloc((size_t)B * Tq * d * esz);
+        const double us = time_us(st, iters, [&] { dec_cross_attn(dt, q, kv, B, B, H, T, Tq, out, st); });
+        printf("cross-attn B=%d T=%d Tq=%d dt=%d : %.2f us  %.0f GB/s\n", B, T, Tq, dt, us,
+               2.0 * B * H * T * 64 * esz / us / 1e3);
         return 0;
     }
     if (what == "layer" || what == "layer2") {
         // layer: one large-v3 decoder layer chain at batch B
         // layer2: two independent chains of batch B on two streams (can they overlap?)
         const int B = ai(2, 8), dt = ai(3, DT_BF16), d = 1280, H = 20, ctx = 448, T = 1500;
-        const int xsplits = ai(4, 1), xwaves = ai(5, 8);
         gemv_prepare(dt);
         const int esz = dt == DT_BF16 ? 2 : 4;
         void* wqkv = drand((size_t)3 * d * d, dt, 1, -4);
@@ -150,47 +141,64 @@ int main(int argc, char** argv) {
         float* b4 = frand(4 * d, 7, -5);
         float* lnw = frand(d, 8, -3);
         float* lnb = frand(d, 9, -4);
-        struct Chain { float* x; void *q, *ao, *ff, *skv, *ckv; DecState* ds; AttnSplit xs; };
+        float* zero = (float*)dalloc((size_t)B * d * 4);
+        struct Chain { float *x, *x2, *pend; void *q, *ao, *ff, *skv, *ckv; DecState* ds; };
         auto mk = [&](uint32_t s) {
             Chain c;
             c.x = frand((size_t)B * d, 10 + s, 0);
+            c.x2 = (float*)dalloc((size_t)B * d * 4);
+            c.pend = (float*)dalloc((size_t)kMaxPend * B * d * 4);
             c.q = dalloc((size_t)B * d * esz);
             c.ao = dalloc((size_t)B * d * esz);
             c.ff = dalloc((size_t)B * 4 * d * esz);
             c.skv = drand((size_t)2 * B * H * ctx * 64, dt, 11 + s, 0);
             c.ckv = drand((size_t)2 * B * H * T * 64, dt, 12 + s, 0);
             c.ds = (DecState*)dalloc(64);
-            c.xs.splits = xsplits; c.xs.waves = xwaves;
-            c.xs.xpart = (float*)dalloc((size_t)B * H * kAttnMaxSplit * 4 * 66 * 4);
-            c.xs.xcnt = (unsigned*)dalloc((size_t)B * H * 4);
             DecState h{128, 0};
             HIP_CHECK(hipMemcpy(c.ds, &h, sizeof(h), hipMemcpyHostToDevice));
             return c;
         };
+        // the engine's layer (Engine::enqueue_decoder_pass): 8 launches, pending slabs after the
+        // self-out (2) and fc2 (4) projections; the chain starts with fc2's 4 slabs pending
         auto layer = [&](const Chain& c, hipStream_t s) {
+            float *xc = c.x, *xo = c.x2;
+            int np = 4;
+            auto ln_input = [&](GemvArgs& a) {
+                a.A = xc;
+                for (int p = 0; p < kMaxPend; ++p) a.pend[p] = p < np ? c.pend + (size_t)p * B * d : zero;
+                a.n_pend = np;
+                a.x_out = np ? xo : nullptr;
+            };
+            auto consumed = [&] { if (np > 0) std::swap(xc, xo); np = 0; };
             GemvArgs a{};
-            a.A = c.x; a.lda = d; a.ln_w = lnw; a.ln_b = lnb; a.R = B; a.W = wqkv; a.N = 3 * d; a.K = d; a.bias = b4;
+            ln_input(a); a.lda = d; a.ln_w = lnw; a.ln_b = lnb; a.R = B;
+            a.W = wqkv; a.N = 3 * d; a.K = d; a.bias = b4;
             a.C = c.q; a.ldc = d; a.cache = c.skv; a.cache_B = B; a.cache_H = H; a.cache_ctx = ctx; a.Tq = 1; a.st = c.ds;
-            gemv(dt, GV_QKV_CACHE, a, s);
+            gemv(dt, GV_QKV_CACHE, A_LN, a, s);
+            consumed();
             dec_self_attn(dt, c.q, c.skv, B, H, ctx, 1, c.ds, c.ao, s);
             a = GemvArgs{};
-            a.A = c.ao; a.lda = d; a.R = B; a.W = wo; a.N = d; a.K = d; a.bias = b4; a.C = c.x; a.ldc = d;
-            gemv(dt, GV_BIAS_RESID, a, s);
+            a.A = c.ao; a.lda = d; a.R = B; a.W = wo; a.N = d; a.K = d; a.bias = b4;
+            a.C = c.pend; a.ldc = d; a.c_split = (int64_t)B * d; a.ksplit = 2; np = 2;
+            gemv(dt, GV_PARTIAL, A_DIRECT, a, s);
             a = GemvArgs{};
-            a.A = c.x; a.lda = d; a.ln_w = lnw; a.ln_b = lnb; a.R = B; a.W = wq; a.N = d; a.K = d; a.bias = b4;
-            a.C = c.q; a.ldc = d;
-            gemv(dt, GV_BIAS, a, s);
-            dec_cross_attn(dt, c.q, c.ckv, B, B, H, T, 1, c.ao, c.xs, s);
+            ln_input(a); a.lda = d; a.ln_w = lnw; a.ln_b = lnb; a.R = B;
+            a.W = wq; a.N = d; a.K = d; a.bias = b4; a.C = c.q; a.ldc = d;
+            gemv(dt, GV_BIAS, A_LN, a, s);
+            consumed();
+            dec_cross_attn(dt, c.q, c.ckv, B, B, H, T, 1, c.ao, s);
             a = GemvArgs{};
-            a.A = c.ao; a.lda = d; a.R = B; a.W = wco; a.N = d; a.K = d; a.bias = b4; a.C = c.x; a.ldc = d;
-            gemv(dt, GV_BIAS_RESID, a, s);
+            a.A = c.ao; a.lda = d; a.R = B; a.W = wco; a.N = d; a.K = d; a.bias = b4; a.C = xc; a.ldc = d;
+            gemv(dt, GV_BIAS_RESID, A_DIRECT, a, s);
             a = GemvArgs{};
-            a.A = c.x; a.lda = d; a.ln_w = lnw; a.ln_b = lnb; a.R = B; a.W = w1; a.N = 4 * d; a.K = d; a.bias = b4;
-            a.C = c.ff; a.ldc = 4 * d;
-            gemv(dt, GV_BIAS_GELU, a, s);
+            ln_input(a); a.lda = d; a.ln_w = lnw; a.ln_b = lnb; a.R = B;
+            a.W = w1; a.N = 4 * d; a.K = d; a.bias = b4; a.C = c.ff; a.ldc = 4 * d;
+            gemv(dt, GV_BIAS_GELU, A_LN, a, s);
+            consumed();
             a = GemvArgs{};
-            a.A = c.ff; a.lda = 4 * d; a.R = B; a.W = w2; a.N = d; a.K = 4 * d; a.bias = b4; a.C = c.x; a.ldc = d;
-            gemv(dt, GV_BIAS_RESID, a, s);
+            a.A = c.ff; a.lda = 4 * d; a.R = B; a.W = w2; a.N = d; a.K = 4 * d; a.bias = b4;
+            a.C = c.pend; a.ldc = d; a.c_split = (int64_t)B * d; a.ksplit = 4; np = 4;
+            gemv(dt, GV_PARTIAL, A_DIRECT, a, s);
         };
         const double bytes = (14.0 * d * d) * esz + 2.0 * B * H * (T + 129) * 64 * esz;
         Chain c0 = mk(0);
