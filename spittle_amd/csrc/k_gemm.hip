@@ -7,7 +7,7 @@
 // Tile: 128 x 128 per 256-thread workgroup (4 waves in 2 x 2, 64 x 64 each),
 // one 128-byte K slab per stage (64 bf16 or 32 f32), operands staged
 // global -> LDS by global_load_lds_dwordx4 (one wave-instruction = 8 rows x 128 B),
-// XOR-swizzled on the source address (chunk ^ (row & 7)) so the ds_read_b128
+// XOR-swizzled on the source address (chunk ^ swz(row)) so the ds_read_b128
 // fragment reads are spread over the bank row, double-buffered so the next
 // slab's DMA overlaps the current slab's MFMAs.
 //   bf16: v_mfma_f32_16x16x32_bf16, 2 k-steps per slab.
@@ -24,14 +24,53 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace spt {
 
 namespace {
 
 constexpr int BM = 128, BN = 128, SLAB = 128;  // SLAB = bytes of K per row per stage
 
+// LDS swizzle of 128-byte rows: a 256-byte bank row holds rows 2q and 2q+1, so 16 consecutive
+// rows (one ds_read_b128 lane group) hit 16 distinct 16-byte slots with chunk' = chunk ^ ((row >> 1) & 7)
+// (chunk ^ (row & 7) leaves rows r and r+8 on the same slot: 2-way conflicts)
+__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
+
 __device__ __forceinline__ void glds16(const void* g, SPT_LDS void* l) {
     __builtin_amdgcn_global_load_lds((const void*)g, l, 16, 0, 0);
+}
+
+// fused epilogue of one output element (row, column): bias, GELU, positional add, residual
+// add or the head-split store of the cross-attention K/V cache
+struct EpiCol { int col; float bv; int64_t kv_off; };
+template <int EPI>
+__device__ __forceinline__ EpiCol epi_col(const GemmArgs& g, int col) {
+    EpiCol e{col, g.bias ? g.bias[col] : 0.0f, 0};
+    if constexpr (EPI == EPI_KVSPLIT) {
+        const int d = g.kv_H * 64;
+        const int l = col / (2 * d), rem = col - l * 2 * d;
+        const int kvi = rem / d, h = (rem - kvi * d) >> 6, el = rem & 63;
+        e.kv_off = ((((int64_t)(l * 2 + kvi) * g.kv_B) * g.kv_H + h) * g.kv_T) * 64 + el;  // + (bb*H*T + t)*64
+    }
+    return e;
+}
+template <typename T, int EPI>
+__device__ __forceinline__ void epi_store(const GemmArgs& g, int bz, int row, const EpiCol& e, float acc) {
+    const float v = acc + e.bv;
+    if constexpr (EPI == EPI_BIAS) {
+        ((T*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col] = from_f<T>(v);
+    } else if constexpr (EPI == EPI_BIAS_GELU) {
+        ((T*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col] = from_f<T>(gelu_tanh(v));
+    } else if constexpr (EPI == EPI_BIAS_GELU_POS) {
+        ((float*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col] = gelu_tanh(v) + g.pos[(size_t)row * g.N + e.col];
+    } else if constexpr (EPI == EPI_BIAS_RESID) {
+        ((float*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col] += v;
+    } else if constexpr (EPI == EPI_KVSPLIT) {
+        const int bb = row / g.kv_T, t = row - bb * g.kv_T;
+        ((T*)g.C)[e.kv_off + ((int64_t)bb * g.kv_H * g.kv_T + t) * 64] = from_f<T>(v);
+    }
 }
 
 template <typename T, int EPI>
@@ -57,7 +96,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int rt = (wid * 4 + i) * 8 + prow;
-        const int c = pch ^ (rt & 7);
+        const int c = pch ^ swz(rt);
         const int ra = min(m0 + rt, g.M - 1);
         srcA[i] = (const char*)(A + (size_t)ra * g.lda) + c * 16;
         srcW[i] = (const char*)(W + (size_t)(n0 + rt) * g.ldw) + c * 16;
@@ -98,9 +137,9 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int ra = wm * 64 + 16 * i + fr;
-                    af[i] = *(const SPT_LDS bf16x8*)(la + ra * SLAB + ((c ^ (ra & 7)) << 4));
+                    af[i] = *(const SPT_LDS bf16x8*)(la + ra * SLAB + ((c ^ swz(ra)) << 4));
                     const int rw = wn * 64 + 16 * i + fr;
-                    wf[i] = *(const SPT_LDS bf16x8*)(lw + rw * SLAB + ((c ^ (rw & 7)) << 4));
+                    wf[i] = *(const SPT_LDS bf16x8*)(lw + rw * SLAB + ((c ^ swz(rw)) << 4));
                 }
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
@@ -117,8 +156,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const int c = 2 * fq + h;
-                    af[i][h] = *(const SPT_LDS f32x4*)(la + ra * SLAB + ((c ^ (ra & 7)) << 4));
-                    wf[i][h] = *(const SPT_LDS f32x4*)(lw + rw * SLAB + ((c ^ (rw & 7)) << 4));
+                    af[i][h] = *(const SPT_LDS f32x4*)(la + ra * SLAB + ((c ^ swz(ra)) << 4));
+                    wf[i][h] = *(const SPT_LDS f32x4*)(lw + rw * SLAB + ((c ^ swz(rw)) << 4));
                 }
             }
 #pragma unroll
@@ -137,45 +176,250 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
     // ---------------------------------------------------------------- epilogue
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int col = n0 + wn * 64 + 16 * j + fr;
-        const float bv = g.bias ? g.bias[col] : 0.0f;
-        int kv_l = 0, kv_kv = 0, kv_h = 0, kv_e = 0;
-        if constexpr (EPI == EPI_KVSPLIT) {
-            const int d = g.kv_H * 64;
-            kv_l = col / (2 * d);
-            const int rem = col - kv_l * 2 * d;
-            kv_kv = rem / d;
-            kv_h = (rem - kv_kv * d) >> 6;
-            kv_e = rem & 63;
-        }
+        const EpiCol ec = epi_col<EPI>(g, n0 + wn * 64 + 16 * j + fr);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = m0 + wm * 64 + 16 * i + 4 * fq + r;
-                if (row >= g.M) continue;
-                float v = acc[i][j][r] + bv;
-                if constexpr (EPI == EPI_BIAS) {
-                    T* C = (T*)g.C + (size_t)bz * g.sC;
-                    C[(size_t)row * g.ldc + col] = from_f<T>(v);
-                } else if constexpr (EPI == EPI_BIAS_GELU) {
-                    T* C = (T*)g.C + (size_t)bz * g.sC;
-                    C[(size_t)row * g.ldc + col] = from_f<T>(gelu_tanh(v));
-                } else if constexpr (EPI == EPI_BIAS_GELU_POS) {
-                    float* C = (float*)g.C + (size_t)bz * g.sC;
-                    C[(size_t)row * g.ldc + col] = gelu_tanh(v) + g.pos[(size_t)row * g.N + col];
-                } else if constexpr (EPI == EPI_BIAS_RESID) {
-                    float* C = (float*)g.C + (size_t)bz * g.sC;
-                    C[(size_t)row * g.ldc + col] += v;
-                } else if constexpr (EPI == EPI_KVSPLIT) {
-                    T* C = (T*)g.C;
-                    const int bb = row / g.kv_T, t = row - bb * g.kv_T;
-                    const size_t off =
-                        ((((size_t)(kv_l * 2 + kv_kv) * g.kv_B + bb) * g.kv_H + kv_h) * g.kv_T + t) * 64 + kv_e;
-                    C[off] = from_f<T>(v);
-                }
+                if (row < g.M) epi_store<T, EPI>(g, bz, row, ec, acc[i][j][r]);
             }
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// 256 x 256 tile, 512 threads = 8 waves as 2 (M) x 4 (N), each wave a 128 x 64 C tile (8 x 4
+// fragments of v_mfma_f32_16x16x32_bf16), BK = 64 (128 B per row), 2 LDS buffers of 64 KiB
+// (A 256 rows + W 256 rows, 128 B each, 16-byte chunk c of row r stored at slot c ^ swz(r)).
+// Each buffer is staged as four half-tiles by global_load_lds_dwordx4 (2 instructions per wave
+// per half-tile):
+//   A0 = C rows {0..63, 128..191}   A1 = {64..127, 192..255}   (the two 64-row halves of
+//   W0 = C cols {0..31, 64..95, ..} W1 = {32..63, 96..127, ..}  every wave's 128 x 64 tile)
+// A K-tile is computed in four phases, one C quadrant (4 x 2 fragments x K 64 = 16 MFMAs) each:
+//   P1 reads A0 + W0 -> quadrant (0,0), stages A1 of K-tile kt+1 (other buffer)
+//   P2 reads W1      -> quadrant (0,1), stages A0 of kt+2 (this buffer: A0 was read in P1)
+//   P3 reads A1      -> quadrant (1,1), stages W0 of kt+2
+//   P4 (registers)   -> quadrant (1,0), stages W1 of kt+2
+// so every half-tile is restaged one phase after its last read (behind that phase's barrier)
+// and read at least four phases after it was issued.  With 2 instructions per half-tile, the
+// half-tile a phase reads next always has exactly 5 half-tiles issued after it: each waiting
+// phase ends with a counted s_waitcnt vmcnt(10) (never 0 in the loop) before its barrier.
+// Past the last K-tile the staging repeats the last K-tile into free halves (keeps the counts
+// uniform); the loop drains vmcnt(0) before the epilogue.  (A persistent variant whose staging
+// runs into the next tile measured no faster: the epilogue's stores, not the prologue, were the
+// per-tile cost, so the epilogue is staged through LDS into 16-byte row stores instead.)
+constexpr int G2_BM = 256, G2_BN = 256, G2_ROW = 128;  // G2_ROW: bytes of K per row per K-tile
+constexpr int G2_BUF = 2 * 256 * G2_ROW;               // one buffer: A + W
+constexpr int G2_LDS = 2 * G2_BUF;                     // 128 KiB
+constexpr int G2_LDS_ALL = 8 * 128 * (128 + 16) > G2_LDS ? 8 * 128 * (128 + 16) : G2_LDS;  // + epilogue staging
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wr = wid >> 2, wc = wid & 3;
+    const int fr = lane & 15, fq = lane >> 4;
+    const int nnt = g.N / G2_BN;
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const int tm = wg / nnt, tn = wg - tm * nnt;
+    const int m0 = tm * G2_BM, n0 = tn * G2_BN;
+    const int bz = blockIdx.z;
+    const bf16* A = (const bf16*)g.A + (size_t)bz * g.sA;
+    const bf16* W = (const bf16*)g.W;
+    const int nkt = g.K / 64;
+
+    // staging sources: half-tile h of A (or W), instruction i (0, 1) of this wave -> 8 rows
+    const int prow = lane >> 3, pch = lane & 7;
+    const char* srcA[2][2];
+    const char* srcW[2][2];
+    int dstA[2][2], dstW[2][2];  // LDS byte offsets (wave-uniform row base) inside a buffer
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int gi = wid * 2 + i;                                   // row group 0..15 of the half
+            const int ra = (gi >> 3) * 128 + h * 64 + (gi & 7) * 8;       // A: 2 blocks of 64 rows
+            const int rw = (gi >> 2) * 64 + h * 32 + (gi & 3) * 8;        // W: 4 blocks of 32 rows
+            const int rA = ra + prow, rW = rw + prow;
+            srcA[h][i] = (const char*)(A + (size_t)min(m0 + rA, g.M - 1) * g.lda) + ((pch ^ swz(rA)) << 4);
+            srcW[h][i] = (const char*)(W + (size_t)(n0 + rW) * g.ldw) + ((pch ^ swz(rW)) << 4);
+            dstA[h][i] = ra * G2_ROW;
+            dstW[h][i] = 256 * G2_ROW + rw * G2_ROW;
+        }
+    auto stageA = [&](int buf, int kt, int h) {
+        const size_t ko = (size_t)min(kt, nkt - 1) * G2_ROW;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(srcA[h][i] + ko),
+                                             (SPT_LDS void*)(smem + buf * G2_BUF + dstA[h][i]), 16, 0, 0);
+    };
+    auto stageW = [&](int buf, int kt, int h) {
+        const size_t ko = (size_t)min(kt, nkt - 1) * G2_ROW;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(srcW[h][i] + ko),
+                                             (SPT_LDS void*)(smem + buf * G2_BUF + dstW[h][i]), 16, 0, 0);
+    };
+    // fragment reads: A rows of quadrant half rh, W rows (C columns) of half ch, k-steps 0/1
+    bf16x8 af[4][2], bw[2][2][2];
+    auto readA = [&](int buf, int rh) {
+        const SPT_LDS char* la = (const SPT_LDS char*)smem + buf * G2_BUF;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = wr * 128 + rh * 64 + 16 * i + fr;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int c = 4 * s + fq;
+                af[i][s] = *(const SPT_LDS bf16x8*)(la + r * G2_ROW + ((c ^ swz(r)) << 4));
+            }
+        }
+    };
+    auto readW = [&](int buf, int ch) {
+        const SPT_LDS char* lw = (const SPT_LDS char*)smem + buf * G2_BUF + 256 * G2_ROW;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int r = wc * 64 + ch * 32 + 16 * j + fr;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int c = 4 * s + fq;
+                bw[ch][j][s] = *(const SPT_LDS bf16x8*)(lw + r * G2_ROW + ((c ^ swz(r)) << 4));
+            }
+        }
+    };
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto quad = [&](int rh, int ch) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[rh * 4 + i][ch * 2 + j] =
+                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bw[ch][j][s], acc[rh * 4 + i][ch * 2 + j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+    };
+#define G2_BARRIER() asm volatile("s_barrier" ::: "memory")
+#define G2_VMWAIT() asm volatile("s_waitcnt vmcnt(10)" ::: "memory")
+
+    // prologue: K-tile 0 whole, K-tile 1 but its A1 (issued by K-tile 0's P1)
+    stageA(0, 0, 0); stageW(0, 0, 0); stageW(0, 0, 1); stageA(0, 0, 1);
+    stageA(1, 1, 0); stageW(1, 1, 0); stageW(1, 1, 1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    G2_BARRIER();
+    for (int kt = 0; kt < nkt; ++kt) {
+        const int c = kt & 1;
+        // P1
+        readA(c, 0);
+        readW(c, 0);
+        stageA(c ^ 1, kt + 1, 1);
+        quad(0, 0);
+        G2_VMWAIT();
+        G2_BARRIER();
+        // P2
+        readW(c, 1);
+        stageA(c, kt + 2, 0);
+        quad(0, 1);
+        G2_VMWAIT();
+        G2_BARRIER();
+        // P3
+        readA(c, 1);
+        stageW(c, kt + 2, 0);
+        quad(1, 1);
+        G2_BARRIER();
+        // P4
+        stageW(c, kt + 2, 1);
+        quad(1, 0);
+        G2_VMWAIT();
+        G2_BARRIER();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    G2_BARRIER();  // every wave's last fragment reads are done: the LDS is free for the epilogue
+#undef G2_BARRIER
+#undef G2_VMWAIT
+
+    // ---------------------------------------------------------------- epilogue
+    // Per wave: the 128 x 64 C tile (after bias / GELU) goes to a private LDS region in MFMA
+    // layout (a lane holds 4 rows of one column), then is read back as 16-byte row chunks
+    // and written with one 16-byte global store per lane per row group (a lane's own values
+    // would be 2- or 4-byte stores at a row stride).  bf16 outputs: one pass of 128 rows,
+    // row stride 144 B; f32 outputs: two passes of 64 rows, row stride 272 B (the 16-byte pad
+    // spreads the four row groups a store instruction writes over distinct banks).
+    constexpr bool F32OUT = EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU_POS;
+    constexpr int ESZ = F32OUT ? 4 : 2;
+    constexpr int RS = 64 * ESZ + 16;          // LDS row stride (bytes)
+    constexpr int PR = F32OUT ? 64 : 128;      // rows per pass
+    constexpr int CPR = 64 * ESZ / 16;         // 16-byte chunks per row (8 or 16)
+    constexpr int RPI = 64 / CPR;              // rows per wave-instruction (8 or 4)
+    char* wreg = smem + wid * (PR * RS);
+    float bv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bv[j] = g.bias ? g.bias[n0 + wc * 64 + 16 * j + fr] : 0.0f;
+#pragma unroll
+    for (int pass = 0; pass < 128 / PR; ++pass) {
+#pragma unroll
+        for (int ii = 0; ii < PR / 16; ++ii) {
+            const int i = pass * (PR / 16) + ii;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int rl = 16 * ii + 4 * fq + r, cl = 16 * j + fr;
+                    float v = acc[i][j][r] + bv[j];
+                    if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_POS) v = gelu_tanh(v);
+                    if constexpr (F32OUT) *(float*)(wreg + rl * RS + cl * 4) = v;
+                    else *(bf16*)(wreg + rl * RS + cl * 2) = f2bf(v);
+                }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+        __builtin_amdgcn_wave_barrier();
+        const int ch = lane % CPR, rsub = lane / CPR;
+#pragma unroll
+        for (int it = 0; it < PR / RPI; ++it) {
+            const int rl = it * RPI + rsub;
+            const int row = m0 + wr * 128 + pass * PR + rl;
+            const uint4 v = *(const uint4*)(wreg + rl * RS + ch * 16);
+            if (row >= g.M) continue;
+            const int col = n0 + wc * 64 + ch * (16 / ESZ);
+            if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+                *(uint4*)((bf16*)g.C + (size_t)bz * g.sC + (size_t)row * g.ldc + col) = v;
+            } else if constexpr (EPI == EPI_KVSPLIT) {
+                const int d = g.kv_H * 64;
+                const int l = col / (2 * d), rem = col - l * 2 * d;
+                const int kvi = rem / d, hh = (rem - kvi * d) >> 6, el = rem & 63;
+                const int bb = row / g.kv_T, t = row - bb * g.kv_T;
+                const int64_t off = ((((int64_t)(l * 2 + kvi) * g.kv_B + bb) * g.kv_H + hh) * g.kv_T + t) * 64 + el;
+                *(uint4*)((bf16*)g.C + off) = v;
+            } else {
+                float* cp = (float*)g.C + (size_t)bz * g.sC + (size_t)row * g.ldc + col;
+                float4 o = *(const float4*)&v;
+                float4 y;
+                if constexpr (EPI == EPI_BIAS_RESID) y = *(const float4*)cp;
+                else y = *(const float4*)(g.pos + (size_t)row * g.N + col);
+                o.x += y.x; o.y += y.y; o.z += y.z; o.w += y.w;
+                *(float4*)cp = o;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+template <int EPI>
+void launch_256(const GemmArgs& g, int batch, hipStream_t st) {
+    static bool attr = false;  // > 64 KiB dynamic LDS: set once per kernel
+    if (!attr) {
+        HIP_CHECK(hipFuncSetAttribute((const void*)gemm256_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS_ALL));
+        attr = true;
+    }
+    dim3 grid(cdiv(g.M, G2_BM) * (g.N / G2_BN), 1, batch);
+    hipLaunchKernelGGL((gemm256_kernel<EPI>), grid, dim3(512), G2_LDS_ALL, st, g);
+    SPT_LAUNCH_CHECK();
 }
 
 template <typename T, int EPI>
@@ -186,12 +430,26 @@ void launch_t(const GemmArgs& g, int batch, hipStream_t st) {
 
 }  // namespace
 
-void gemm_nt(int dtype, int epi, const GemmArgs& g, int batch, hipStream_t st) {
+void gemm_nt(int dtype, int epi, const GemmArgs& g, int batch, hipStream_t st) { gemm_nt_variant(dtype, epi, g, batch, 0, st); }
+
+void gemm_nt_variant(int dtype, int epi, const GemmArgs& g, int batch, int variant, hipStream_t st) {
     if (g.N % BN != 0 || (g.K * (dtype == DT_BF16 ? 2 : 4)) % SLAB != 0 || g.M <= 0)
         throw std::runtime_error("gemm_nt: unsupported shape M=" + std::to_string(g.M) + " N=" +
                                  std::to_string(g.N) + " K=" + std::to_string(g.K));
 #define SPT_GEMM_CASE(T, E) \
     case E: launch_t<T, E>(g, batch, st); return;
+    static const bool force128 = getenv("SPT_GEMM128") != nullptr;  // A/B switch for measurements
+    const bool use256 = variant == 2 || (variant == 0 && !force128);
+    const bool fits32 = (int64_t)g.M * g.lda < (1ll << 31) && (int64_t)g.N * g.ldw < (1ll << 31);
+    if (dtype == DT_BF16 && use256 && fits32 && g.N % G2_BN == 0 && g.K % 64 == 0) {
+        switch (epi) {
+            case EPI_BIAS: launch_256<EPI_BIAS>(g, batch, st); return;
+            case EPI_BIAS_GELU: launch_256<EPI_BIAS_GELU>(g, batch, st); return;
+            case EPI_BIAS_GELU_POS: launch_256<EPI_BIAS_GELU_POS>(g, batch, st); return;
+            case EPI_BIAS_RESID: launch_256<EPI_BIAS_RESID>(g, batch, st); return;
+            case EPI_KVSPLIT: launch_256<EPI_KVSPLIT>(g, batch, st); return;
+        }
+    }
     if (dtype == DT_BF16) {
         switch (epi) {
             SPT_GEMM_CASE(bf16, EPI_BIAS)

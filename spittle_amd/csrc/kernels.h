@@ -20,6 +20,8 @@ struct GemmArgs {
     int kv_B, kv_T, kv_H;                 // EPI_KVSPLIT: dest [L][2][kv_B][kv_H][kv_T][64]
 };
 void gemm_nt(int dtype, int epi, const GemmArgs& g, int batch, hipStream_t st);
+// variant 0: automatic (bf16 N % 256 == 0 -> 256 x 256 tile); 1: 128 x 128 tile; 2: prefer 256 x 256
+void gemm_nt_variant(int dtype, int epi, const GemmArgs& g, int batch, int variant, hipStream_t st);
 
 // ------------------------------------------------------------------ weights (k_init.hip)
 enum { WK_MAT = 0, WK_BIAS = 1, WK_LNW = 2, WK_LNB = 3, WK_TOK = 4, WK_DPOS = 5 };

@@ -3,7 +3,7 @@
 //   ubench gemv  N K R mode ln dtype [ksplit npend]  mode: 0 bias 1 gelu 2 partial 3 qkv 4 logits 5 resid
 //   ubench attn  B H ctx nkeys Tq dtype   self-attention
 //   ubench xattn B T Tq dtype            cross-attention
-//   ubench gemm  M N K epi dtype
+//   ubench gemm  M N K epi dtype         128 vs 256 tile (time, bitwise diff)
 //   ubench layer B dtype                 one large-v3 decoder layer (8 launches)
 //   ubench layer2 B dtype [...]          two such chains on two streams
 //   ubench null
@@ -124,6 +124,44 @@ int main(int argc, char** argv) {
         const double us = time_us(st, iters, [&] { dec_cross_attn(dt, q, kv, B, B, H, T, Tq, out, st); });
         printf("cross-attn B=%d T=%d Tq=%d dt=%d : %.2f us  %.0f GB/s\n", B, T, Tq, dt, us,
                2.0 * B * H * T * 64 * esz / us / 1e3);
+        return 0;
+    }
+    if (what == "gemm") {  // 128 x 128 vs 256 x 256 tile: timing and bitwise agreement
+        const int M = ai(2, 12000), N = ai(3, 5120), K = ai(4, 1280), epi = ai(5, 0), dt = ai(6, DT_BF16);
+        void* A = drand((size_t)M * K, dt, 1, -2);
+        void* W = drand((size_t)N * K, dt, 2, -5);
+        float* bias = frand(N, 3, -5);
+        const size_t cbytes = (size_t)M * N * 4;
+        void* C = dalloc(cbytes);
+        GemmArgs g{};
+        g.A = A; g.lda = K; g.W = W; g.ldw = K; g.M = M; g.N = N; g.K = K; g.bias = bias; g.C = C; g.ldc = N;
+        g.kv_B = M / 1500; g.kv_T = 1500; g.kv_H = 20;
+        if (epi == EPI_BIAS_GELU_POS) g.pos = frand((size_t)M * N, 4, 0);
+        HIP_CHECK(hipDeviceSynchronize());  // inputs are generated on the null stream
+        std::vector<char> ref(cbytes), out(cbytes);
+        double us[3] = {0, 0, 0};
+        for (int v = 1; v <= 2; ++v) {
+            HIP_CHECK(hipMemsetAsync(C, 0, cbytes, st));
+            gemm_nt_variant(dt, epi, g, 1, v, st);
+            HIP_CHECK(hipStreamSynchronize(st));
+            HIP_CHECK(hipMemcpy(v == 1 ? ref.data() : out.data(), C, cbytes, hipMemcpyDeviceToHost));
+            us[v] = time_us(st, 20, [&] { gemm_nt_variant(dt, epi, g, 1, v, st); });
+        }
+        size_t diff = 0, shown = 0;
+        for (size_t i = 0; i < cbytes; ++i) {
+            if (ref[i] == out[i]) continue;
+            ++diff;
+            if (shown < 6 && epi == EPI_KVSPLIT && (i & 1) == 0) {  // decode [L][2][B][H][T][64] bf16
+                const size_t e = i / 2, el = e % 64, t = e / 64 % 1500, h = e / 64 / 1500 % 20, bb = e / 64 / 1500 / 20 % g.kv_B,
+                             lk = e / 64 / 1500 / 20 / g.kv_B;
+                const size_t row = bb * 1500 + t, col = (lk / 2) * 2560 + (lk % 2) * 1280 + h * 64 + el;
+                printf("  diff at row %zu col %zu: 128=%04x 256=%04x\n", row, col, ((uint16_t*)ref.data())[e], ((uint16_t*)out.data())[e]);
+                ++shown;
+            }
+        }
+        const double fl = 2.0 * M * N * K;
+        printf("gemm M=%d N=%d K=%d epi=%d dt=%d : 128-tile %.2f us %.1f TF/s | 256-tile %.2f us %.1f TF/s | bytes differing %zu\n",
+               M, N, K, epi, dt, us[1], fl / us[1] / 1e6, us[2], fl / us[2] / 1e6, diff);
         return 0;
     }
     if (what == "layer" || what == "layer2") {
