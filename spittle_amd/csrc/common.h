@@ -35,8 +35,12 @@ __host__ __device__ inline float bf2f(bf16 v) {
     x.u = (uint32_t)v << 16;
     return x.f;
 }
-// round-to-nearest-even (inputs are finite in this pipeline)
+// round-to-nearest-even; on the device one v_cvt_pk_bf16_f32 (same RNE for finite inputs,
+// keeps NaNs NaN), on the host the integer form
 __host__ __device__ inline bf16 f2bf(float f) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_bit_cast(bf16, (__bf16)f);
+#endif
     union { uint32_t u; float f; } x;
     x.f = f;
     uint32_t u = x.u;
@@ -59,9 +63,13 @@ template <typename T> __device__ inline T from_f(float v);
 template <> __device__ inline float from_f<float>(float v) { return v; }
 template <> __device__ inline bf16 from_f<bf16>(float v) { return f2bf(v); }
 
+// GELU, tanh form (ggml / whisper.cpp): 0.5 x (1 + tanh(u)), u = sqrt(2/pi) (x + 0.044715 x^3),
+// evaluated as x * sigmoid(2u) = x / (1 + 2^(-2u log2 e)): one v_exp_f32 + one v_rcp_f32
+// instead of tanhf (the same function; differs from libm tanhf by a few f32 ulp)
 __device__ inline float gelu_tanh(float x) {
-    const float c = 0.7978845608028654f;
-    return 0.5f * x * (1.0f + tanhf(c * (x + 0.044715f * x * x * x)));
+    const float c2 = -2.0f * 0.7978845608028654f * 1.4426950408889634f;
+    const float e = __builtin_amdgcn_exp2f(c2 * (x + 0.044715f * x * x * x));
+    return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
 
 __device__ inline float wave_sum(float v) {
