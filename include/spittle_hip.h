@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 1
+#define SPT_ABI_VERSION 2
 
 typedef enum {
     SPT_OK = 0,
@@ -61,15 +61,19 @@ typedef struct {
 } spt_model_params;
 
 typedef struct {
-    const char* language;        /* ISO-639-1 ("en", "zh", ...); NULL = auto-detect */
+    const char* language;        /* ISO-639-1 ("en", "zh", ...); NULL or "auto" = auto-detect
+                                    (whisper_lang_auto_detect on the utterance's first 30 s) */
     int32_t translate;           /* task <|translate|> instead of <|transcribe|> */
-    const char* initial_prompt;  /* jargon prompt (src-tauri/src/jargon.rs:594); needs a vocab */
+    const char* initial_prompt;  /* jargon prompt text (src-tauri/src/jargon.rs:594); needs a vocab */
     uint32_t flags;              /* SPT_SUPPRESS_BLANK | SPT_NO_TIMESTAMPS | SPT_IGNORE_EOT */
     int32_t max_new_tokens;      /* generated tokens per 30 s window (<= 220 like whisper.cpp) */
     float temperature;           /* only 0 (greedy) is implemented */
     int32_t beam_size;           /* only 1 (greedy) is implemented */
     const int32_t* forced_tokens;/* test hook (teacher forcing): [batch][n_forced] or NULL */
     int32_t n_forced;
+    const int32_t* prompt_tokens;/* whisper_full_params.prompt_tokens: decoded before [sot ...] as
+                                    [prev] + the last min(224, n) of them; NULL = none */
+    int32_t n_prompt_tokens;
 } spt_infer_params;
 
 typedef struct {
@@ -79,6 +83,8 @@ typedef struct {
     float* top2;            /* runner-up suppressed logit, per step */
     int32_t n_tokens;
     int32_t n_windows;      /* 30 s windows the input was split into */
+    int32_t language;       /* language index decoded with (whisper.cpp order, spt_language_code);
+                               -1 for English-only models */
 } spt_result;
 
 typedef struct {
@@ -119,6 +125,8 @@ spt_status spt_transcribe_batch(spt_ctx* ctx, const float* const* pcm, const siz
 spt_status spt_transcribe_batch_device(spt_ctx* ctx, const float* pcm_dev, size_t stride, const size_t* n_samples,
                                        size_t batch, const spt_infer_params* params, spt_result** out);
 void spt_result_free(spt_result* r);
+/* ISO-639-1 code of a language index ("en" = 0, "zh" = 1, ...), NULL if out of range */
+const char* spt_language_code(int32_t lang_id);
 
 spt_status spt_get_timings(const spt_ctx* ctx, spt_timings* t);
 

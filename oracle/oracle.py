@@ -77,6 +77,7 @@ def lib():
         L.wo_decode.argtypes = [C.c_void_p, fp, ip, C.c_int, C.c_int, C.c_uint32, C.c_int, ip, ip, fp, fp]
         L.wo_decode_logits.argtypes = [C.c_void_p, fp, ip, C.c_int, C.c_int, fp]
         L.wo_special_tokens.argtypes = [C.c_int, ip]
+        L.wo_lang_detect.argtypes = [C.c_void_p, fp, C.c_int, fp]
         _lib = L
     return _lib
 
@@ -121,11 +122,15 @@ def special_tokens(n_vocab: int) -> dict:
     return dict(zip(keys, (int(x) for x in o)))
 
 
-def default_prompt(n_vocab: int, lang_id: int = 0, translate: bool = False) -> list[int]:
+def default_prompt(n_vocab: int, lang_id: int = 0, translate: bool = False, past=None) -> list[int]:
     """[sot, lang, task, notimestamps] for multilingual, [sot, notimestamps] for .en
-    (whisper_full's prompt_init with no_timestamps)."""
+    (whisper_full's prompt_init with no_timestamps); with `past` (prompt tokens) whisper_full
+    prepends [prev] + the last min(n_text_ctx / 2 = 224, len) of them."""
     sp = special_tokens(n_vocab)
-    p = [sp["sot"]]
+    p = []
+    if past is not None and len(past) > 0:
+        p = [sp["prev"]] + [int(t) for t in list(past)[-224:]]
+    p.append(sp["sot"])
     if sp["n_langs"] > 0:
         p += [sp["sot"] + 1 + lang_id, sp["translate"] if translate else sp["transcribe"]]
     p.append(sp["not"])
@@ -179,6 +184,15 @@ class Model:
         if rc < 0:
             raise ValueError("wo_decode failed")
         return toks, t1, t2
+
+    def detect_language(self, enc: np.ndarray, gelu: int = GELU_TANH):
+        """whisper_lang_auto_detect: (language index, softmax probabilities over languages);
+        (-1, None) for an English-only vocabulary."""
+        enc = np.ascontiguousarray(enc, dtype=np.float32)
+        n = special_tokens(self.dims.n_vocab)["n_langs"]
+        probs = np.zeros(max(n, 1), np.float32)
+        lid = lib().wo_lang_detect(self._p, _f(enc), gelu, _f(probs))
+        return lid, (probs[:n] if n > 0 else None)
 
     def logits(self, enc: np.ndarray, toks, gelu: int = GELU_TANH) -> np.ndarray:
         enc = np.ascontiguousarray(enc, dtype=np.float32)

@@ -534,6 +534,36 @@ int wo_decode_logits(const wo_model* m, const float* enc, const int32_t* toks, i
     return 0;
 }
 
+/* whisper.cpp whisper_lang_auto_detect_with_state, offset_ms = 0: decode [sot] at n_past 0,
+ * take the logits of the n_langs language tokens (sot + 1 + i), sort them descending and
+ * return the first; probabilities are the softmax over the language logits only. */
+int wo_lang_detect(const wo_model* m, const float* enc, int gelu_mode, float* probs) {
+    int32_t sp[10];
+    wo_special_tokens(m->dm.n_vocab, sp);
+    const int n_langs = sp[9];
+    if (n_langs <= 0) return -1;
+    dec_state s;
+    dec_state_init(m, enc, &s, 1);
+    const int32_t sot = sp[1];
+    dec_forward(m, &s, &sot, 1, 0, gelu_mode);
+    int best = 0;
+    float bmax = -INFINITY;
+    for (int i = 0; i < n_langs; i++) {
+        const float v = s.logits[sot + 1 + i];
+        if (v > bmax) { bmax = v; best = i; }
+    }
+    if (probs) {
+        double sum = 0.0;
+        for (int i = 0; i < n_langs; i++) {
+            probs[i] = expf(s.logits[sot + 1 + i] - bmax);
+            sum += probs[i];
+        }
+        for (int i = 0; i < n_langs; i++) probs[i] = (float)(probs[i] / sum);
+    }
+    dec_state_free(&s);
+    return best;
+}
+
 /* whisper_process_logits, greedy / no-timestamp subset */
 static void suppress(const wo_model* m, float* lg, int is_initial, uint32_t flags) {
     int32_t sp[10];

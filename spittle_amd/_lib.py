@@ -22,7 +22,7 @@ EXPORTS = [
     "spt_version", "spt_default_model_params", "spt_default_infer_params", "spt_ctx_create",
     "spt_ctx_destroy", "spt_last_error", "spt_ctx_info", "spt_transcribe", "spt_transcribe_batch",
     "spt_transcribe_batch_device", "spt_result_free", "spt_get_timings", "spt_debug_mel",
-    "spt_debug_encode", "spt_debug_weight_checksum", "spt_probe_kernel",
+    "spt_debug_encode", "spt_debug_weight_checksum", "spt_probe_kernel", "spt_language_code",
 ]
 PROBES = {"dec_cross_attn": 0, "dec_self_attn": 1, "dec_logits": 2, "dec_fc1": 3, "enc_fc1_gemm": 4,
           "enc_attn": 5}
@@ -36,12 +36,14 @@ class ModelParams(C.Structure):
 class InferParams(C.Structure):
     _fields_ = [("language", C.c_char_p), ("translate", C.c_int32), ("initial_prompt", C.c_char_p),
                 ("flags", C.c_uint32), ("max_new_tokens", C.c_int32), ("temperature", C.c_float),
-                ("beam_size", C.c_int32), ("forced_tokens", C.POINTER(C.c_int32)), ("n_forced", C.c_int32)]
+                ("beam_size", C.c_int32), ("forced_tokens", C.POINTER(C.c_int32)), ("n_forced", C.c_int32),
+                ("prompt_tokens", C.POINTER(C.c_int32)), ("n_prompt_tokens", C.c_int32)]
 
 
 class Result(C.Structure):
     _fields_ = [("text", C.c_char_p), ("tokens", C.POINTER(C.c_int32)), ("top1", C.POINTER(C.c_float)),
-                ("top2", C.POINTER(C.c_float)), ("n_tokens", C.c_int32), ("n_windows", C.c_int32)]
+                ("top2", C.POINTER(C.c_float)), ("n_tokens", C.c_int32), ("n_windows", C.c_int32),
+                ("language", C.c_int32)]
 
 
 class ModelInfo(C.Structure):
@@ -85,6 +87,8 @@ def load():
     L.spt_transcribe_batch_device.argtypes = [vp, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t), C.c_size_t,
                                               C.POINTER(InferParams), C.POINTER(C.POINTER(Result))]
     L.spt_result_free.argtypes = [C.POINTER(Result)]
+    L.spt_language_code.argtypes = [C.c_int32]
+    L.spt_language_code.restype = C.c_char_p
     L.spt_get_timings.argtypes = [vp, C.POINTER(Timings)]
     L.spt_debug_mel.argtypes = [vp, fp, C.c_size_t, fp]
     L.spt_debug_encode.argtypes = [vp, fp, fp]

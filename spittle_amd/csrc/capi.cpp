@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <algorithm>
 #include <memory>
 #include <new>
 #include <string>
@@ -51,30 +52,51 @@ spt_status classify(const std::exception& e) {
     return SPT_ERR_INVALID_ARG;
 }
 
-// whisper_full's prompt_init: [sot] (+ [lang, task] for multilingual) + [notimestamps]
-spt_status build_request(spt_ctx* c, const spt_infer_params* p, spt::DecodeRequest* rq) {
+// whisper_full's prompt_init: [sot] (+ [lang, task] for multilingual) + [notimestamps]; its
+// prompt_past ([prev] + the last n_text_ctx / 2 prompt tokens) goes to rq->prefix.  With no
+// language (the app's "auto", settings.rs:925) *auto is set and the caller fills rq->lang_tok.
+spt_status build_request(spt_ctx* c, const spt_infer_params* p, spt::DecodeRequest* rq, bool* autolang) {
     spt_infer_params d;
     spt_default_infer_params(&d);
     if (!p) p = &d;
     const spt::ModelDims& dm = c->eng->dims();
     const spt::Specials sp = spt::specials_for(dm.n_vocab);
+    *autolang = false;
     if (p->beam_size > 1) return fail(c, SPT_ERR_UNSUPPORTED, "beam search is not implemented (greedy only)");
     if (p->temperature != 0.0f) return fail(c, SPT_ERR_UNSUPPORTED, "only temperature 0 (greedy) is implemented");
     if (p->initial_prompt && p->initial_prompt[0])
-        return fail(c, SPT_ERR_UNSUPPORTED, "initial_prompt needs a tokenizer vocabulary (ggml model loading not implemented)");
+        return fail(c, SPT_ERR_UNSUPPORTED,
+                    "initial_prompt text needs the model's tokenizer vocabulary (ggml loading); pass prompt_tokens");
     rq->prompt.clear();
+    rq->prefix.clear();
+    rq->lang_tok.clear();
+    if (p->prompt_tokens && p->n_prompt_tokens > 0) {
+        const int n_take = std::min(p->n_prompt_tokens, dm.n_text_ctx / 2);
+        rq->prefix.push_back(sp.prev);
+        for (int i = p->n_prompt_tokens - n_take; i < p->n_prompt_tokens; ++i) {
+            const int t = p->prompt_tokens[i];
+            if (t < 0 || t >= dm.n_vocab) return fail(c, SPT_ERR_INVALID_ARG, "prompt token out of the vocabulary");
+            rq->prefix.push_back(t);
+        }
+    }
     rq->prompt.push_back(sp.sot);
     if (sp.n_langs > 0) {
-        if (!p->language) return fail(c, SPT_ERR_UNSUPPORTED, "language auto-detection is not implemented; pass a language");
-        const int lid = spt::lang_id(p->language);
-        if (lid < 0 || lid >= sp.n_langs) return fail(c, SPT_ERR_INVALID_ARG, std::string("unknown language '") + p->language + "'");
-        rq->prompt.push_back(sp.sot + 1 + lid);
+        const bool autod = !p->language || !p->language[0] || std::string(p->language) == "auto";
+        int lid = 0;
+        if (!autod) {
+            lid = spt::lang_id(p->language);
+            if (lid < 0 || lid >= sp.n_langs)
+                return fail(c, SPT_ERR_INVALID_ARG, std::string("unknown language '") + p->language + "'");
+        }
+        *autolang = autod;
+        rq->prompt.push_back(sp.sot + 1 + lid);  // replaced per sequence when auto-detecting
         rq->prompt.push_back(p->translate ? sp.translate : sp.transcribe);
     }
     if (p->flags & SPT_NO_TIMESTAMPS) rq->prompt.push_back(sp.not_);
     else return fail(c, SPT_ERR_UNSUPPORTED, "timestamp decoding is not implemented (set SPT_NO_TIMESTAMPS)");
     int n = p->max_new_tokens > 0 ? p->max_new_tokens : 220;
-    if ((int)rq->prompt.size() + n > dm.n_text_ctx + 1) n = dm.n_text_ctx + 1 - (int)rq->prompt.size();
+    const int used = (int)(rq->prefix.size() + rq->prompt.size());
+    if (used + n > dm.n_text_ctx + 1) n = dm.n_text_ctx + 1 - used;
     rq->n_steps = n;
     rq->flags = p->flags;
     rq->forced = p->forced_tokens;
@@ -83,15 +105,16 @@ spt_status build_request(spt_ctx* c, const spt_infer_params* p, spt::DecodeReque
     return SPT_OK;
 }
 
-spt_result* make_result(const int* tok, const float* t1, const float* t2, int n_steps, int n_windows, int eot,
-                        std::vector<int>* acc_tok, std::vector<float>* acc1, std::vector<float>* acc2,
-                        std::string* text) {
-    (void)tok; (void)t1; (void)t2; (void)n_steps; (void)eot;
+int lang_index(int lang_tok, const spt::Specials& sp) { return lang_tok > sp.sot ? lang_tok - sp.sot - 1 : -1; }
+
+spt_result* make_result(int n_windows, int language, std::vector<int>* acc_tok, std::vector<float>* acc1,
+                        std::vector<float>* acc2, std::string* text) {
     spt_result* r = (spt_result*)calloc(1, sizeof(spt_result));
     if (!r) return nullptr;
     const size_t n = acc_tok->size();
     r->n_tokens = (int32_t)n;
     r->n_windows = n_windows;
+    r->language = language;
     r->tokens = (int32_t*)malloc(sizeof(int32_t) * (n ? n : 1));
     r->top1 = (float*)malloc(sizeof(float) * (n ? n : 1));
     r->top2 = (float*)malloc(sizeof(float) * (n ? n : 1));
@@ -115,14 +138,19 @@ struct Window { int utt; const float* host; const float* dev; int n; };
 spt_status run_windows(spt_ctx* c, std::vector<Window>& win, size_t n_utt, const spt_infer_params* p,
                        spt_result** out) {
     spt::DecodeRequest rq;
-    spt_status s = build_request(c, p, &rq);
+    bool autolang = false;
+    spt_status s = build_request(c, p, &rq, &autolang);
     if (s != SPT_OK) return s;
     Engine& e = *c->eng;
-    const int eot = spt::specials_for(e.dims().n_vocab).eot;
+    const spt::Specials sp = spt::specials_for(e.dims().n_vocab);
+    const int eot = sp.eot;
     std::vector<std::vector<int>> tok(n_utt);
     std::vector<std::vector<float>> t1(n_utt), t2(n_utt);
     std::vector<std::string> text(n_utt);
     std::vector<int> nwin(n_utt, 0);
+    // language per utterance: fixed, or detected on its first window (whisper_full detects once
+    // per call from offset 0); later windows reuse it
+    std::vector<int> utt_lang(n_utt, (!autolang && rq.prompt.size() >= 3) ? rq.prompt[1] : -1);
     const int cap = e.max_batch();
     for (size_t g0 = 0; g0 < win.size(); g0 += cap) {
         const int B = (int)std::min<size_t>(cap, win.size() - g0);
@@ -132,16 +160,27 @@ spt_status run_windows(spt_ctx* c, std::vector<Window>& win, size_t n_utt, const
             ns[b] = win[g0 + b].n;
             hp[b] = win[g0 + b].host;
         }
-        std::vector<int> otok((size_t)B * rq.n_steps);
+        if (autolang) {
+            rq.lang_tok.assign(B, 0);
+            for (int b = 0; b < B; ++b) {
+                const int u = win[g0 + b].utt;
+                if (utt_lang[u] >= 0) { rq.lang_tok[b] = utt_lang[u]; continue; }
+                int src = b;  // the utterance's first window in this batch
+                while (src > 0 && win[g0 + src - 1].utt == u) --src;
+                rq.lang_tok[b] = -(src + 1);
+            }
+        }
+        std::vector<int> otok((size_t)B * rq.n_steps), lang(B, -1);
         std::vector<float> o1((size_t)B * rq.n_steps), o2((size_t)B * rq.n_steps);
         if (win[g0].dev) {
             // device windows are laid out contiguously by the caller (stride in Window.n is the slot)
-            e.transcribe_device(win[g0].dev, kWindow, ns.data(), B, rq, otok.data(), o1.data(), o2.data());
+            e.transcribe_device(win[g0].dev, kWindow, ns.data(), B, rq, otok.data(), o1.data(), o2.data(), lang.data());
         } else {
-            e.transcribe_host(hp.data(), ns.data(), B, rq, otok.data(), o1.data(), o2.data());
+            e.transcribe_host(hp.data(), ns.data(), B, rq, otok.data(), o1.data(), o2.data(), lang.data());
         }
         for (int b = 0; b < B; ++b) {
             const int u = win[g0 + b].utt;
+            if (utt_lang[u] < 0) utt_lang[u] = lang[b];
             nwin[u]++;
             for (int s2 = 0; s2 < rq.n_steps; ++s2) {
                 const int t = otok[(size_t)b * rq.n_steps + s2];
@@ -155,7 +194,7 @@ spt_status run_windows(spt_ctx* c, std::vector<Window>& win, size_t n_utt, const
         }
     }
     for (size_t u = 0; u < n_utt; ++u) {
-        out[u] = make_result(nullptr, nullptr, nullptr, 0, nwin[u], eot, &tok[u], &t1[u], &t2[u], &text[u]);
+        out[u] = make_result(nwin[u], lang_index(utt_lang[u], sp), &tok[u], &t1[u], &t2[u], &text[u]);
         if (!out[u]) {
             for (size_t v = 0; v < u; ++v) { spt_result_free(out[v]); out[v] = nullptr; }
             return fail(c, SPT_ERR_OOM, "host allocation failed");
@@ -168,7 +207,9 @@ spt_status run_windows(spt_ctx* c, std::vector<Window>& win, size_t n_utt, const
 
 extern "C" {
 
-const char* spt_version(void) { return "spittle_amd 0.1.0 (gfx950, ABI 1)"; }
+const char* spt_version(void) { return "spittle_amd 0.2.0 (gfx950, ABI 2)"; }
+
+const char* spt_language_code(int32_t lang_id) { return spt::lang_code(lang_id); }
 
 void spt_default_model_params(spt_model_params* p) {
     if (!p) return;
@@ -286,7 +327,7 @@ spt_status spt_transcribe_batch(spt_ctx* ctx, const float* const* pcm, const siz
         for (size_t u : empty) {
             if (out[u]) spt_result_free(out[u]);
             std::vector<int> t; std::vector<float> a, b; std::string txt;
-            out[u] = make_result(nullptr, nullptr, nullptr, 0, 0, 0, &t, &a, &b, &txt);
+            out[u] = make_result(0, -1, &t, &a, &b, &txt);
         }
         return SPT_OK;
     } catch (const std::exception& e) {
@@ -308,20 +349,26 @@ spt_status spt_transcribe_batch_device(spt_ctx* ctx, const float* pcm_dev, size_
     if (batch > (size_t)ctx->eng->max_batch()) return fail(ctx, SPT_ERR_INVALID_ARG, "batch exceeds max_batch");
     if (stride < (size_t)kWindow) return fail(ctx, SPT_ERR_INVALID_ARG, "device stride must be >= 480000");
     spt::DecodeRequest rq;
-    spt_status s = build_request(ctx, params, &rq);
+    bool autolang = false;
+    spt_status s = build_request(ctx, params, &rq, &autolang);
     if (s != SPT_OK) return s;
     try {
         std::vector<int> ns(batch);
+        if (autolang) {  // each window is its own utterance here
+            rq.lang_tok.resize(batch);
+            for (size_t b = 0; b < batch; ++b) rq.lang_tok[b] = -(int)(b + 1);
+        }
         for (size_t b = 0; b < batch; ++b) {
             if (n_samples[b] > (size_t)kWindow) return fail(ctx, SPT_ERR_INVALID_ARG, "device windows hold <= 480000 samples");
             ns[b] = (int)n_samples[b];
         }
         Engine& e = *ctx->eng;
         const int B = (int)batch;
-        std::vector<int> otok((size_t)B * rq.n_steps);
+        std::vector<int> otok((size_t)B * rq.n_steps), lang(B, -1);
         std::vector<float> o1((size_t)B * rq.n_steps), o2((size_t)B * rq.n_steps);
-        e.transcribe_device(pcm_dev, (int64_t)stride, ns.data(), B, rq, otok.data(), o1.data(), o2.data());
-        const int eot = spt::specials_for(e.dims().n_vocab).eot;
+        e.transcribe_device(pcm_dev, (int64_t)stride, ns.data(), B, rq, otok.data(), o1.data(), o2.data(), lang.data());
+        const spt::Specials sp = spt::specials_for(e.dims().n_vocab);
+        const int eot = sp.eot;
         for (int b = 0; b < B; ++b) {
             std::vector<int> t; std::vector<float> a, c2; std::string txt;
             for (int s2 = 0; s2 < rq.n_steps; ++s2) {
@@ -333,7 +380,7 @@ spt_status spt_transcribe_batch_device(spt_ctx* ctx, const float* pcm_dev, size_
                 if (tk < eot) txt += "[" + std::to_string(tk) + "]";
                 if (tk == eot && !(rq.flags & SPT_IGNORE_EOT)) break;
             }
-            out[b] = make_result(nullptr, nullptr, nullptr, 0, 1, eot, &t, &a, &c2, &txt);
+            out[b] = make_result(1, lang_index(lang[b], sp), &t, &a, &c2, &txt);
         }
         return SPT_OK;
     } catch (const std::exception& e) {

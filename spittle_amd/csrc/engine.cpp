@@ -41,18 +41,22 @@ Specials specials_for(int n_vocab) {
     return s;
 }
 
+static const char* const kLangs[] = {
+    "en", "zh", "de", "es", "ru", "ko", "fr", "ja", "pt", "tr", "pl", "ca", "nl", "ar", "sv", "it", "id",
+    "hi", "fi", "vi", "he", "uk", "el", "ms", "cs", "ro", "da", "hu", "ta", "no", "th", "ur", "hr", "bg",
+    "lt", "la", "mi", "ml", "cy", "sk", "te", "fa", "lv", "bn", "sr", "az", "sl", "kn", "et", "mk", "br",
+    "eu", "is", "hy", "ne", "mn", "bs", "kk", "sq", "sw", "gl", "mr", "pa", "si", "km", "sn", "yo", "so",
+    "af", "oc", "ka", "be", "tg", "sd", "gu", "am", "yi", "lo", "uz", "fo", "ht", "ps", "tk", "nn", "mt",
+    "sa", "lb", "my", "bo", "tl", "mg", "as", "tt", "haw", "ln", "ha", "ba", "jw", "su", "yue"};
+constexpr int kNumLangs = (int)(sizeof(kLangs) / sizeof(kLangs[0]));
+
 int lang_id(const std::string& code) {
-    static const char* langs[] = {
-        "en", "zh", "de", "es", "ru", "ko", "fr", "ja", "pt", "tr", "pl", "ca", "nl", "ar", "sv", "it", "id",
-        "hi", "fi", "vi", "he", "uk", "el", "ms", "cs", "ro", "da", "hu", "ta", "no", "th", "ur", "hr", "bg",
-        "lt", "la", "mi", "ml", "cy", "sk", "te", "fa", "lv", "bn", "sr", "az", "sl", "kn", "et", "mk", "br",
-        "eu", "is", "hy", "ne", "mn", "bs", "kk", "sq", "sw", "gl", "mr", "pa", "si", "km", "sn", "yo", "so",
-        "af", "oc", "ka", "be", "tg", "sd", "gu", "am", "yi", "lo", "uz", "fo", "ht", "ps", "tk", "nn", "mt",
-        "sa", "lb", "my", "bo", "tl", "mg", "as", "tt", "haw", "ln", "ha", "ba", "jw", "su", "yue"};
-    for (int i = 0; i < (int)(sizeof(langs) / sizeof(langs[0])); ++i)
-        if (code == langs[i]) return i;
+    for (int i = 0; i < kNumLangs; ++i)
+        if (code == kLangs[i]) return i;
     return -1;
 }
+
+const char* lang_code(int id) { return (id >= 0 && id < kNumLangs) ? kLangs[id] : nullptr; }
 
 bool parse_synthetic_spec(const std::string& spec, ModelDims* dm, uint64_t* seed, std::string* err) {
     const std::string pfx = "synthetic:";
@@ -349,7 +353,7 @@ void Engine::upload_tables() {
 // ----------------------------------------------------------------------------- workspace
 void Engine::alloc_workspace() {
     const int64_t B = max_batch_, d = dm_.d, T = dm_.n_audio_ctx, L = dm_.n_dec, ctx = dm_.n_text_ctx;
-    const int64_t H = dm_.n_head, V = dm_.n_vocab, R = B * 4;
+    const int64_t V = dm_.n_vocab, R = B * 4;
     for (int pass = 0; pass < 2; ++pass) {
         Carver c{pass ? aarena_ : nullptr};
         auto A = [&](int64_t n) { return c.take(n * esz_); };
@@ -367,6 +371,7 @@ void Engine::alloc_workspace() {
         enc_out_ = A(B * T * d);
         ckv_ = A(L * 2 * B * T * d);
         suppress_ = (uint32_t*)c.take((V / 32 + 1) * 4);
+        suppress_lang_ = (uint32_t*)c.take((V / 32 + 1) * 4);
         scratch_ = (double*)c.take(64);
         for (DecGroup& g : groups_) {  // each group sized for the whole batch (groups are re-sliced per call)
             g.dx = (float*)c.take(R * d * 4);
@@ -467,6 +472,13 @@ void Engine::run_cross_kv(int B) {
 // attention output projection keeps the read-modify-write residual add, because slabs there
 // would land on the 320-workgroup fc1 LayerNorm prologue (+1.2 us per slab measured).
 void Engine::enqueue_decoder_pass(DecGroup& g, int B_total, int Tq, const DecodeRequest& rq, int out_cap) {
+    float* x = enqueue_layers(g, B_total, Tq);
+    enqueue_head(g, Tq, rq, out_cap, x, suppress_, (rq.flags & 1u) != 0);
+}
+
+// The decoder layers over this pass's Tq input rows per sequence (embedded in g.dx); returns
+// the residual buffer holding the result (plus g.pend's pending slabs, n = fc2's split).
+float* Engine::enqueue_layers(DecGroup& g, int B_total, int Tq) {
     const int d = dm_.d, H = dm_.n_head, ctx = dm_.n_text_ctx, T = dm_.n_audio_ctx, B = g.B, R = B * Tq;
     const int64_t self_layer = (int64_t)2 * B * H * ctx * 64, cross_layer = (int64_t)2 * B_total * H * T * 64;
     const int ks = dt_ == DT_BF16 ? 128 : 64;
@@ -531,16 +543,28 @@ void Engine::enqueue_decoder_pass(DecGroup& g, int B_total, int Tq, const Decode
         partial(a, fc2_split_);
         gemv(dt_, GV_PARTIAL, A_DIRECT, a, st);
     }
+    return xc;
+}
+
+// Final LayerNorm of each sequence's last row + logits (suppression mask `sup`, the step-0
+// blank rule when `blank`) + top-2 partials, then argmax / record / next embedding / advance.
+void Engine::enqueue_head(DecGroup& g, int Tq, const DecodeRequest& rq, int out_cap, float* xc,
+                          const uint32_t* sup, bool blank) {
+    const int d = dm_.d, ctx = dm_.n_text_ctx, B = g.B, R = B * Tq;
+    hipStream_t st = g.st;
     const Specials sp = specials_for(dm_.n_vocab);
     const int n_tiles = (dm_.n_vocab + 15) / 16;
     GemvArgs a{};
-    ln_input(a);  // final LayerNorm of the last token of each sequence; the combined rows are not needed
-    a.x_out = nullptr;
+    // final LayerNorm of the last token of each sequence (x + fc2's pending slabs); the
+    // combined rows are not needed
+    a.A = xc;
+    for (int p = 0; p < kMaxPend; ++p) a.pend[p] = p < fc2_split_ ? g.pend + (int64_t)p * R * d : zero_;
+    a.n_pend = fc2_split_;
     a.lda = Tq * d; a.a_row0 = (Tq - 1) * d; a.ln_w = lnf_w_; a.ln_b = lnf_b_; a.R = B;
     a.W = tok_emb_; a.N = dm_.n_vocab; a.K = d; a.C = g.logits; a.ldc = dm_.n_vocab; a.st = g.ds;
-    a.suppress = suppress_;
-    a.blank0 = (rq.flags & 1u) ? sp.eot : -1;
-    a.blank1 = (rq.flags & 1u) ? 220 : -1;
+    a.suppress = sup;
+    a.blank0 = blank ? sp.eot : -1;
+    a.blank1 = blank ? 220 : -1;
     a.part = g.part; a.n_tiles = n_tiles;
     gemv(dt_, GV_LOGITS, A_LN, a, st);
     FinalizeArgs f{};
@@ -554,12 +578,18 @@ void Engine::enqueue_decoder_pass(DecGroup& g, int B_total, int Tq, const Decode
     dec_finalize(dt_, f, B, st);
 }
 
-void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1, float* top2) {
+void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1, float* top2, int* lang_out) {
     const int Tq = (int)rq.prompt.size();
     const int ctx = dm_.n_text_ctx;
+    const int P = (int)rq.prefix.size();
     if (Tq < 1 || Tq > 4) throw std::runtime_error("prompt must have 1..4 tokens");
     if (B * Tq > 64) throw std::runtime_error("batch x prompt rows exceed 64");
-    if (rq.n_steps < 1 || Tq + rq.n_steps > ctx + 1) throw std::runtime_error("n_steps out of range");
+    if (P > ctx / 2 + 1) throw std::runtime_error("prompt prefix longer than n_text_ctx / 2 + 1");
+    for (int t : rq.prefix)
+        if (t < 0 || t >= dm_.n_vocab) throw std::runtime_error("prompt token out of the vocabulary");
+    if (!rq.lang_tok.empty() && ((int)rq.lang_tok.size() != B || Tq < 3))
+        throw std::runtime_error("per-sequence language tokens need a [sot, lang, task, ...] prompt");
+    if (rq.n_steps < 1 || P + Tq + rq.n_steps > ctx + 1) throw std::runtime_error("n_steps out of range");
     if (rq.n_forced > ctx) throw std::runtime_error("too many forced tokens");
     const int out_cap = rq.n_steps;
     const Specials sp = specials_for(dm_.n_vocab);
@@ -582,8 +612,6 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
     const int G = std::min(n_groups_, B);
     HIP_CHECK(hipEventRecord(ev_[6], st_));
     std::vector<DecGroup*> act;
-    static thread_local std::vector<std::vector<int>> tins;  // host sources of async copies outlive the call
-    tins.resize(G);
     for (int gi = 0, b0 = 0; gi < G; ++gi) {
         DecGroup& g = groups_[gi];
         g.b0 = b0;
@@ -591,19 +619,80 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         b0 += g.B;
         act.push_back(&g);
         HIP_CHECK(hipStreamWaitEvent(g.st, ev_[6], 0));
-        std::vector<int>& tin = tins[gi];
-        tin.resize((size_t)g.B * Tq);
-        for (int b = 0; b < g.B; ++b)
-            for (int t = 0; t < Tq; ++t) tin[(size_t)b * Tq + t] = rq.prompt[t];
-        HIP_CHECK(hipMemcpyAsync(g.tok_in, tin.data(), tin.size() * 4, hipMemcpyHostToDevice, g.st));
+        // host sources of this call's token uploads (kept alive in the group until the next call)
+        g.host_tok.assign((size_t)g.B * (1 + 4 * ((rq.prefix.size() + 3) / 4 + 1)), 0);
+        g.host_used = 0;
         if (rq.n_forced > 0)
             HIP_CHECK(hipMemcpyAsync(g.forced, rq.forced + (size_t)g.b0 * rq.n_forced, (size_t)g.B * rq.n_forced * 4,
                                      hipMemcpyHostToDevice, g.st));
+    }
+    auto upload_tokens = [&](DecGroup& g, const std::function<int(int, int)>& tok, int n) {  // [g.B][n]
+        int* h = g.host_tok.data() + g.host_used;
+        for (int b = 0; b < g.B; ++b)
+            for (int t = 0; t < n; ++t) h[b * n + t] = tok(g.b0 + b, t);
+        g.host_used += g.B * n;
+        HIP_CHECK(hipMemcpyAsync(g.tok_in, h, (size_t)g.B * n * 4, hipMemcpyHostToDevice, g.st));
+    };
+    auto reset_outputs = [&](DecGroup& g) {
         HIP_CHECK(hipMemsetAsync(g.done, 0, g.B * 4, g.st));
         HIP_CHECK(hipMemsetAsync(g.out_tok, 0xFF, (size_t)g.B * out_cap * 4, g.st));
         fill_f32(g.out_t1, (int64_t)g.B * out_cap, -INFINITY, g.st);
         fill_f32(g.out_t2, (int64_t)g.B * out_cap, -INFINITY, g.st);
         dec_reset(g.ds, g.arrive, g.st);
+    };
+    // language auto-detection (whisper_lang_auto_detect_with_state): one pass on [sot] with every
+    // non-language token suppressed; the argmax is the language token
+    std::vector<int> lang(B, -1);
+    bool detect = false;
+    for (int v : rq.lang_tok) detect = detect || v < 0;
+    if (detect) {
+        if (sp.n_langs <= 0) throw std::runtime_error("language detection needs a multilingual model");
+        if (!suppress_lang_ready_) {
+            const int V = dm_.n_vocab;
+            std::vector<uint32_t> m(V / 32 + 1, ~0u);
+            for (int i = 0; i < sp.n_langs; ++i) m[(sp.sot + 1 + i) >> 5] &= ~(1u << ((sp.sot + 1 + i) & 31));
+            HIP_CHECK(hipMemcpy(suppress_lang_, m.data(), m.size() * 4, hipMemcpyHostToDevice));
+            suppress_lang_ready_ = true;
+        }
+        DecodeRequest dq;  // no forcing, no blank rule, EOT irrelevant
+        dq.flags = 4u;
+        for (DecGroup* g : act) {
+            reset_outputs(*g);
+            upload_tokens(*g, [&](int, int) { return sp.sot; }, 1);
+            dec_embed(dt_, g->tok_in, g->B, 1, dm_.d, tok_emb_, dec_pos_, g->ds, g->dx, g->st);
+            float* x = enqueue_layers(*g, B, 1);
+            enqueue_head(*g, 1, dq, out_cap, x, suppress_lang_, false);
+        }
+        std::vector<int> first((size_t)B * out_cap);
+        for (DecGroup* g : act) {
+            HIP_CHECK(hipMemcpyAsync(first.data() + (size_t)g->b0 * out_cap, g->out_tok, (size_t)g->B * out_cap * 4,
+                                     hipMemcpyDeviceToHost, g->st));
+            HIP_CHECK(hipStreamSynchronize(g->st));
+        }
+        for (int b = 0; b < B; ++b) {
+            const int v = rq.lang_tok[b];
+            lang[b] = v >= 0 ? v : first[(size_t)(-v - 1) * out_cap];
+            if (lang[b] <= sp.sot || lang[b] > sp.sot + sp.n_langs) throw std::runtime_error("language detection failed");
+        }
+    } else if (!rq.lang_tok.empty()) {
+        for (int b = 0; b < B; ++b) lang[b] = rq.lang_tok[b];
+    }
+    if (lang_out)
+        for (int b = 0; b < B; ++b) lang_out[b] = lang[b] >= 0 ? lang[b] : (Tq >= 3 ? rq.prompt[1] : -1);
+    for (DecGroup* gp : act) {
+        DecGroup& g = *gp;
+        reset_outputs(g);
+        // whisper_full prompt_past ([prev] + prompt tokens): prefilled in chunks of <= 4 rows per
+        // sequence through the decoder layers only (no logits), positions 0..P-1
+        const int P = (int)rq.prefix.size();
+        for (int c0 = 0; c0 < P; c0 += 4) {
+            const int n = std::min(4, P - c0);
+            upload_tokens(g, [&](int, int t) { return rq.prefix[c0 + t]; }, n);
+            dec_embed(dt_, g.tok_in, g.B * n, n, dm_.d, tok_emb_, dec_pos_, g.ds, g.dx, g.st);
+            enqueue_layers(g, B, n);
+            dec_advance(g.ds, n, g.st);
+        }
+        upload_tokens(g, [&](int b, int t) { return (t == 1 && lang[b] >= 0) ? lang[b] : rq.prompt[t]; }, Tq);
         dec_embed(dt_, g.tok_in, g.B * Tq, Tq, dm_.d, tok_emb_, dec_pos_, g.ds, g.dx, g.st);
         enqueue_decoder_pass(g, B, Tq, rq, out_cap);  // prompt pass produces token 0
     }
@@ -667,7 +756,7 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
 }
 
 void Engine::transcribe_device(const float* pcm_dev, int64_t stride, const int* n_samples, int B,
-                               const DecodeRequest& rq, int* tokens, float* top1, float* top2) {
+                               const DecodeRequest& rq, int* tokens, float* top1, float* top2, int* lang_out) {
     select();
     if (B < 1 || B > max_batch_) throw std::runtime_error("batch exceeds the context's max_batch");
     for (int b = 0; b < B; ++b)
@@ -682,7 +771,7 @@ void Engine::transcribe_device(const float* pcm_dev, int64_t stride, const int* 
     HIP_CHECK(hipEventRecord(ev_[3], st_));
     run_cross_kv(B);
     HIP_CHECK(hipEventRecord(ev_[4], st_));
-    run_decode(B, rq, tokens, top1, top2);
+    run_decode(B, rq, tokens, top1, top2, lang_out);
     HIP_CHECK(hipEventRecord(ev_[5], st_));
     HIP_CHECK(hipStreamSynchronize(st_));
     HIP_CHECK(hipGetLastError());
@@ -712,11 +801,11 @@ void Engine::stage_pcm(const float* const* pcm, const int* n, int B) {
 }
 
 void Engine::transcribe_host(const float* const* pcm, const int* n_samples, int B, const DecodeRequest& rq,
-                             int* tokens, float* top1, float* top2) {
+                             int* tokens, float* top1, float* top2, int* lang_out) {
     select();
     if (B < 1 || B > max_batch_) throw std::runtime_error("batch exceeds the context's max_batch");
     stage_pcm(pcm, n_samples, B);
-    transcribe_device(pcm_, 480000, n_samples, B, rq, tokens, top1, top2);
+    transcribe_device(pcm_, 480000, n_samples, B, rq, tokens, top1, top2, lang_out);
 }
 
 // ----------------------------------------------------------------------------- debug hooks

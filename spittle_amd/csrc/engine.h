@@ -23,9 +23,14 @@ struct Specials {
 };
 Specials specials_for(int n_vocab);
 int lang_id(const std::string& code);  // whisper.cpp g_lang order; -1 if unknown
+const char* lang_code(int id);         // nullptr if out of range
 
 struct DecodeRequest {
-    std::vector<int> prompt;    // shared by every sequence of the batch
+    std::vector<int> prompt;    // [sot, (lang, task,) notimestamps]: shared by every sequence
+    std::vector<int> prefix;    // whisper_full prompt_past ([prev] + prompt tokens), prefilled first
+    // per sequence (empty = prompt as given): >= 0 the language token for prompt[1]; -(s + 1)
+    // the token detected (whisper_lang_auto_detect) on sequence s of this batch
+    std::vector<int> lang_tok;
     int n_steps = 128;
     uint32_t flags = 3;         // SUPPRESS_BLANK | NO_TIMESTAMPS
     const int32_t* forced = nullptr;
@@ -53,11 +58,12 @@ public:
 
     // pcm_dev: B windows of <= 480000 samples at pcm_dev + b * stride (device memory)
     // tokens/top1/top2: host [B][n_steps]
+    // lang_out (optional, [B]): the language token each sequence was decoded with (-1: none)
     void transcribe_device(const float* pcm_dev, int64_t stride, const int* n_samples, int B, const DecodeRequest& rq,
-                           int* tokens, float* top1, float* top2);
+                           int* tokens, float* top1, float* top2, int* lang_out = nullptr);
     // host PCM convenience (stages into the engine's pcm buffer)
     void transcribe_host(const float* const* pcm, const int* n_samples, int B, const DecodeRequest& rq, int* tokens,
-                         float* top1, float* top2);
+                         float* top1, float* top2, int* lang_out = nullptr);
 
     void debug_mel(const float* pcm_host, int n, float* out_host);
     void debug_encode(const float* mel_host, float* out_host);
@@ -94,6 +100,8 @@ private:
         float* dx2 = nullptr;         // second residual buffer (ping-pong with dx)
         float* pend = nullptr;        // pending partial slabs [kMaxPend][R][d]
         std::map<GraphKey, hipGraphExec_t> graphs;
+        std::vector<int> host_tok;    // host sources of the call's token uploads
+        size_t host_used = 0;
     };
 
     void select() const;
@@ -105,8 +113,11 @@ private:
     void run_mel(const float* pcm_dev, int64_t stride, int B, float* dbg);
     void run_encoder(int B);
     void run_cross_kv(int B);
-    void run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1, float* top2);
+    void run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1, float* top2, int* lang_out);
     void enqueue_decoder_pass(DecGroup& g, int B_total, int Tq, const DecodeRequest& rq, int out_cap);
+    float* enqueue_layers(DecGroup& g, int B_total, int Tq);
+    void enqueue_head(DecGroup& g, int Tq, const DecodeRequest& rq, int out_cap, float* xc, const uint32_t* sup,
+                      bool blank);
 
     ModelDims dm_;
     int dt_, dev_, max_batch_;
@@ -150,6 +161,8 @@ private:
     void *xn_ = nullptr, *qkv_ = nullptr, *ao_ = nullptr, *ff_ = nullptr, *enc_out_ = nullptr;
     void* ckv_ = nullptr;   // cross K/V [L][2][B][H][1500][64]
     uint32_t* suppress_ = nullptr;
+    uint32_t* suppress_lang_ = nullptr;  // all but the language tokens (language detection)
+    bool suppress_lang_ready_ = false;
     double* scratch_ = nullptr;
     float* zero_ = nullptr;  // [R][d] zeros: the operand of an unused pending slab
     std::vector<DecGroup> groups_;

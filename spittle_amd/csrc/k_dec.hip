@@ -698,6 +698,8 @@ __global__ __launch_bounds__(256) void finalize_kernel(FinalizeArgs a) {
     }
 }
 
+__global__ void advance_kernel(DecState* ds, int n) { ds->pos0 += n; }
+
 __global__ void reset_kernel(DecState* ds, unsigned* arrive) {
     ds->pos0 = 0;
     ds->step = 0;
@@ -782,6 +784,10 @@ void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int B_layou
 void dec_finalize(int dtype, const FinalizeArgs& a, int B, hipStream_t st) {
     if (dtype == DT_BF16) hipLaunchKernelGGL(finalize_kernel<bf16>, dim3(B), dim3(256), 0, st, a);
     else hipLaunchKernelGGL(finalize_kernel<float>, dim3(B), dim3(256), 0, st, a);
+}
+
+void dec_advance(DecState* ds, int n, hipStream_t st) {
+    hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(1), 0, st, ds, n);
 }
 
 void dec_reset(DecState* ds, unsigned* arrive, hipStream_t st) {

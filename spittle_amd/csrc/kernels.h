@@ -118,5 +118,7 @@ struct FinalizeArgs {
 // argmax reduce + record + next-token embed + step advance (replaces embed/argmax/advance)
 void dec_finalize(int dtype, const FinalizeArgs& a, int B, hipStream_t st);
 void dec_reset(DecState* ds, unsigned* arrive, hipStream_t st);
+// pos0 += n (after a prefill pass that produces no token)
+void dec_advance(DecState* ds, int n, hipStream_t st);
 
 }  // namespace spt

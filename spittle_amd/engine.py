@@ -44,9 +44,12 @@ class WhisperModelParams:
 
 @dataclass
 class WhisperInferenceParams:
-    language: Optional[str] = None      # None = auto-detect (settings "auto")
+    language: Optional[str] = None      # None / "auto" = auto-detect (settings "auto")
     translate: bool = False
     initial_prompt: Optional[str] = None
+    # whisper_full_params.prompt_tokens: token ids decoded before [sot ...] (what initial_prompt
+    # becomes after tokenization)
+    prompt_tokens: Optional[Sequence[int]] = None
     # whisper_full_params the app leaves at their defaults
     suppress_blank: bool = True
     no_timestamps: bool = True
@@ -73,6 +76,7 @@ class TranscriptionResult:
     top1: Optional[np.ndarray] = None
     top2: Optional[np.ndarray] = None
     n_windows: int = 0
+    language: Optional[str] = None      # ISO-639-1 code decoded with (detected or given)
 
 
 def _infer_params(p: Optional[WhisperInferenceParams], keep: list) -> L.InferParams:
@@ -91,6 +95,11 @@ def _infer_params(p: Optional[WhisperInferenceParams], keep: list) -> L.InferPar
         keep.append(f)
         ip.forced_tokens = f.ctypes.data_as(C.POINTER(C.c_int32))
         ip.n_forced = int(f.shape[-1])
+    if p.prompt_tokens is not None and len(p.prompt_tokens) > 0:
+        t = np.ascontiguousarray(np.asarray(p.prompt_tokens, dtype=np.int32).reshape(-1))
+        keep.append(t)
+        ip.prompt_tokens = t.ctypes.data_as(C.POINTER(C.c_int32))
+        ip.n_prompt_tokens = int(t.size)
     return ip
 
 
@@ -100,9 +109,11 @@ def _take_result(rp) -> TranscriptionResult:
     toks = [r.tokens[i] for i in range(n)]
     t1 = np.ctypeslib.as_array(r.top1, shape=(n,)).copy() if n else np.zeros(0, np.float32)
     t2 = np.ctypeslib.as_array(r.top2, shape=(n,)).copy() if n else np.zeros(0, np.float32)
+    lib = L.load()
+    code = lib.spt_language_code(r.language) if r.language >= 0 else None
     res = TranscriptionResult(text=(r.text or b"").decode("utf-8", "replace"), segments=[], tokens=toks, top1=t1,
-                              top2=t2, n_windows=r.n_windows)
-    L.load().spt_result_free(rp)
+                              top2=t2, n_windows=r.n_windows, language=code.decode() if code else None)
+    lib.spt_result_free(rp)
     return res
 
 

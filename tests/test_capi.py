@@ -42,10 +42,17 @@ def test_version_and_defaults():
 def test_struct_layouts_match_header():
     # sizes of the ABI structs as the C compiler lays them out (x86-64 SysV)
     assert C.sizeof(L.ModelParams) == 24
-    assert C.sizeof(L.InferParams) == 56
-    assert C.sizeof(L.Result) == 40
+    assert C.sizeof(L.InferParams) == 72
+    assert C.sizeof(L.Result) == 48
     assert C.sizeof(L.ModelInfo) == 56
     assert C.sizeof(L.Timings) == 56
+
+
+def test_language_codes():
+    lib = L.load()
+    assert lib.spt_language_code(0) == b"en" and lib.spt_language_code(1) == b"zh"
+    assert lib.spt_language_code(99) == b"yue"
+    assert lib.spt_language_code(100) is None and lib.spt_language_code(-1) is None
 
 
 def test_create_errors_are_reported_not_raised():
