@@ -6,6 +6,6 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 for C in FETCH_SIZE WRITE_SIZE; do
   SPT_NO_GRAPH=1 timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d gpurun_out/pmc_${TAG}_$C -o run -- \
-     python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/pmc_${TAG}_$C.log 2>&1 || { echo "pmc $C failed"; exit 1; }
+     python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --decode-steps 8 > gpurun_out/pmc_${TAG}_$C.log 2>&1 || { echo "pmc $C failed"; exit 1; }
 done
-python3 scripts/pmc_parse.py $TAG
+# parse locally after the merge: python3 scripts/pmc_parse.py $TAG

@@ -10,9 +10,9 @@ from collections import defaultdict
 
 tag = sys.argv[1] if len(sys.argv) > 1 else "r1"
 SEL = {
-    "dec_cross_attn": lambda n: "dec_attn_kernel" in n and "false" in n,
-    "dec_logits": lambda n: "gemv_kernel" in n and ", 4, true" in n,
-    "enc_fc1_gemm": lambda n: "gemm_nt_kernel<unsigned short, 1>" in n,
+    "dec_cross_attn": lambda n: "cross_attn_kernel<unsigned short, 1>" in n,
+    "dec_logits": lambda n: "gemv_kernel<unsigned short, 4," in n,
+    "enc_fc1_gemm": lambda n: "gemm256_kernel<1>" in n,
 }
 vals = {k: defaultdict(list) for k in SEL}
 for counter in ("FETCH_SIZE", "WRITE_SIZE"):
