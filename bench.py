@@ -81,17 +81,18 @@ def cpu_baseline(model_spec: str, sample_steps: int, decode_steps: int) -> dict:
 
 DOMINANT = "dec_cross_attn"  # largest share of device time (profiles/*_kernel_stats.csv)
 KERNEL_NAMES = {
-    "dec_cross_attn": "dec_attn_kernel<bf16,1,false> (decoder cross-attention, 1 layer)",
-    "dec_logits": "gemv_kernel<bf16,GV_LOGITS,...> (final LN + logits + top-2)",
-    "dec_fc1": "gemv_kernel<bf16,GV_BIAS_GELU,...> (decoder LN + fc1 + GELU)",
-    "enc_fc1_gemm": "gemm_nt_kernel<bf16,EPI_BIAS_GELU> (encoder fc1)",
+    "dec_cross_attn": "cross_attn_kernel<bf16,1> (decoder cross-attention, 1 layer)",
+    "dec_logits": "gemv_kernel<bf16,GV_LOGITS,A_LN> (final LN + logits + top-2)",
+    "dec_fc1": "gemv_kernel<bf16,GV_BIAS_GELU,A_LN> (decoder LN + fc1 + GELU)",
+    "enc_fc1_gemm": "gemm256_kernel<EPI_BIAS_GELU> (encoder fc1, 256x256 tile)",
     "enc_attn": "attn_bf16_kernel (encoder flash attention, 1 layer)",
 }
 
 
 def roofline(eng, iters: int = 50):
-    """Dominant-kernel roofline from HIP events on the engine stream (spt_probe_kernel:
-    the kernel re-launched back to back on the buffers of the last timed call).
+    """Dominant-kernel roofline from HIP events on the engine stream (spt_probe_kernel: the
+    kernel re-launched on the buffers of the last timed call; decoder kernels one launch at a
+    time behind a 512 MB cache-evicting read, as in the decode loop).
     achieved = algorithmic bytes (or flops) per launch / average launch duration.
     traffic = PMC-measured HBM bytes per launch of the same kernel, from the committed
     rocprofv3 --pmc summary (profiles/pmc_<kernel>.json), when present."""

@@ -130,10 +130,13 @@ const char* spt_language_code(int32_t lang_id);
 
 spt_status spt_get_timings(const spt_ctx* ctx, spt_timings* t);
 
-/* Kernel probe (measurement): re-launch one hot-path kernel `iters` times back to
- * back on the engine stream, on the buffers of the last call, between two HIP
- * events.  avg_us = mean launch-to-launch time; work = algorithmic bytes (HBM-bound
- * kernels) or flops (MFMA-bound kernels) per launch, work_is_flops says which. */
+/* Kernel probe (measurement): re-launch one hot-path kernel `iters` times on the engine
+ * stream, on the buffers of the last call.  Decoder kernels (kinds 0-3) are timed between two
+ * HIP events after a 512 MB read of other weights (the cold Infinity Cache they meet in the
+ * decode loop); kinds 0 and 3 as 8 launches over 8 different layers back to back, like the
+ * loop; encoder kernels back to back.  avg_us = mean
+ * time per launch; work = algorithmic bytes (HBM-bound kernels) or flops (MFMA-bound kernels)
+ * per launch, work_is_flops says which. */
 typedef enum {
     SPT_PROBE_DEC_CROSS_ATTN = 0,  /* decoder cross-attention, one layer */
     SPT_PROBE_DEC_SELF_ATTN = 1,   /* decoder self-attention, one layer */

@@ -126,6 +126,7 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     cp_ = ((dm_.n_mels + 63) / 64) * 64;
     if ((3 * cp_ * esz_) % 128) cp_ = ((dm_.n_mels + 127) / 128) * 128;
     if (const char* g = getenv("SPT_DECODE_GROUPS")) n_groups_ = std::max(1, std::min(2, atoi(g)));
+    if (const char* v = getenv("SPT_XATTN_SPLIT")) xsplit_ = std::max(1, std::min(4, atoi(v)));
     // cross-attention key split / waves per workgroup: fixed per engine (never per batch)
     // projection K splits (self-out: 2, fc2: 4; fixed per engine, never per batch). The pending-
     // slab count a LayerNorm prologue sums is a kernel template constant: 2 after the self-out
@@ -391,6 +392,7 @@ void Engine::alloc_workspace() {
             g.ds = (DecState*)c.take(sizeof(DecState));
             g.dx2 = (float*)c.take(R * d * 4);
             g.pend = (float*)c.take((int64_t)kMaxPend * R * d * 4);
+            g.xpart = (float*)c.take((int64_t)R * dm_.n_head * 4 * 66 * 4);
         }
         zero_ = (float*)c.take(R * d * 4);  // never written: the "no pending slab" operand
         if (!pass) {
@@ -526,11 +528,12 @@ float* Engine::enqueue_layers(DecGroup& g, int B_total, int Tq) {
         a.W = e.cq_w; a.N = d; a.K = d; a.bias = e.cq_b; a.C = g.dq; a.ldc = d;
         gemv(dt_, GV_BIAS, A_LN, a, st);
         consumed();
-        dec_cross_attn(dt_, g.dq, ckv_l, B, B_total, H, T, Tq, g.dao, st);
-        // cross output projection, residual add in place
+        dec_cross_attn(dt_, g.dq, ckv_l, B, B_total, H, T, Tq, g.dao, st, xsplit_, g.xpart);
+        // cross output projection (merging the key chunks in its prologue), residual add in place
         a = GemvArgs{};
         a.A = g.dao; a.lda = d; a.R = R; a.W = e.co_w; a.N = d; a.K = d; a.bias = e.co_b; a.C = xc; a.ldc = d;
-        gemv(dt_, GV_BIAS_RESID, A_DIRECT, a, st);
+        if (xsplit_ > 1) { a.apart = g.xpart; a.a_splits = xsplit_; a.a_heads = H; }
+        gemv(dt_, GV_BIAS_RESID, xsplit_ > 1 ? A_ATTN : A_DIRECT, a, st);
         // LN3 + fc1 + GELU
         a = GemvArgs{};
         ln_input(a); a.lda = d; a.ln_w = e.ln3_w; a.ln_b = e.ln3_b; a.R = R;
@@ -867,11 +870,18 @@ double Engine::probe(int kind, int iters, double* work, int* is_flops) {
     const int d = dm_.d, H = dm_.n_head, T = dm_.n_audio_ctx, ctx = dm_.n_text_ctx, V = dm_.n_vocab;
     DecGroup& g = groups_[0];
     const int Bg = g.B > 0 ? g.B : B;
+    // kinds 0 and 3 launch the kernel of nl different decoder layers back to back (as in the
+    // decode loop: each on its own, cache-cold weights / K/V); the time is per launch
+    const int nl = (kind == 0 || kind == 3) ? std::min(8, dm_.n_dec) : 1;
     std::function<void()> launch;
     *is_flops = 0;
     switch (kind) {
-        case 0:  // cross-attention of decoder layer 0 over this group's cross K/V
-            launch = [&] { dec_cross_attn(dt_, g.dq, ckv_, Bg, B, H, T, 1, g.dao, st_); };
+        case 0:  // cross-attention of layers 0..nl-1 (one launch each) over this group's cross K/V
+            launch = [&] {
+                for (int l = 0; l < nl; ++l)
+                    dec_cross_attn(dt_, g.dq, (const char*)ckv_ + (int64_t)2 * B * H * T * 64 * l * esz_, Bg, B, H,
+                                   T, 1, g.dao, st_, xsplit_, g.xpart);
+            };
             *work = 2.0 * Bg * H * T * 64 * esz_;
             break;
         case 1:
@@ -897,10 +907,12 @@ double Engine::probe(int kind, int iters, double* work, int* is_flops) {
         case 3: {
             launch = [&] {
                 GemvArgs a{};
-                a.A = g.dx; a.lda = d; a.ln_w = dec_[0].ln3_w; a.ln_b = dec_[0].ln3_b; a.R = Bg;
-                for (int p = 0; p < kMaxPend; ++p) a.pend[p] = zero_;
-                a.W = dec_[0].fc1_w; a.N = 4 * d; a.K = d; a.bias = dec_[0].fc1_b; a.C = g.dff; a.ldc = 4 * d;
-                gemv(dt_, GV_BIAS_GELU, A_LN, a, st_);
+                for (int l = 0; l < nl; ++l) {
+                    a.A = g.dx; a.lda = d; a.ln_w = dec_[l].ln3_w; a.ln_b = dec_[l].ln3_b; a.R = Bg;
+                    for (int p = 0; p < kMaxPend; ++p) a.pend[p] = zero_;
+                    a.W = dec_[l].fc1_w; a.N = 4 * d; a.K = d; a.bias = dec_[l].fc1_b; a.C = g.dff; a.ldc = 4 * d;
+                    gemv(dt_, GV_BIAS_GELU, A_LN, a, st_);
+                }
             };
             *work = 4.0 * d * d * esz_;
             break;
@@ -928,6 +940,25 @@ double Engine::probe(int kind, int iters, double* work, int* is_flops) {
         if (kind >= 4 && dm_.n_enc < 1) throw std::runtime_error("model has no encoder layers");
     }
     launch();  // warm
+    if (kind <= 3) {
+        // decoder kernels: inside the decode loop their operands come from HBM (a pass streams
+        // ~4 GB through the 256 MB Infinity Cache), so each timed group of launches follows a
+        // read of 512 MB of other weights, and only the launches are between the two events
+        const int64_t fb = std::min<int64_t>(wbytes_, (int64_t)512 << 20) & ~(int64_t)15;
+        double tot = 0.0;
+        iters = std::max(1, iters / nl);
+        for (int i = 0; i < iters; ++i) {
+            cache_flush(warena_, fb, (unsigned*)scratch_, st_);
+            HIP_CHECK(hipEventRecord(ev_[0], st_));
+            launch();
+            HIP_CHECK(hipEventRecord(ev_[1], st_));
+            HIP_CHECK(hipEventSynchronize(ev_[1]));
+            float ms;
+            HIP_CHECK(hipEventElapsedTime(&ms, ev_[0], ev_[1]));
+            tot += ms;
+        }
+        return tot * 1000.0 / (iters * nl);
+    }
     HIP_CHECK(hipEventRecord(ev_[0], st_));
     for (int i = 0; i < iters; ++i) launch();
     HIP_CHECK(hipEventRecord(ev_[1], st_));

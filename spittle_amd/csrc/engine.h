@@ -99,6 +99,7 @@ private:
         DecState* ds = nullptr;
         float* dx2 = nullptr;         // second residual buffer (ping-pong with dx)
         float* pend = nullptr;        // pending partial slabs [kMaxPend][R][d]
+        float* xpart = nullptr;       // cross-attention chunk partials [R][H][<=4][66]
         std::map<GraphKey, hipGraphExec_t> graphs;
         std::vector<int> host_tok;    // host sources of the call's token uploads
         size_t host_used = 0;
@@ -125,6 +126,7 @@ private:
     int esz_;     // bytes per weight / activation element
     int cp_;      // padded mel channels (conv1 K = 3 * cp_)
     static constexpr int so_split_ = 2, fc2_split_ = 4;  // K splits of the self-out / fc2 projections
+    int xsplit_ = 1;  // cross-attention key chunks per (b, h) (merged by the output projection)
     int n_groups_ = 1;  // SPT_DECODE_GROUPS=2 splits the batch over two streams
     hipStream_t st_ = nullptr;
     std::vector<hipEvent_t> ev_;

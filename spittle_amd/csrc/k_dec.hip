@@ -93,11 +93,17 @@ __device__ __forceinline__ F load_w(const F* p) {
 //   A_DIRECT  activation rows [R][lda] of type T read straight into MFMA fragments;
 //   A_LN      LayerNorm of the f32 residual rows x + pend[0..np-1] (the pending partial slabs
 //             of the previous GV_PARTIAL launch), staged as a bank-padded LDS image;
-//             workgroup (0, 0) also writes the combined rows to x_out.
-// kernel-side A source codes: A_DIRECT, or LN_SRC(np) = A_LN with np pending slabs (0, 2, 4)
+//             workgroup (0, 0) also writes the combined rows to x_out;
+//   A_ATTN    the cross-attention output merged from its S key-chunk partials
+//             [R][H][S][66] = {o[64], m, l} (rows of this workgroup's K range), staged in LDS.
+// kernel-side A source codes: A_DIRECT, LN_SRC(np) = A_LN with np pending slabs (0, 2, 4), or
+// ATTN_SRC(s) = A_ATTN combining s cross-attention key chunks
 constexpr int LN_SRC(int np) { return 16 + np; }
-constexpr bool is_ln(int asrc) { return asrc >= 16; }
+constexpr bool is_ln(int asrc) { return asrc >= 16 && asrc < 32; }
 constexpr int ln_np(int asrc) { return asrc - 16; }
+constexpr int ATTN_SRC(int s) { return 32 + s; }
+constexpr bool is_attn(int asrc) { return asrc >= 32; }
+constexpr int attn_s(int asrc) { return asrc - 32; }
 
 template <typename T, int MODE, int ASRC, int RG, int NWV, int CT, int MAXJ>
 __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
@@ -207,6 +213,40 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
                     o[3] = from_f<T>((v[i].w - mean) * rstd * g.w + b.w);
                 }
             }
+        }
+        __syncthreads();
+    }
+
+    if constexpr (is_attn(ASRC)) {
+        // flash-decoding merge of the S chunks: heads covering this workgroup's K range;
+        // thread <-> (row r, head h, element e)
+        constexpr int S = attn_s(ASRC);
+        T* img = (T*)smem;
+        const int H = a.a_heads;
+        const int h0 = (ss0 * KS) >> 6, h1 = min(H, (ss1 * KS + 63) >> 6);
+        const int nh = h1 - h0;
+        for (int idx = tid; idx < a.R * nh * 64; idx += 64 * NWV) {
+            const int r = idx / (nh * 64), rem = idx - r * nh * 64;
+            const int h = h0 + (rem >> 6), e = rem & 63;
+            const float* pp = a.apart + ((size_t)r * H + h) * S * 66;
+            float mc[S], lc[S], oc[S];
+#pragma unroll
+            for (int c = 0; c < S; ++c) {
+                mc[c] = pp[c * 66 + 64];
+                lc[c] = pp[c * 66 + 65];
+                oc[c] = pp[c * 66 + e];
+            }
+            float M = mc[0];
+#pragma unroll
+            for (int c = 1; c < S; ++c) M = fmaxf(M, mc[c]);
+            float L = 0.f, O = 0.f;
+#pragma unroll
+            for (int c = 0; c < S; ++c) {
+                const float f = mc[c] == -INFINITY ? 0.f : exp2f(mc[c] - M);
+                L += lc[c] * f;
+                O += oc[c] * f;
+            }
+            img[(size_t)r * lds_ld + h * 64 + e] = from_f<T>(O / L);
         }
         __syncthreads();
     }
@@ -365,7 +405,10 @@ void gemv_launch_cfg(const GemvArgs& a, hipStream_t st) {
     X(GV_LOGITS, LN_SRC(0))             \
     X(GV_LOGITS, LN_SRC(4))             \
     X(GV_PARTIAL, A_DIRECT)             \
-    X(GV_BIAS_RESID, A_DIRECT)
+    X(GV_BIAS_RESID, A_DIRECT)          \
+    X(GV_BIAS_RESID, ATTN_SRC(2))       \
+    X(GV_BIAS_RESID, ATTN_SRC(3))       \
+    X(GV_BIAS_RESID, ATTN_SRC(4))
 
 // > 64 KiB of dynamic LDS must be enabled per kernel, outside any stream capture
 template <typename T, int MODE, int ASRC>
@@ -606,10 +649,10 @@ __global__ __launch_bounds__(64 * AW) void self_attn_kernel(const T* __restrict_
 // kv: [2][B_layout][H][T_enc][64] at the group's first sequence.  (A fused LayerNorm + cross-Q
 // projection prologue and key-chunk splits were measured slower on MI355X: r1
 // exp_fused_xattn_pending_slabs.txt.)
-template <typename T, int NQ>
+template <typename T, int NQ, bool SPLIT>
 __global__ __launch_bounds__(64 * AW) void cross_attn_kernel(const T* __restrict__ q, const T* __restrict__ kv,
                                                              int B_layout, int H, int T_enc, int Tq,
-                                                             T* __restrict__ out) {
+                                                             T* __restrict__ out, float* __restrict__ part) {
     __shared__ float s_m[AW][NQ], s_l[AW][NQ];
     __shared__ float s_o[AW][NQ][64];
     const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
@@ -627,14 +670,27 @@ __global__ __launch_bounds__(64 * AW) void cross_attn_kernel(const T* __restrict
         for (int e = 0; e < 8; ++e) qv[t][e] = to_f<T>(qr[e]) * kLog2Scale;
         lim[t] = T_enc;
     }
-    aw.run(wid, cdiv(T_enc, AttnWave<T, NQ>::KB), false, qv, lim, Tq);
+    // SPLIT: this workgroup's chunk of the key blocks (gridDim.y chunks, block-aligned)
+    const int nblk_all = cdiv(T_enc, AttnWave<T, NQ>::KB);
+    const int S = SPLIT ? (int)gridDim.y : 1, sp = SPLIT ? (int)blockIdx.y : 0;
+    const int per = cdiv(nblk_all, S), blk0 = sp * per, nblk = min(nblk_all, blk0 + per);
+    aw.run(blk0 + wid, nblk, false, qv, lim, Tq);
     aw.to_lds(s_m, s_l, s_o, wid, lane);
     __syncthreads();
     if (tid < 64 * Tq) {
         const int t = tid >> 6, e = tid & 63;
         float M, L, O;
         attn_merge<NQ>(s_m, s_l, s_o, t, e, M, L, O);
-        out[(size_t)(b * Tq + t) * (H * 64) + h * 64 + e] = from_f<T>(O / L);
+        if constexpr (SPLIT) {  // partial {o[64], m, l} for the output projection's merge prologue
+            float* pp = part + ((((size_t)(b * Tq + t)) * H + h) * S + sp) * 66;
+            pp[e] = O;
+            if (e == 0) {
+                pp[64] = M;
+                pp[65] = L;
+            }
+        } else {
+            out[(size_t)(b * Tq + t) * (H * 64) + h * 64 + e] = from_f<T>(O / L);
+        }
     }
 }
 
@@ -731,7 +787,9 @@ void gemv(int dtype, int mode, int asrc, const GemvArgs& a_in, hipStream_t st) {
     if (asrc == A_LN)
         for (int p = 0; p < 4; ++p)
             if (!a.pend[p]) throw std::runtime_error("gemv: LayerNorm prologue needs 4 pending slabs (zero slab if none)");
-    const int code = asrc == A_LN ? LN_SRC(a.n_pend) : asrc;
+    if (asrc == A_ATTN && (!a.apart || a.a_splits < 2 || a.a_splits > 4 || a.a_heads * 64 != a.K))
+        throw std::runtime_error("gemv: attention-merge prologue needs 2..4 chunks over all heads");
+    const int code = asrc == A_LN ? LN_SRC(a.n_pend) : asrc == A_ATTN ? ATTN_SRC(a.a_splits) : asrc;
 #define SPT_GV(M, S)                                                      \
     if (mode == M && code == S) {                                         \
         if (dtype == DT_BF16) gemv_launch<bf16, M, S>(a, st);             \
@@ -767,15 +825,19 @@ void dec_self_attn(int dtype, const void* q, const void* cache, int B, int H, in
 }
 
 void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int B_layout, int H, int T_enc, int Tq, void* out,
-                    hipStream_t st) {
+                    hipStream_t st, int splits, float* part) {
     if (Tq < 1 || Tq > 4) throw std::runtime_error("dec_cross_attn: 1..4 queries per sequence");
-    const dim3 grid(B * H), blk(64 * AW);
-#define SPT_XA(T, NQ) \
-    hipLaunchKernelGGL((cross_attn_kernel<T, NQ>), grid, blk, 0, st, (const T*)q, (const T*)kv, B_layout, H, T_enc, Tq, (T*)out)
+    if (splits < 1 || splits > 4 || (splits > 1 && !part)) throw std::runtime_error("dec_cross_attn: 1..4 key chunks");
+    const dim3 grid(B * H, splits), blk(64 * AW);
+#define SPT_XA(T, NQ, SP)                                                                                   \
+    hipLaunchKernelGGL((cross_attn_kernel<T, NQ, SP>), grid, blk, 0, st, (const T*)q, (const T*)kv, B_layout, H, \
+                       T_enc, Tq, (T*)out, part)
     if (dtype == DT_BF16) {
-        if (Tq == 1) SPT_XA(bf16, 1); else SPT_XA(bf16, 4);
+        if (Tq == 1) { if (splits > 1) SPT_XA(bf16, 1, true); else SPT_XA(bf16, 1, false); }
+        else { if (splits > 1) SPT_XA(bf16, 4, true); else SPT_XA(bf16, 4, false); }
     } else {
-        if (Tq == 1) SPT_XA(float, 1); else SPT_XA(float, 4);
+        if (Tq == 1) { if (splits > 1) SPT_XA(float, 1, true); else SPT_XA(float, 1, false); }
+        else { if (splits > 1) SPT_XA(float, 4, true); else SPT_XA(float, 4, false); }
     }
 #undef SPT_XA
     SPT_LAUNCH_CHECK();

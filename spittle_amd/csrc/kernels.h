@@ -32,6 +32,8 @@ void gen_weights(int store_dtype, void* dst, int64_t n, uint64_t seed, uint32_t 
 void gen_conv_weights(int store_dtype, void* dst, int N, int C, int Cp, uint64_t seed, uint32_t tid,
                       int scale_exp, hipStream_t st);
 void fill_f32(float* dst, int64_t n, float v, hipStream_t st);
+// read `bytes` of p once (measurement: cold caches before a probed launch)
+void cache_flush(const void* p, int64_t bytes, unsigned* sink, hipStream_t st);
 // weight checksum helper for tests: sum of |w| and sum of w (f64) of a device tensor
 void tensor_checksum(int dtype, const void* src, int64_t n, double* out2_dev, hipStream_t st);
 
@@ -69,13 +71,14 @@ struct DecState {        // device-resident step state
 };
 
 enum { GV_BIAS = 0, GV_BIAS_GELU = 1, GV_PARTIAL = 2, GV_QKV_CACHE = 3, GV_LOGITS = 4, GV_BIAS_RESID = 5 };
-enum { A_DIRECT = 0, A_LN = 1 };
+enum { A_DIRECT = 0, A_LN = 1, A_ATTN = 2 };
 struct GemvArgs {
     // A rows: row i at A + (i * lda + a_row0); A_DIRECT: dtype activations; A_LN: f32 residual rows
     const void* A; int lda; int a_row0;
     const float* ln_w; const float* ln_b; // A_LN: LayerNorm of x + pend[0] + .. + pend[3]
     const float* pend[4]; int n_pend;     // A_LN: pending partial slabs (same layout as A): n_pend = 0, 2 or 4
     float* x_out;                         // A_LN: combined rows written here by workgroup (0, 0) (or nullptr)
+    const float* apart; int a_splits, a_heads;  // A_ATTN: cross-attention chunk partials [R][H][S][66]
     int R;                                // rows (<= 64)
     const void* W; int N, K;              // W [N][K]
     const float* bias;
@@ -100,9 +103,11 @@ void dec_embed(int dtype, const int* tok, int R, int Tq, int d, const void* tok_
 void dec_self_attn(int dtype, const void* q, const void* cache, int B, int H, int ctx, int Tq,
                    const DecState* ds, void* out, hipStream_t st);
 // cross attention over all T_enc cached encoder keys: q [R][d] -> out [R][d]
-// kv: [2][B_layout][H][T_enc][64] (already offset to the first of the B sequences)
+// kv: [2][B_layout][H][T_enc][64] (already offset to the first of the B sequences).
+// splits > 1: the keys of each (b, h) in `splits` chunks (one workgroup each) that write
+// partials [R][H][splits][66] = {o[64], m, l} to `part` instead (merged by an A_ATTN GEMV)
 void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int B_layout, int H, int T_enc, int Tq,
-                    void* out, hipStream_t st);
+                    void* out, hipStream_t st, int splits = 1, float* part = nullptr);
 
 struct FinalizeArgs {
     const void* part; int n_tiles;        // logits top-2 partials [B][n_tiles]

@@ -2,9 +2,9 @@
 // Times the library's launchers with HIP events, back-to-back launches on one stream.
 //   ubench gemv  N K R mode ln dtype [ksplit npend]  mode: 0 bias 1 gelu 2 partial 3 qkv 4 logits 5 resid
 //   ubench attn  B H ctx nkeys Tq dtype   self-attention
-//   ubench xattn B T Tq dtype            cross-attention
+//   ubench xattn B T splits dtype        cross-attention, 8 layers back to back
 //   ubench gemm  M N K epi dtype         128 vs 256 tile (time, bitwise diff)
-//   ubench layer B dtype                 one large-v3 decoder layer (8 launches)
+//   ubench layer B dtype [xsplit]        one large-v3 decoder layer (8 launches)
 //   ubench layer2 B dtype [...]          two such chains on two streams
 //   ubench null
 #include <hip/hip_runtime.h>
@@ -115,14 +115,20 @@ int main(int argc, char** argv) {
                2.0 * B * H * nk * 64 * esz / us / 1e3);
         return 0;
     }
-    if (what == "xattn") {  // cross-attention over T encoder keys
-        const int B = ai(2, 8), T = ai(3, 1500), Tq = ai(4, 1), dt = ai(5, DT_BF16), d = 1280, H = 20;
+    if (what == "xattn") {  // cross-attention over T encoder keys of NL layers back to back (cache-cold)
+        const int B = ai(2, 8), T = ai(3, 1500), S = ai(4, 1), dt = ai(5, DT_BF16), NL = 8, d = 1280, H = 20;
         const int esz = dt == DT_BF16 ? 2 : 4;
-        void* q = drand((size_t)B * Tq * d, dt, 1, 0);
-        void* kv = drand((size_t)2 * B * H * T * 64, dt, 2, 0);
-        void* out = dalloc((size_t)B * Tq * d * esz);
-        const double us = time_us(st, iters, [&] { dec_cross_attn(dt, q, kv, B, B, H, T, Tq, out, st); });
-        printf("cross-attn B=%d T=%d Tq=%d dt=%d : %.2f us  %.0f GB/s\n", B, T, Tq, dt, us,
+        void* q = drand((size_t)B * d, dt, 1, 0);
+        const size_t layer = (size_t)2 * B * H * T * 64;
+        void* kv = drand(layer * NL, dt, 2, 0);
+        void* out = dalloc((size_t)B * d * esz);
+        float* part = (float*)dalloc((size_t)B * H * 4 * 66 * 4);
+        HIP_CHECK(hipDeviceSynchronize());
+        const double us = time_us(st, 10, [&] {
+            for (int l = 0; l < NL; ++l)
+                dec_cross_attn(dt, q, (const char*)kv + layer * l * esz, B, B, H, T, 1, out, st, S, part);
+        }) / NL;
+        printf("cross-attn B=%d T=%d splits=%d dt=%d (8 layers back to back) : %.2f us  %.0f GB/s\n", B, T, S, dt, us,
                2.0 * B * H * T * 64 * esz / us / 1e3);
         return 0;
     }
@@ -167,7 +173,7 @@ int main(int argc, char** argv) {
     if (what == "layer" || what == "layer2") {
         // layer: one large-v3 decoder layer chain at batch B
         // layer2: two independent chains of batch B on two streams (can they overlap?)
-        const int B = ai(2, 8), dt = ai(3, DT_BF16), d = 1280, H = 20, ctx = 448, T = 1500;
+        const int B = ai(2, 8), dt = ai(3, DT_BF16), xs = ai(4, 1), d = 1280, H = 20, ctx = 448, T = 1500;
         gemv_prepare(dt);
         const int esz = dt == DT_BF16 ? 2 : 4;
         void* wqkv = drand((size_t)3 * d * d, dt, 1, -4);
@@ -180,12 +186,13 @@ int main(int argc, char** argv) {
         float* lnw = frand(d, 8, -3);
         float* lnb = frand(d, 9, -4);
         float* zero = (float*)dalloc((size_t)B * d * 4);
-        struct Chain { float *x, *x2, *pend; void *q, *ao, *ff, *skv, *ckv; DecState* ds; };
+        struct Chain { float *x, *x2, *pend, *xpart; void *q, *ao, *ff, *skv, *ckv; DecState* ds; };
         auto mk = [&](uint32_t s) {
             Chain c;
             c.x = frand((size_t)B * d, 10 + s, 0);
             c.x2 = (float*)dalloc((size_t)B * d * 4);
             c.pend = (float*)dalloc((size_t)kMaxPend * B * d * 4);
+            c.xpart = (float*)dalloc((size_t)B * H * 4 * 66 * 4);
             c.q = dalloc((size_t)B * d * esz);
             c.ao = dalloc((size_t)B * d * esz);
             c.ff = dalloc((size_t)B * 4 * d * esz);
@@ -224,10 +231,11 @@ int main(int argc, char** argv) {
             a.W = wq; a.N = d; a.K = d; a.bias = b4; a.C = c.q; a.ldc = d;
             gemv(dt, GV_BIAS, A_LN, a, s);
             consumed();
-            dec_cross_attn(dt, c.q, c.ckv, B, B, H, T, 1, c.ao, s);
+            dec_cross_attn(dt, c.q, c.ckv, B, B, H, T, 1, c.ao, s, xs, c.xpart);
             a = GemvArgs{};
             a.A = c.ao; a.lda = d; a.R = B; a.W = wco; a.N = d; a.K = d; a.bias = b4; a.C = xc; a.ldc = d;
-            gemv(dt, GV_BIAS_RESID, A_DIRECT, a, s);
+            if (xs > 1) { a.apart = c.xpart; a.a_splits = xs; a.a_heads = H; }
+            gemv(dt, GV_BIAS_RESID, xs > 1 ? A_ATTN : A_DIRECT, a, s);
             a = GemvArgs{};
             ln_input(a); a.lda = d; a.ln_w = lnw; a.ln_b = lnb; a.R = B;
             a.W = w1; a.N = 4 * d; a.K = d; a.bias = b4; a.C = c.ff; a.ldc = 4 * d;
