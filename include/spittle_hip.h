@@ -64,7 +64,7 @@ typedef struct {
     const char* language;        /* ISO-639-1 ("en", "zh", ...); NULL or "auto" = auto-detect
                                     (whisper_lang_auto_detect on the utterance's first 30 s) */
     int32_t translate;           /* task <|translate|> instead of <|transcribe|> */
-    const char* initial_prompt;  /* jargon prompt text (src-tauri/src/jargon.rs:594); needs a vocab */
+    const char* initial_prompt;  /* jargon prompt text (src-tauri/src/jargon.rs:594); ggml models */
     uint32_t flags;              /* SPT_SUPPRESS_BLANK | SPT_NO_TIMESTAMPS | SPT_IGNORE_EOT */
     int32_t max_new_tokens;      /* generated tokens per 30 s window (<= 220 like whisper.cpp) */
     float temperature;           /* only 0 (greedy) is implemented */
@@ -77,7 +77,7 @@ typedef struct {
 } spt_infer_params;
 
 typedef struct {
-    char* text;             /* UTF-8; for synthetic models the token ids as "[id]" */
+    char* text;             /* the text tokens' strings; for synthetic models the ids as "[id]" */
     int32_t* tokens;        /* generated token ids (EOT included, stops after it) */
     float* top1;            /* suppressed logit of the chosen token, per step */
     float* top2;            /* runner-up suppressed logit, per step */
@@ -108,7 +108,10 @@ void spt_default_model_params(spt_model_params* p);
 void spt_default_infer_params(spt_infer_params* p);
 
 /* model_spec: "synthetic:<tiny.en|tiny|base|small|medium|large-v3>[:enc=N][:dec=N][:seed=S]"
- * or a filesystem path (ggml .bin loading is not implemented yet -> SPT_ERR_UNSUPPORTED). */
+ * or the path of a whisper.cpp ggml model file (the catalog's ggml-*.bin; tensor types f32,
+ * f16, q4_0, q4_1, q5_0, q5_1, q8_0; dequantised once at load into the engine dtype).
+ * Replaces WhisperEngine::load_model(&path) (transcribe-rs; src-tauri/src/managers/
+ * transcription.rs:261-276); bad files fail with SPT_ERR_LOAD and a message. */
 spt_status spt_ctx_create(const char* model_spec, const spt_model_params* params, spt_ctx** out,
                           char* err, size_t errlen);
 void spt_ctx_destroy(spt_ctx* ctx);
@@ -127,6 +130,13 @@ spt_status spt_transcribe_batch_device(spt_ctx* ctx, const float* pcm_dev, size_
 void spt_result_free(spt_result* r);
 /* ISO-639-1 code of a language index ("en" = 0, "zh" = 1, ...), NULL if out of range */
 const char* spt_language_code(int32_t lang_id);
+
+/* whisper_tokenize of the model's vocabulary (ggml models only; SPT_ERR_UNSUPPORTED for
+ * synthetic ones).  *n_out = the token count even when it exceeds n_max (then
+ * SPT_ERR_INVALID_ARG and nothing is written past n_max). */
+spt_status spt_tokenize(spt_ctx* ctx, const char* text, int32_t* tokens, int32_t n_max, int32_t* n_out);
+/* whisper_token_to_str: the bytes of token id (owned by the context), NULL without a vocab */
+const char* spt_token_to_str(const spt_ctx* ctx, int32_t id);
 
 spt_status spt_get_timings(const spt_ctx* ctx, spt_timings* t);
 
@@ -155,6 +165,11 @@ spt_status spt_debug_mel(spt_ctx* ctx, const float* pcm16k, size_t n_samples, fl
 spt_status spt_debug_encode(spt_ctx* ctx, const float* mel, float* out);
 /* sum|w| and sum w of the weight tensor with a given id (oracle/wo_model.c table) */
 spt_status spt_debug_weight_checksum(spt_ctx* ctx, int32_t tensor_id, double* out2);
+/* host-only (no device): whisper_tokenize with the vocabulary of a ggml file */
+spt_status spt_debug_ggml_tokenize(const char* model_path, const char* text, int32_t* tokens, int32_t n_max,
+                                   int32_t* n_out);
+/* host-only: the host reference dequantisation of n elements of one ggml type to f32 */
+spt_status spt_debug_ggml_dequant(int32_t ggml_type, const void* src, int64_t n, float* dst);
 
 #ifdef __cplusplus
 }

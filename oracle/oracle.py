@@ -78,6 +78,7 @@ def lib():
         L.wo_decode_logits.argtypes = [C.c_void_p, fp, ip, C.c_int, C.c_int, fp]
         L.wo_special_tokens.argtypes = [C.c_int, ip]
         L.wo_lang_detect.argtypes = [C.c_void_p, fp, C.c_int, fp]
+        L.wo_tensor_set.argtypes = [C.c_void_p, C.c_int, fp, C.c_int64]
         _lib = L
     return _lib
 
@@ -163,6 +164,12 @@ class Model:
             L.wo_tensor_info(self._p, i, C.byref(tid), C.byref(n), C.byref(ptr))
             out[tid.value] = np.ctypeslib.as_array(ptr, shape=(n.value,)).copy()
         return out
+
+    def set_tensor(self, tid: int, data: np.ndarray) -> None:
+        a = np.ascontiguousarray(data, dtype=np.float32).ravel()
+        rc = lib().wo_tensor_set(self._p, int(tid), _f(a), C.c_int64(a.size))
+        if rc != 0:
+            raise ValueError(f"wo_tensor_set({tid}) failed rc={rc}")
 
     def encode(self, mel_: np.ndarray, gelu: int = GELU_TANH) -> np.ndarray:
         mel_ = np.ascontiguousarray(mel_, dtype=np.float32)

@@ -221,6 +221,16 @@ int wo_tensor_info(const wo_model* m, int i, int* tid, int64_t* numel, const flo
     return 0;
 }
 
+int wo_tensor_set(wo_model* m, int tid, const float* data, int64_t numel) {
+    for (int i = 0; i < m->n_t; i++)
+        if (m->t[i].tid == tid) {
+            if (m->t[i].numel != numel) return -2;
+            memcpy(*m->t[i].slot, data, sizeof(float) * (size_t)numel);
+            return 0;
+        }
+    return -1;
+}
+
 void wo_set_threads(int n) {
 #ifdef _OPENMP
     if (n > 0) omp_set_num_threads(n);

@@ -23,6 +23,7 @@ EXPORTS = [
     "spt_ctx_destroy", "spt_last_error", "spt_ctx_info", "spt_transcribe", "spt_transcribe_batch",
     "spt_transcribe_batch_device", "spt_result_free", "spt_get_timings", "spt_debug_mel",
     "spt_debug_encode", "spt_debug_weight_checksum", "spt_probe_kernel", "spt_language_code",
+    "spt_tokenize", "spt_token_to_str", "spt_debug_ggml_tokenize", "spt_debug_ggml_dequant",
 ]
 PROBES = {"dec_cross_attn": 0, "dec_self_attn": 1, "dec_logits": 2, "dec_fc1": 3, "enc_fc1_gemm": 4,
           "enc_attn": 5}
@@ -89,6 +90,12 @@ def load():
     L.spt_result_free.argtypes = [C.POINTER(Result)]
     L.spt_language_code.argtypes = [C.c_int32]
     L.spt_language_code.restype = C.c_char_p
+    ip = C.POINTER(C.c_int32)
+    L.spt_tokenize.argtypes = [vp, C.c_char_p, ip, C.c_int32, ip]
+    L.spt_token_to_str.argtypes = [vp, C.c_int32]
+    L.spt_token_to_str.restype = C.c_char_p
+    L.spt_debug_ggml_tokenize.argtypes = [C.c_char_p, C.c_char_p, ip, C.c_int32, ip]
+    L.spt_debug_ggml_dequant.argtypes = [C.c_int32, C.c_void_p, C.c_int64, fp]
     L.spt_get_timings.argtypes = [vp, C.POINTER(Timings)]
     L.spt_debug_mel.argtypes = [vp, fp, C.c_size_t, fp]
     L.spt_debug_encode.argtypes = [vp, fp, fp]
@@ -97,7 +104,7 @@ def load():
                                    C.POINTER(C.c_int32)]
     for fn in ("spt_ctx_info", "spt_transcribe", "spt_transcribe_batch", "spt_transcribe_batch_device",
                "spt_get_timings", "spt_debug_mel", "spt_debug_encode", "spt_debug_weight_checksum",
-               "spt_probe_kernel"):
+               "spt_probe_kernel", "spt_tokenize", "spt_debug_ggml_tokenize", "spt_debug_ggml_dequant"):
         getattr(L, fn).restype = C.c_int
     _lib = L
     return L

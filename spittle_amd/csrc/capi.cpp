@@ -19,11 +19,14 @@
 #include "../../include/spittle_hip.h"
 #include "common.h"
 #include "engine.h"
+#include "ggml_file.h"
+#include "vocab.h"
 
 using spt::Engine;
 
 struct spt_ctx {
     std::unique_ptr<Engine> eng;
+    std::unique_ptr<spt::Vocab> vocab;  // ggml models; synthetic models have none
     std::string spec;
     std::string err;
 };
@@ -64,17 +67,27 @@ spt_status build_request(spt_ctx* c, const spt_infer_params* p, spt::DecodeReque
     *autolang = false;
     if (p->beam_size > 1) return fail(c, SPT_ERR_UNSUPPORTED, "beam search is not implemented (greedy only)");
     if (p->temperature != 0.0f) return fail(c, SPT_ERR_UNSUPPORTED, "only temperature 0 (greedy) is implemented");
-    if (p->initial_prompt && p->initial_prompt[0])
-        return fail(c, SPT_ERR_UNSUPPORTED,
-                    "initial_prompt text needs the model's tokenizer vocabulary (ggml loading); pass prompt_tokens");
+    // whisper_full: initial_prompt is tokenised (whisper_tokenize) only when no prompt_tokens
+    // are given; either way the tokens become the prompt_past
+    std::vector<int32_t> ptoks;
+    if (p->prompt_tokens && p->n_prompt_tokens > 0) {
+        ptoks.assign(p->prompt_tokens, p->prompt_tokens + p->n_prompt_tokens);
+    } else if (p->initial_prompt && p->initial_prompt[0]) {
+        if (!c->vocab)
+            return fail(c, SPT_ERR_UNSUPPORTED,
+                        "initial_prompt text needs the tokenizer vocabulary of a ggml model; pass prompt_tokens");
+        const std::vector<int> t = c->vocab->tokenize(p->initial_prompt, nullptr);
+        ptoks.assign(t.begin(), t.end());
+    }
     rq->prompt.clear();
     rq->prefix.clear();
     rq->lang_tok.clear();
-    if (p->prompt_tokens && p->n_prompt_tokens > 0) {
-        const int n_take = std::min(p->n_prompt_tokens, dm.n_text_ctx / 2);
+    if (!ptoks.empty()) {
+        const int np = (int)ptoks.size();
+        const int n_take = std::min(np, dm.n_text_ctx / 2);
         rq->prefix.push_back(sp.prev);
-        for (int i = p->n_prompt_tokens - n_take; i < p->n_prompt_tokens; ++i) {
-            const int t = p->prompt_tokens[i];
+        for (int i = np - n_take; i < np; ++i) {
+            const int t = ptoks[i];
             if (t < 0 || t >= dm.n_vocab) return fail(c, SPT_ERR_INVALID_ARG, "prompt token out of the vocabulary");
             rq->prefix.push_back(t);
         }
@@ -103,6 +116,13 @@ spt_status build_request(spt_ctx* c, const spt_infer_params* p, spt::DecodeReque
     rq->n_forced = p->forced_tokens ? p->n_forced : 0;
     if (rq->n_forced < 0 || rq->n_forced > dm.n_text_ctx) return fail(c, SPT_ERR_INVALID_ARG, "n_forced out of range");
     return SPT_OK;
+}
+
+// whisper_full's segment text: the token strings of the text tokens (ids >= eot are skipped);
+// a synthetic model has no vocabulary and shows the ids as "[id]"
+void append_text(const spt_ctx* c, std::string* text, int t) {
+    if (c->vocab) *text += c->vocab->str(t);
+    else *text += "[" + std::to_string(t) + "]";
 }
 
 int lang_index(int lang_tok, const spt::Specials& sp) { return lang_tok > sp.sot ? lang_tok - sp.sot - 1 : -1; }
@@ -188,7 +208,7 @@ spt_status run_windows(spt_ctx* c, std::vector<Window>& win, size_t n_utt, const
                 tok[u].push_back(t);
                 t1[u].push_back(o1[(size_t)b * rq.n_steps + s2]);
                 t2[u].push_back(o2[(size_t)b * rq.n_steps + s2]);
-                if (t < eot) text[u] += "[" + std::to_string(t) + "]";  // synthetic model: no vocabulary
+                if (t < eot) append_text(c, &text[u], t);
                 if (t == eot && !(rq.flags & SPT_IGNORE_EOT)) break;
             }
         }
@@ -207,7 +227,7 @@ spt_status run_windows(spt_ctx* c, std::vector<Window>& win, size_t n_utt, const
 
 extern "C" {
 
-const char* spt_version(void) { return "spittle_amd 0.2.0 (gfx950, ABI 2)"; }
+const char* spt_version(void) { return "spittle_amd 0.3.0 (gfx950, ABI 2)"; }
 
 const char* spt_language_code(int32_t lang_id) { return spt::lang_code(lang_id); }
 
@@ -248,6 +268,7 @@ spt_status spt_ctx_create(const char* model_spec, const spt_model_params* params
     uint64_t seed = mp.seed;
     std::string perr;
     const std::string spec(model_spec);
+    std::unique_ptr<spt::GgmlFile> file;
     if (!spt::parse_synthetic_spec(spec, &dm, &seed, &perr)) {
         FILE* f = fopen(model_spec, "rb");
         if (!f) {
@@ -255,8 +276,12 @@ spt_status spt_ctx_create(const char* model_spec, const spt_model_params* params
             return SPT_ERR_LOAD;
         }
         fclose(f);
-        set_err(err, errlen, "ggml model loading is not implemented yet: " + spec);
-        return SPT_ERR_UNSUPPORTED;
+        file.reset(new spt::GgmlFile());
+        if (!file->open(spec, &perr) || !spt::ggml_dims(*file, &dm, &perr)) {
+            set_err(err, errlen, spec + ": " + perr);
+            return SPT_ERR_LOAD;
+        }
+        perr.clear();
     }
     if (!perr.empty()) {
         set_err(err, errlen, perr);
@@ -275,7 +300,8 @@ spt_status spt_ctx_create(const char* model_spec, const spt_model_params* params
     if (!c) return SPT_ERR_OOM;
     try {
         c->eng.reset(new Engine(dm, mp.dtype == SPT_DTYPE_BF16 ? spt::DT_BF16 : spt::DT_F32, mp.device,
-                                mp.max_batch, seed));
+                                mp.max_batch, seed, file.get()));
+        if (file) c->vocab.reset(new spt::Vocab(file->vocab(), dm.n_vocab, spt::specials_for(dm.n_vocab)));
     } catch (const std::exception& e) {
         set_err(err, errlen, e.what());
         const spt_status s = classify(e);
@@ -377,7 +403,7 @@ spt_status spt_transcribe_batch_device(spt_ctx* ctx, const float* pcm_dev, size_
                 t.push_back(tk);
                 a.push_back(o1[(size_t)b * rq.n_steps + s2]);
                 c2.push_back(o2[(size_t)b * rq.n_steps + s2]);
-                if (tk < eot) txt += "[" + std::to_string(tk) + "]";
+                if (tk < eot) append_text(ctx, &txt, tk);
                 if (tk == eot && !(rq.flags & SPT_IGNORE_EOT)) break;
             }
             out[b] = make_result(1, lang_index(lang[b], sp), &t, &a, &c2, &txt);
@@ -395,6 +421,25 @@ void spt_result_free(spt_result* r) {
     free(r->top1);
     free(r->top2);
     free(r);
+}
+
+spt_status spt_tokenize(spt_ctx* ctx, const char* text, int32_t* tokens, int32_t n_max, int32_t* n_out) {
+    if (!ctx || !text || !n_out || (n_max > 0 && !tokens)) return fail(ctx, SPT_ERR_INVALID_ARG, "null argument");
+    if (!ctx->vocab) return fail(ctx, SPT_ERR_UNSUPPORTED, "synthetic models have no vocabulary");
+    try {
+        const std::vector<int> t = ctx->vocab->tokenize(text, nullptr);
+        *n_out = (int32_t)t.size();
+        if ((int64_t)t.size() > n_max) return fail(ctx, SPT_ERR_INVALID_ARG, "token buffer too small");
+        for (size_t i = 0; i < t.size(); ++i) tokens[i] = t[i];
+        return SPT_OK;
+    } catch (const std::exception& e) {
+        return fail(ctx, classify(e), e.what());
+    }
+}
+
+const char* spt_token_to_str(const spt_ctx* ctx, int32_t id) {
+    if (!ctx || !ctx->vocab || id < 0 || id >= ctx->vocab->size()) return nullptr;
+    return ctx->vocab->str(id).c_str();
 }
 
 spt_status spt_get_timings(const spt_ctx* ctx, spt_timings* t) {
@@ -434,6 +479,29 @@ spt_status spt_debug_weight_checksum(spt_ctx* ctx, int32_t tensor_id, double* ou
     } catch (const std::exception& e) {
         return fail(ctx, classify(e), e.what());
     }
+}
+
+spt_status spt_debug_ggml_tokenize(const char* model_path, const char* text, int32_t* tokens, int32_t n_max,
+                                   int32_t* n_out) {
+    if (!model_path || !text || !n_out || (n_max > 0 && !tokens)) return SPT_ERR_INVALID_ARG;
+    spt::GgmlFile f;
+    std::string err;
+    if (!f.open(model_path, &err)) return SPT_ERR_LOAD;
+    spt::Vocab v(f.vocab(), f.hparams().n_vocab, spt::specials_for(f.hparams().n_vocab));
+    const std::vector<int> t = v.tokenize(text, nullptr);
+    *n_out = (int32_t)t.size();
+    if ((int64_t)t.size() > n_max) return SPT_ERR_INVALID_ARG;
+    for (size_t i = 0; i < t.size(); ++i) tokens[i] = t[i];
+    return SPT_OK;
+}
+
+spt_status spt_debug_ggml_dequant(int32_t ggml_type, const void* src, int64_t n, float* dst) {
+    if (!src || !dst || n < 0) return SPT_ERR_INVALID_ARG;
+    int blck, bytes;
+    spt::GgmlFile::type_block(ggml_type, &blck, &bytes);
+    if (!blck) return SPT_ERR_UNSUPPORTED;
+    if (n % blck) return SPT_ERR_INVALID_ARG;
+    return spt::ggml_dequant_host(ggml_type, (const uint8_t*)src, n, dst) ? SPT_OK : SPT_ERR_UNSUPPORTED;
 }
 
 }  // extern "C"

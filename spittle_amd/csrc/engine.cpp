@@ -8,6 +8,7 @@
 // / whisper_sample_token loop, for the greedy, fixed-language, no-timestamp
 // protocol of BASELINE.md.
 #include "engine.h"
+#include "ggml_file.h"
 
 #include <cstdio>
 
@@ -118,7 +119,7 @@ struct Carver {
 
 void Engine::select() const { HIP_CHECK(hipSetDevice(dev_)); }
 
-Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64_t seed)
+Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64_t seed, const GgmlFile* src)
     : dm_(dm), dt_(dtype), dev_(device), max_batch_(max_batch), seed_(seed) {
     if (dm_.d % 128 || dm_.d / 64 != dm_.n_head) throw std::runtime_error("unsupported model width");
     if (max_batch_ < 1 || max_batch_ > 64) throw std::runtime_error("max_batch must be in 1..64");
@@ -140,15 +141,23 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
         HIP_CHECK(hipStreamCreateWithFlags(&g.st, hipStreamNonBlocking));
         HIP_CHECK(hipEventCreateWithFlags(&g.ev, hipEventDisableTiming));
     }
-    gemv_prepare(dt_);
-    alloc_weights();
-    generate_weights();
-    upload_tables();
-    alloc_workspace();
-    HIP_CHECK(hipStreamSynchronize(st_));
+    try {
+        gemv_prepare(dt_);
+        alloc_weights();
+        if (src) load_ggml(*src);
+        else generate_weights();
+        upload_tables(src ? &src->mel_filters() : nullptr);
+        alloc_workspace();
+        HIP_CHECK(hipStreamSynchronize(st_));
+    } catch (...) {
+        release();  // a throwing constructor runs no destructor
+        throw;
+    }
 }
 
-Engine::~Engine() {
+Engine::~Engine() { release(); }
+
+void Engine::release() {
     (void)hipSetDevice(dev_);
     if (st_) (void)hipStreamSynchronize(st_);
     for (auto& g : groups_) {
@@ -163,6 +172,12 @@ Engine::~Engine() {
         if (p) (void)hipFree(p);
     for (auto& e : ev_) (void)hipEventDestroy(e);
     if (st_) (void)hipStreamDestroy(st_);
+    groups_.clear();
+    ev_.clear();
+    warena_ = aarena_ = nullptr;
+    hann_ = sinv_ = cosv_ = filt_ = nullptr;
+    grp_ = nullptr;
+    st_ = nullptr;
 }
 
 // ----------------------------------------------------------------------------- weights
@@ -289,7 +304,155 @@ void Engine::generate_weights() {
     HIP_CHECK(hipGetLastError());
 }
 
-void Engine::upload_tables() {
+// ----------------------------------------------------------------------------- ggml models
+bool ggml_dims(const GgmlFile& f, ModelDims* dm, std::string* err) {
+    const GgmlHparams& h = f.hparams();
+    if (h.n_audio_state != h.n_text_state) { *err = "encoder and decoder widths differ"; return false; }
+    if (h.n_audio_head != h.n_text_head || h.n_audio_state != 64 * h.n_audio_head) {
+        *err = "unsupported head layout (head dim must be 64)";
+        return false;
+    }
+    if (h.n_audio_ctx != 1500 || h.n_text_ctx != 448) { *err = "unsupported context sizes"; return false; }
+    if (h.n_mels != 80 && h.n_mels != 128) { *err = "unsupported n_mels " + std::to_string(h.n_mels); return false; }
+    if (f.n_mel_filters() != h.n_mels || f.n_fft() != 201) { *err = "mel filterbank is not [n_mels][201]"; return false; }
+    if (h.n_audio_layer < 1 || h.n_text_layer < 1 || h.n_vocab < 51864) { *err = "bad layer count or vocabulary"; return false; }
+    dm->name = "ggml";
+    dm->n_mels = h.n_mels;
+    dm->d = h.n_audio_state;
+    dm->n_head = h.n_audio_head;
+    dm->n_enc = h.n_audio_layer;
+    dm->n_dec = h.n_text_layer;
+    dm->n_vocab = h.n_vocab;
+    dm->n_audio_ctx = h.n_audio_ctx;
+    dm->n_text_ctx = h.n_text_ctx;
+    return true;
+}
+
+// whisper.cpp whisper_model_load's tensor names -> the engine arena.  Matrices (and the token
+// embedding, conv kernels) are stored in the engine dtype, everything else in f32; q/k/v are
+// fused into one [3d][d] matrix (the key has no bias: zeros), each decoder layer's cross K/V
+// projection into ckv_w_ rows [2l d, 2l d + 2d).  Conv kernels are re-laid [d][C][3] ->
+// [d][3][Cp] (Cp = padded mel channels) for the implicit-GEMM convolution.  Tensor ids match
+// generate_weights() so the checksum probes address both kinds of model alike.
+void Engine::load_ggml(const GgmlFile& f) {
+    const int64_t d = dm_.d, dd = d * d;
+    std::vector<std::pair<const GgmlTensor*, std::string>> used;
+    auto need = [&](const std::string& name, int64_t n) -> const GgmlTensor* {
+        const GgmlTensor* t = f.find(name);
+        if (!t) throw std::runtime_error("model file lacks tensor " + name);
+        if (t->numel() != n)
+            throw std::runtime_error("tensor " + name + " has " + std::to_string(t->numel()) + " elements, expected " +
+                                     std::to_string(n));
+        return t;
+    };
+    size_t stage_bytes = 0;
+    struct Staging {
+        void* p = nullptr;
+        ~Staging() { if (p) (void)hipFree(p); }
+    } staging;
+    for (int pass = 0; pass < 2; ++pass) {  // pass 0 sizes the staging buffer, pass 1 loads
+        if (pass) HIP_CHECK(hipMalloc(&staging.p, std::max<size_t>(stage_bytes, 256)));
+        void* stage = staging.p;
+        auto put = [&](const std::string& name, int64_t n, void* dst, int dt, int tid) {
+            const GgmlTensor* t = need(name, n);
+            if (!pass) { stage_bytes = std::max(stage_bytes, t->nbytes); return; }
+            HIP_CHECK(hipMemcpyAsync(stage, t->data, t->nbytes, hipMemcpyHostToDevice, st_));
+            ggml_dequant(t->type, stage, n, dt, dst, st_);
+            HIP_CHECK(hipStreamSynchronize(st_));  // the staging buffer is reused by the next tensor
+            tref_[tid] = TRef{dst, n, dt};
+        };
+        auto putf = [&](const std::string& name, int64_t n, float* dst, int tid) { put(name, n, dst, DT_F32, tid); };
+        auto putw = [&](const std::string& name, int64_t n, void* dst, int tid) { put(name, n, dst, dt_, tid); };
+        auto at = [&](void* p, int64_t elems) { return (void*)((char*)p + elems * esz_); };
+        auto conv = [&](const std::string& name, int C, int Cp, void* dst, int tid) {
+            const GgmlTensor* t = need(name, d * C * 3);
+            if (!pass) return;
+            std::vector<float> src((size_t)t->numel());
+            if (!ggml_dequant_host(t->type, t->data, t->numel(), src.data()))
+                throw std::runtime_error("unsupported ggml type for " + name);
+            std::vector<float> lay((size_t)d * 3 * Cp, 0.0f);
+            for (int64_t n = 0; n < d; ++n)
+                for (int c = 0; c < C; ++c)
+                    for (int j = 0; j < 3; ++j) lay[((size_t)n * 3 + j) * Cp + c] = src[((size_t)n * C + c) * 3 + j];
+            if (dt_ == DT_BF16) {
+                std::vector<bf16> h(lay.size());
+                for (size_t i = 0; i < lay.size(); ++i) h[i] = f2bf(lay[i]);
+                HIP_CHECK(hipMemcpy(dst, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+            } else {
+                HIP_CHECK(hipMemcpy(dst, lay.data(), lay.size() * 4, hipMemcpyHostToDevice));
+            }
+            tref_[tid] = TRef{dst, (int64_t)lay.size(), dt_};
+        };
+        conv("encoder.conv1.weight", dm_.n_mels, cp_, conv1_w_, 1);
+        putf("encoder.conv1.bias", d, conv1_b_, 2);
+        conv("encoder.conv2.weight", (int)d, (int)d, conv2_w_, 3);
+        putf("encoder.conv2.bias", d, conv2_b_, 4);
+        putf("encoder.ln_post.weight", d, lnp_w_, 5);
+        putf("encoder.ln_post.bias", d, lnp_b_, 6);
+        putf("encoder.positional_embedding", (int64_t)dm_.n_audio_ctx * d, enc_pos_, 7);
+        for (int l = 0; l < dm_.n_enc; ++l) {
+            EncL& e = enc_[l];
+            const int b = 100 + 32 * l;
+            const std::string p = "encoder.blocks." + std::to_string(l) + ".";
+            putf(p + "attn_ln.weight", d, e.ln1_w, b + 0);
+            putf(p + "attn_ln.bias", d, e.ln1_b, b + 1);
+            putw(p + "attn.query.weight", dd, at(e.qkv_w, 0), b + 2);
+            putf(p + "attn.query.bias", d, e.qkv_b, b + 3);
+            putw(p + "attn.key.weight", dd, at(e.qkv_w, dd), b + 4);
+            putw(p + "attn.value.weight", dd, at(e.qkv_w, 2 * dd), b + 5);
+            putf(p + "attn.value.bias", d, e.qkv_b + 2 * d, b + 6);
+            putw(p + "attn.out.weight", dd, e.o_w, b + 7);
+            putf(p + "attn.out.bias", d, e.o_b, b + 8);
+            putf(p + "mlp_ln.weight", d, e.ln2_w, b + 9);
+            putf(p + "mlp_ln.bias", d, e.ln2_b, b + 10);
+            putw(p + "mlp.0.weight", 4 * dd, e.fc1_w, b + 11);
+            putf(p + "mlp.0.bias", 4 * d, e.fc1_b, b + 12);
+            putw(p + "mlp.2.weight", 4 * dd, e.fc2_w, b + 13);
+            putf(p + "mlp.2.bias", d, e.fc2_b, b + 14);
+            if (pass) fill_f32(e.qkv_b + d, d, 0.0f, st_);
+        }
+        putw("decoder.token_embedding.weight", (int64_t)dm_.n_vocab * d, tok_emb_, 10);
+        putf("decoder.positional_embedding", (int64_t)dm_.n_text_ctx * d, dec_pos_, 11);
+        putf("decoder.ln.weight", d, lnf_w_, 12);
+        putf("decoder.ln.bias", d, lnf_b_, 13);
+        for (int l = 0; l < dm_.n_dec; ++l) {
+            DecL& e = dec_[l];
+            const int b = 5000 + 32 * l;
+            const std::string p = "decoder.blocks." + std::to_string(l) + ".";
+            putf(p + "attn_ln.weight", d, e.ln1_w, b + 0);
+            putf(p + "attn_ln.bias", d, e.ln1_b, b + 1);
+            putw(p + "attn.query.weight", dd, at(e.qkv_w, 0), b + 2);
+            putf(p + "attn.query.bias", d, e.qkv_b, b + 3);
+            putw(p + "attn.key.weight", dd, at(e.qkv_w, dd), b + 4);
+            putw(p + "attn.value.weight", dd, at(e.qkv_w, 2 * dd), b + 5);
+            putf(p + "attn.value.bias", d, e.qkv_b + 2 * d, b + 6);
+            putw(p + "attn.out.weight", dd, e.so_w, b + 7);
+            putf(p + "attn.out.bias", d, e.so_b, b + 8);
+            putf(p + "cross_attn_ln.weight", d, e.ln2_w, b + 9);
+            putf(p + "cross_attn_ln.bias", d, e.ln2_b, b + 10);
+            putw(p + "cross_attn.query.weight", dd, e.cq_w, b + 11);
+            putf(p + "cross_attn.query.bias", d, e.cq_b, b + 12);
+            putw(p + "cross_attn.key.weight", dd, at(ckv_w_, (2 * l) * dd), b + 13);
+            putw(p + "cross_attn.value.weight", dd, at(ckv_w_, (2 * l + 1) * dd), b + 14);
+            putf(p + "cross_attn.value.bias", d, ckv_b_ + (2 * l + 1) * d, b + 15);
+            putw(p + "cross_attn.out.weight", dd, e.co_w, b + 16);
+            putf(p + "cross_attn.out.bias", d, e.co_b, b + 17);
+            putf(p + "mlp_ln.weight", d, e.ln3_w, b + 18);
+            putf(p + "mlp_ln.bias", d, e.ln3_b, b + 19);
+            putw(p + "mlp.0.weight", 4 * dd, e.fc1_w, b + 20);
+            putf(p + "mlp.0.bias", 4 * d, e.fc1_b, b + 21);
+            putw(p + "mlp.2.weight", 4 * dd, e.fc2_w, b + 22);
+            putf(p + "mlp.2.bias", d, e.fc2_b, b + 23);
+            if (pass) {
+                fill_f32(e.qkv_b + d, d, 0.0f, st_);
+                fill_f32(ckv_b_ + (2 * l) * d, d, 0.0f, st_);
+            }
+        }
+        if (pass) HIP_CHECK(hipStreamSynchronize(st_));
+    }
+}
+
+void Engine::upload_tables(const std::vector<float>* filters) {
     // whisper_global_cache: sin/cos tables and periodic Hann from float(theta)
     std::vector<float> hann(400), sv(400), cv(400);
     for (int i = 0; i < 400; ++i) {
@@ -317,17 +480,20 @@ void Engine::upload_tables() {
     }
     std::vector<float> filt((size_t)nm * 201);
     std::vector<int> grp(2 * nm);
+    if (filters) filt = *filters;  // the model file's bank (ggml_dims checked [n_mels][201])
     for (int j = 0; j < nm; ++j) {
         const double en = 2.0 / (ff[j + 2] - ff[j]);
         int lo = -1, hi = -1;
         for (int k = 0; k < 201; ++k) {
-            const double fk = 8000.0 * k / 200.0;
-            const double down = -(ff[j] - fk) / (ff[j + 1] - ff[j]);
-            const double up = (ff[j + 2] - fk) / (ff[j + 2] - ff[j + 1]);
-            double v = std::min(down, up);
-            if (v < 0) v = 0;
-            const float fv = (float)(v * en);
-            filt[(size_t)j * 201 + k] = fv;
+            if (!filters) {
+                const double fk = 8000.0 * k / 200.0;
+                const double down = -(ff[j] - fk) / (ff[j + 1] - ff[j]);
+                const double up = (ff[j + 2] - fk) / (ff[j + 2] - ff[j + 1]);
+                double v = std::min(down, up);
+                if (v < 0) v = 0;
+                filt[(size_t)j * 201 + k] = (float)(v * en);
+            }
+            const float fv = filt[(size_t)j * 201 + k];
             if (fv != 0.0f) {
                 if (lo < 0) lo = k;
                 hi = k;

@@ -11,6 +11,8 @@
 
 namespace spt {
 
+class GgmlFile;
+
 struct ModelDims {
     std::string name;
     int n_mels = 80, d = 384, n_head = 6, n_enc = 4, n_dec = 4, n_vocab = 51864;
@@ -44,7 +46,9 @@ struct Timings {
 
 class Engine {
 public:
-    Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64_t seed);
+    // src == nullptr: synthetic weights from `seed`; else the weights, mel filters of a ggml file
+    // (dm from ggml_dims(*src)); the file is read during construction only
+    Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64_t seed, const GgmlFile* src = nullptr);
     ~Engine();
     Engine(const Engine&) = delete;
     Engine& operator=(const Engine&) = delete;
@@ -106,10 +110,12 @@ private:
     };
 
     void select() const;
+    void release();
     void alloc_weights();
     void generate_weights();
+    void load_ggml(const GgmlFile& f);
     void alloc_workspace();
-    void upload_tables();
+    void upload_tables(const std::vector<float>* filters);
     void stage_pcm(const float* const* pcm, const int* n, int B);
     void run_mel(const float* pcm_dev, int64_t stride, int B, float* dbg);
     void run_encoder(int B);
@@ -174,6 +180,9 @@ private:
 
     Timings tm_;
 };
+
+// model dimensions of a ggml file's hparams; false + *err if the engine cannot run it
+bool ggml_dims(const GgmlFile& f, ModelDims* dm, std::string* err);
 
 // parse "synthetic:<model>[:enc=N][:dec=N][:seed=S]"; returns false if not synthetic
 bool parse_synthetic_spec(const std::string& spec, ModelDims* dm, uint64_t* seed, std::string* err);

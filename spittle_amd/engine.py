@@ -128,8 +128,8 @@ class WhisperEngine:
 
     # -- lifecycle ----------------------------------------------------------
     def load_model(self, model_path: str) -> None:
-        """`model_path`: a ggml .bin path (not yet supported) or
-        ``synthetic:<name>[:enc=N][:dec=N][:seed=S]``."""
+        """`model_path`: a whisper.cpp ggml .bin file (f32/f16/q4_0/q4_1/q5_0/q5_1/q8_0 tensors)
+        or ``synthetic:<name>[:enc=N][:dec=N][:seed=S]``."""
         self.unload_model()
         mp = L.ModelParams()
         self._lib.spt_default_model_params(C.byref(mp))
@@ -234,6 +234,20 @@ class WhisperEngine:
         self._check(self._lib.spt_probe_kernel(self._ctx, L.PROBES[kernel], int(iters), C.byref(us), C.byref(work),
                                                C.byref(fl)))
         return {"avg_us": us.value, "work": work.value, "work_is_flops": bool(fl.value)}
+
+    def tokenize(self, text: str) -> list[int]:
+        """whisper_tokenize with the loaded ggml model's vocabulary (greedy longest match)."""
+        self._need()
+        raw = text.encode("utf-8")
+        n = C.c_int32()
+        buf = (C.c_int32 * max(1, len(raw) + 1))()
+        self._check(self._lib.spt_tokenize(self._ctx, raw, buf, len(raw) + 1, C.byref(n)))
+        return [buf[i] for i in range(n.value)]
+
+    def token_to_str(self, token: int) -> Optional[bytes]:
+        """whisper_token_to_str: the token's bytes (None for synthetic models / bad ids)."""
+        self._need()
+        return self._lib.spt_token_to_str(self._ctx, int(token))
 
     def weight_checksum(self, tensor_id: int):
         self._need()
