@@ -24,11 +24,11 @@ import struct
 import numpy as np
 
 MAGIC = 0x67676D6C
-F32, F16, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0 = 0, 1, 2, 3, 6, 7, 8
+F32, F16, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q4_K, Q5_K, Q6_K = 0, 1, 2, 3, 6, 7, 8, 12, 13, 14
 BLOCK = {F32: (1, 4), F16: (1, 2), Q4_0: (32, 18), Q4_1: (32, 20), Q5_0: (32, 22), Q5_1: (32, 24),
-         Q8_0: (32, 34)}
+         Q8_0: (32, 34), Q4_K: (256, 144), Q5_K: (256, 176), Q6_K: (256, 210)}
 # file-level ftype (ggml_ftype) of a model whose 2-D weights are of a given tensor type
-FTYPE = {F32: 0, F16: 1, Q4_0: 2, Q4_1: 3, Q8_0: 7, Q5_0: 8, Q5_1: 9}
+FTYPE = {F32: 0, F16: 1, Q4_0: 2, Q4_1: 3, Q8_0: 7, Q5_0: 8, Q5_1: 9, Q4_K: 12, Q5_K: 13, Q6_K: 14}
 
 
 # ----------------------------------------------------------------------------- quantisation
@@ -36,9 +36,122 @@ def _f16(x):
     return np.asarray(x, np.float32).astype(np.float16)
 
 
+def _rnd(v):
+    return np.sign(v) * np.floor(np.abs(v) + 0.5)
+
+
+def _pack_k4_scales(sc: np.ndarray, mn: np.ndarray) -> np.ndarray:
+    """inverse of get_scale_min_k4: 8 six-bit scale and min codes -> 12 bytes"""
+    q = np.zeros((sc.shape[0], 12), np.uint8)
+    for j in range(4):
+        q[:, j] = (sc[:, j] & 63) | ((sc[:, j + 4] >> 4) << 6)
+        q[:, j + 4] = (mn[:, j] & 63) | ((mn[:, j + 4] >> 4) << 6)
+        q[:, j + 8] = (sc[:, j + 4] & 0xF) | ((mn[:, j + 4] & 0xF) << 4)
+    return q
+
+
+def _quantize_k(x: np.ndarray, t: int) -> bytes:
+    """A valid (not ggml's iterative, error-minimising) encoding of the K-quant formats: the
+    tests only need well-formed blocks to compare the loader with dequantize()."""
+    b = x.reshape(-1, 256).astype(np.float32)
+    nb = b.shape[0]
+    if t == Q6_K:
+        sub = b.reshape(nb, 16, 16)
+        s = np.abs(sub).max(axis=2) / 31.0
+        d = (s.max(axis=1) / 127.0).astype(np.float32)
+        d16 = _f16(d)
+        dq = d16.astype(np.float32)
+        sc = np.clip(_rnd(s / np.where(dq > 0, dq, 1)[:, None]), -128, 127).astype(np.int8)
+        step = dq[:, None] * sc.astype(np.float32)
+        q = np.clip(_rnd(sub / np.where(step != 0, step, 1)[:, :, None]), -32, 31).astype(np.int32) + 32
+        q = q.reshape(nb, 256)
+        out = np.zeros((nb, 210), np.uint8)
+        for h in range(2):
+            e = q[:, 128 * h:128 * h + 128]
+            out[:, 64 * h:64 * h + 32] = (e[:, 0:32] & 0xF) | ((e[:, 64:96] & 0xF) << 4)
+            out[:, 64 * h + 32:64 * h + 64] = (e[:, 32:64] & 0xF) | ((e[:, 96:128] & 0xF) << 4)
+            out[:, 128 + 32 * h:128 + 32 * h + 32] = ((e[:, 0:32] >> 4) | ((e[:, 32:64] >> 4) << 2) |
+                                                     ((e[:, 64:96] >> 4) << 4) | ((e[:, 96:128] >> 4) << 6))
+        out[:, 192:208] = sc.view(np.uint8)
+        out[:, 208:210] = d16.view(np.uint8).reshape(nb, 2)
+        return out.tobytes()
+    qmax = 15 if t == Q4_K else 31
+    sub = b.reshape(nb, 8, 32)
+    lo = np.minimum(sub.min(axis=2), 0.0)
+    s = (sub.max(axis=2) - lo) / qmax
+    d16, m16 = _f16(s.max(axis=1) / 63.0), _f16(-lo.min(axis=1) / 63.0)
+    d, dmin = d16.astype(np.float32), m16.astype(np.float32)
+    sc = np.clip(np.ceil(s / np.where(d > 0, d, 1)[:, None]), 0, 63).astype(np.int32)
+    mn = np.clip(_rnd(-lo / np.where(dmin > 0, dmin, 1)[:, None]), 0, 63).astype(np.int32)
+    step = d[:, None] * sc
+    q = np.clip(_rnd((sub + (dmin[:, None] * mn)[:, :, None]) / np.where(step > 0, step, 1)[:, :, None]), 0, qmax)
+    q = q.astype(np.int32).reshape(nb, 4, 2, 32)  # [group][low/high sub-block][l]
+    out = np.zeros((nb, 144 if t == Q4_K else 176), np.uint8)
+    out[:, 0:2] = d16.view(np.uint8).reshape(nb, 2)
+    out[:, 2:4] = m16.view(np.uint8).reshape(nb, 2)
+    out[:, 4:16] = _pack_k4_scales(sc, mn)
+    o = 16
+    if t == Q5_K:
+        qh = np.zeros((nb, 32), np.int32)
+        for g in range(4):
+            qh |= ((q[:, g, 0] >> 4) & 1) << (2 * g)
+            qh |= ((q[:, g, 1] >> 4) & 1) << (2 * g + 1)
+        out[:, 16:48] = qh.astype(np.uint8)
+        o = 48
+    ql = (q[:, :, 0] & 0xF) | ((q[:, :, 1] & 0xF) << 4)
+    out[:, o:o + 128] = ql.reshape(nb, 128).astype(np.uint8)
+    return out.tobytes()
+
+
+def _dequantize_k(a: np.ndarray, t: int, n: int) -> np.ndarray:
+    """dequantize_row_q4_K / q5_K / q6_K (products rounded one at a time)"""
+    _, nbytes = BLOCK[t]
+    b = a[: (n // 256) * nbytes].reshape(-1, nbytes)
+    nb = b.shape[0]
+    if t == Q6_K:
+        ql, qh = b[:, 0:128].astype(np.int32), b[:, 128:192].astype(np.int32)
+        sc = b[:, 192:208].view(np.int8).astype(np.float32)
+        d = b[:, 208:210].copy().view(np.float16).astype(np.float32)[:, 0]
+        q = np.zeros((nb, 256), np.int32)
+        for h in range(2):
+            a_, b_, c = ql[:, 64 * h:64 * h + 32], ql[:, 64 * h + 32:64 * h + 64], qh[:, 32 * h:32 * h + 32]
+            q[:, 128 * h:128 * h + 32] = (a_ & 0xF) | (((c >> 0) & 3) << 4)
+            q[:, 128 * h + 32:128 * h + 64] = (b_ & 0xF) | (((c >> 2) & 3) << 4)
+            q[:, 128 * h + 64:128 * h + 96] = (a_ >> 4) | (((c >> 4) & 3) << 4)
+            q[:, 128 * h + 96:128 * h + 128] = (b_ >> 4) | (((c >> 6) & 3) << 4)
+        ds = (d[:, None] * sc).astype(np.float32)  # [nb][16]: d * sc, then * q
+        v = np.repeat(ds, 16, axis=1) * (q - 32).astype(np.float32)
+        return v.astype(np.float32).ravel()
+    d = b[:, 0:2].copy().view(np.float16).astype(np.float32)[:, 0]
+    dmin = b[:, 2:4].copy().view(np.float16).astype(np.float32)[:, 0]
+    s = b[:, 4:16].astype(np.int32)
+    sc, mn = np.zeros((nb, 8), np.int32), np.zeros((nb, 8), np.int32)
+    for j in range(8):
+        if j < 4:
+            sc[:, j], mn[:, j] = s[:, j] & 63, s[:, j + 4] & 63
+        else:
+            sc[:, j] = (s[:, j + 4] & 0xF) | ((s[:, j - 4] >> 6) << 4)
+            mn[:, j] = (s[:, j + 4] >> 4) | ((s[:, j] >> 6) << 4)
+    o = 48 if t == Q5_K else 16
+    ql = b[:, o:o + 128].astype(np.int32).reshape(nb, 4, 32)
+    q = np.stack([ql & 0xF, ql >> 4], axis=2)  # [nb][4][2][32]
+    if t == Q5_K:
+        qh = b[:, 16:48].astype(np.int32)
+        for g in range(4):
+            q[:, g, 0] += ((qh >> (2 * g)) & 1) * 16
+            q[:, g, 1] += ((qh >> (2 * g + 1)) & 1) * 16
+    dd = (d[:, None] * sc.astype(np.float32)).astype(np.float32).reshape(nb, 4, 2, 1)
+    mm = (dmin[:, None] * mn.astype(np.float32)).astype(np.float32).reshape(nb, 4, 2, 1)
+    v = (dd * q.astype(np.float32)).astype(np.float32) - mm
+    return v.astype(np.float32).ravel()
+
+
 def quantize(x: np.ndarray, t: int) -> bytes:
-    """ggml-quants.c quantize_row_*_ref of a flat f32 array (length % 32 == 0 for q types)."""
+    """ggml-quants.c quantize_row_*_ref of a flat f32 array (length % 32 == 0 for q types;
+    % 256 for the K types, whose encoder here is a simple valid one, see _quantize_k)."""
     x = np.ascontiguousarray(x, np.float32).ravel()
+    if t in (Q4_K, Q5_K, Q6_K):
+        return _quantize_k(x, t)
     if t == F32:
         return x.tobytes()
     if t == F16:
@@ -96,6 +209,8 @@ def dequantize(raw: bytes, t: int, n: int) -> np.ndarray:
         return a.view(np.float32)[:n].copy()
     if t == F16:
         return a.view(np.float16)[:n].astype(np.float32)
+    if t in (Q4_K, Q5_K, Q6_K):
+        return _dequantize_k(a, t, n)
     _, bytes_ = BLOCK[t]
     b = a[: (n // 32) * bytes_].reshape(-1, bytes_)
     d = b[:, 0:2].copy().view(np.float16).astype(np.float32)[:, 0]

@@ -123,6 +123,9 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     : dm_(dm), dt_(dtype), dev_(device), max_batch_(max_batch), seed_(seed) {
     if (dm_.d % 128 || dm_.d / 64 != dm_.n_head) throw std::runtime_error("unsupported model width");
     if (max_batch_ < 1 || max_batch_ > 64) throw std::runtime_error("max_batch must be in 1..64");
+    if (dt_ == DT_F32 && dm_.d > 1024)  // LayerNorm-prologue GEMVs stage <= 16 f32 super-steps
+        throw std::runtime_error("the f32 engine supports model widths up to 1024 (tiny..medium); load " +
+                                 std::to_string(dm_.d) + "-wide models in bf16");
     esz_ = dt_ == DT_BF16 ? 2 : 4;
     cp_ = ((dm_.n_mels + 63) / 64) * 64;
     if ((3 * cp_ * esz_) % 128) cp_ = ((dm_.n_mels + 127) / 128) * 128;

@@ -1,6 +1,7 @@
 // ggml_file.cpp -- see ggml_file.h.  Host side of model loading only: the bulk
 // dequantisation of the weight matrices runs on the device (k_init.hip ggml_dequant).
 #include "ggml_file.h"
+#include "ggml_quant.h"
 
 #include <fcntl.h>
 #include <math.h>
@@ -12,28 +13,6 @@
 namespace spt {
 
 namespace {
-
-float h2f(uint16_t h) {  // IEEE half -> float
-    const uint32_t s = (uint32_t)(h & 0x8000) << 16;
-    uint32_t e = (h >> 10) & 0x1f, m = h & 0x3ff;
-    uint32_t u;
-    if (e == 0) {
-        if (m == 0) u = s;
-        else {  // subnormal
-            e = 127 - 15 + 1;
-            while (!(m & 0x400)) { m <<= 1; --e; }
-            m &= 0x3ff;
-            u = s | (e << 23) | (m << 13);
-        }
-    } else if (e == 31) {
-        u = s | 0x7f800000u | (m << 13);
-    } else {
-        u = s | ((e + 127 - 15) << 23) | (m << 13);
-    }
-    float f;
-    memcpy(&f, &u, 4);
-    return f;
-}
 
 struct Reader {
     const uint8_t* p;
@@ -56,18 +35,7 @@ struct Reader {
 
 }  // namespace
 
-void GgmlFile::type_block(int type, int* blck, int* bytes) {
-    switch (type) {
-        case GG_F32: *blck = 1; *bytes = 4; return;
-        case GG_F16: *blck = 1; *bytes = 2; return;
-        case GG_Q4_0: *blck = 32; *bytes = 18; return;
-        case GG_Q4_1: *blck = 32; *bytes = 20; return;
-        case GG_Q5_0: *blck = 32; *bytes = 22; return;
-        case GG_Q5_1: *blck = 32; *bytes = 24; return;
-        case GG_Q8_0: *blck = 32; *bytes = 34; return;
-        default: *blck = 0; *bytes = 0; return;
-    }
-}
+void GgmlFile::type_block(int type, int* blck, int* bytes) { ggml_block_geom(type, blck, bytes); }
 
 GgmlFile::~GgmlFile() {
     if (map_) munmap(map_, size_);
@@ -134,65 +102,23 @@ const GgmlTensor* GgmlFile::find(const std::string& name) const {
     return it == index_.end() ? nullptr : &tensors_[it->second];
 }
 
-// ggml-quants.c dequantize_row_* (block formats of ggml: d / m f16 scale and offset, 4-bit
-// nibbles lo = elements 0..15, hi = 16..31 of a block; q5 adds the fifth bit from qh)
 bool ggml_dequant_host(int type, const uint8_t* src, int64_t n, float* dst) {
-    auto f16 = [](const uint8_t* p) { uint16_t h; memcpy(&h, p, 2); return h2f(h); };
-    switch (type) {
-        case GG_F32: memcpy(dst, src, n * 4); return true;
-        case GG_F16:
-            for (int64_t i = 0; i < n; ++i) dst[i] = f16(src + 2 * i);
-            return true;
-        case GG_Q8_0:
-            for (int64_t b = 0; b < n / 32; ++b) {
-                const uint8_t* p = src + b * 34;
-                const float d = f16(p);
-                for (int j = 0; j < 32; ++j) dst[b * 32 + j] = d * (float)(int8_t)p[2 + j];
-            }
-            return true;
-        case GG_Q4_0:
-        case GG_Q4_1:
-            for (int64_t b = 0; b < n / 32; ++b) {
-                const uint8_t* p = src + b * (type == GG_Q4_0 ? 18 : 20);
-                const float d = f16(p), m = type == GG_Q4_1 ? f16(p + 2) : 0.0f;
-                const uint8_t* qs = p + (type == GG_Q4_0 ? 2 : 4);
-                for (int j = 0; j < 16; ++j) {
-                    const int lo = qs[j] & 0xf, hi = qs[j] >> 4;
-                    if (type == GG_Q4_0) {
-                        dst[b * 32 + j] = (float)(lo - 8) * d;
-                        dst[b * 32 + j + 16] = (float)(hi - 8) * d;
-                    } else {
-                        dst[b * 32 + j] = (float)lo * d + m;
-                        dst[b * 32 + j + 16] = (float)hi * d + m;
-                    }
-                }
-            }
-            return true;
-        case GG_Q5_0:
-        case GG_Q5_1:
-            for (int64_t b = 0; b < n / 32; ++b) {
-                const uint8_t* p = src + b * (type == GG_Q5_0 ? 22 : 24);
-                const float d = f16(p), m = type == GG_Q5_1 ? f16(p + 2) : 0.0f;
-                const uint8_t* q = p + (type == GG_Q5_0 ? 2 : 4);
-                uint32_t qh;
-                memcpy(&qh, q, 4);
-                const uint8_t* qs = q + 4;
-                for (int j = 0; j < 16; ++j) {
-                    const int x0 = (qs[j] & 0xf) | (((qh >> j) << 4) & 0x10);
-                    const int x1 = (qs[j] >> 4) | ((qh >> (j + 12)) & 0x10);
-                    if (type == GG_Q5_0) {
-                        dst[b * 32 + j] = (float)(x0 - 16) * d;
-                        dst[b * 32 + j + 16] = (float)(x1 - 16) * d;
-                    } else {
-                        dst[b * 32 + j] = (float)x0 * d + m;
-                        dst[b * 32 + j + 16] = (float)x1 * d + m;
-                    }
-                }
-            }
-            return true;
-        default:
-            return false;
+    if (type == GQ_F32) {
+        memcpy(dst, src, n * 4);
+        return true;
     }
+    if (type == GQ_F16) {
+        for (int64_t i = 0; i < n; ++i) dst[i] = gq_half(src + 2 * i);
+        return true;
+    }
+    int blck, bytes;
+    ggml_block_geom(type, &blck, &bytes);
+    if (!blck || n % blck) return false;
+    for (int64_t b = 0; b < n / blck; ++b) {
+        float* o = dst + b * blck;
+        ggml_dequant_block(type, src + b * bytes, [o](int i, float v) { o[i] = v; });
+    }
+    return true;
 }
 
 }  // namespace spt

@@ -18,10 +18,6 @@
 
 namespace spt {
 
-// ggml type ids (ggml.h enum ggml_type)
-enum { GG_F32 = 0, GG_F16 = 1, GG_Q4_0 = 2, GG_Q4_1 = 3, GG_Q5_0 = 6, GG_Q5_1 = 7, GG_Q8_0 = 8,
-       GG_Q4_K = 12, GG_Q5_K = 13, GG_Q6_K = 14 };
-
 struct GgmlTensor {
     std::string name;
     int type = 0;

@@ -8,6 +8,7 @@
 // are rounded to bf16 with round-to-nearest-even, exactly as the oracle does.
 #include "common.h"
 #include "kernels.h"
+#include "ggml_quant.h"
 
 namespace spt {
 
@@ -123,64 +124,33 @@ void cache_flush(const void* p, int64_t bytes, unsigned* sink, hipStream_t st) {
 
 // ---------------------------------------------------------------- ggml weight dequantisation
 // Model loading (ggml_file.h): the raw ggml blocks are copied to the device as they lie in the
-// file and expanded here, one thread per 32-element block (per element for f32/f16), into the
-// engine's storage type.  Block formats (ggml-quants.c dequantize_row_*): f16 scale d (and
-// offset m for the _1 types); nibbles j and j+16 of a block share byte j; q5 takes its fifth
-// bit from the 32-bit qh word.  Values are d*q (+m) in f32, then rounded once to bf16 (RNE).
+// file and expanded here into the engine's storage type, one thread per block (per element for
+// f32 / f16), by the routine the host shares (ggml_quant.h); values are f32, then rounded once
+// to bf16 (RNE) for a bf16 engine.
 namespace {
-__device__ __forceinline__ float ld_f16(const uint8_t* p) {
-    const uint16_t h = (uint16_t)p[0] | ((uint16_t)p[1] << 8);
-    return (float)__builtin_bit_cast(_Float16, h);
-}
 template <typename T>
 __global__ __launch_bounds__(256) void dequant_kernel(int type, const uint8_t* __restrict__ src, int64_t n,
                                                       T* __restrict__ dst) {
-#pragma clang fp contract(off)  // d*q and + m rounded separately, as ggml's C does
     const int64_t stride = (int64_t)gridDim.x * 256;
-    if (type == 0 || type == 1) {  // f32, f16: per element
-        for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-            float v;
-            if (type == 0) v = ((const float*)src)[i];
-            else v = ld_f16(src + 2 * i);
-            dst[i] = from_f<T>(v);
-        }
+    if (type == GQ_F32 || type == GQ_F16) {
+        for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
+            dst[i] = from_f<T>(type == GQ_F32 ? ((const float*)src)[i] : gq_half(src + 2 * i));
         return;
     }
-    const int bytes = type == 2 ? 18 : type == 3 ? 20 : type == 6 ? 22 : type == 7 ? 24 : 34;
-    const bool has_m = type == 3 || type == 7;
-    for (int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x; b < n / 32; b += stride) {
-        const uint8_t* p = src + b * bytes;
-        const float d = ld_f16(p), m = has_m ? ld_f16(p + 2) : 0.0f;
-        const uint8_t* q = p + (has_m ? 4 : 2);
-        T* o = dst + b * 32;
-        if (type == 8) {  // q8_0
-#pragma unroll 8
-            for (int j = 0; j < 32; ++j) o[j] = from_f<T>(d * (float)(int8_t)q[j]);
-            continue;
-        }
-        uint32_t qh = 0;
-        if (type == 6 || type == 7) {
-            qh = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
-            q += 4;
-        }
-        const int off = (type == 2) ? 8 : (type == 6) ? 16 : 0;  // symmetric types centre the code
-#pragma unroll 4
-        for (int j = 0; j < 16; ++j) {
-            int x0 = q[j] & 0xf, x1 = q[j] >> 4;
-            if (type == 6 || type == 7) {
-                x0 |= ((qh >> j) << 4) & 0x10;
-                x1 |= (qh >> (j + 12)) & 0x10;
-            }
-            o[j] = from_f<T>((float)(x0 - off) * d + m);
-            o[j + 16] = from_f<T>((float)(x1 - off) * d + m);
-        }
+    int blck, bytes;
+    ggml_block_geom(type, &blck, &bytes);
+    for (int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x; b < n / blck; b += stride) {
+        T* o = dst + b * blck;
+        ggml_dequant_block(type, src + b * bytes, [o](int i, float v) { o[i] = from_f<T>(v); });
     }
 }
 }  // namespace
 
 void ggml_dequant(int type, const void* src, int64_t n, int out_dtype, void* dst, hipStream_t st) {
-    const int64_t units = (type == 0 || type == 1) ? n : n / 32;
-    const int g = grid_for(units);
+    int blck, bytes;
+    ggml_block_geom(type, &blck, &bytes);
+    if (!blck || n % blck) throw std::runtime_error("ggml_dequant: unsupported type or ragged tensor");
+    const int g = grid_for(n / blck);
     if (out_dtype == DT_BF16)
         hipLaunchKernelGGL(dequant_kernel<bf16>, dim3(g), dim3(256), 0, st, type, (const uint8_t*)src, n, (bf16*)dst);
     else

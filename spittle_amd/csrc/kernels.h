@@ -34,7 +34,7 @@ void gen_conv_weights(int store_dtype, void* dst, int N, int C, int Cp, uint64_t
 void fill_f32(float* dst, int64_t n, float v, hipStream_t st);
 // read `bytes` of p once (measurement: cold caches before a probed launch)
 // ggml tensor bytes on the device -> engine storage (out_dtype DT_F32 / DT_BF16); type is the
-// ggml type id (0 f32, 1 f16, 2 q4_0, 3 q4_1, 6 q5_0, 7 q5_1, 8 q8_0), n a multiple of 32
+// ggml type id (ggml_quant.h GQ_*), n a multiple of the type's block
 void ggml_dequant(int type, const void* src, int64_t n, int out_dtype, void* dst, hipStream_t st);
 void cache_flush(const void* p, int64_t bytes, unsigned* sink, hipStream_t st);
 // weight checksum helper for tests: sum of |w| and sum of w (f64) of a device tensor

@@ -56,36 +56,64 @@ def test_known_answer_blocks():
         assert np.array_equal(_host_dequant(raw, t, 32), G.dequantize(raw, t, 32))
 
 
-@pytest.mark.parametrize("t", [G.F32, G.F16, G.Q4_0, G.Q4_1, G.Q5_0, G.Q5_1, G.Q8_0])
+@pytest.mark.parametrize("t", [G.F32, G.F16, G.Q4_0, G.Q4_1, G.Q5_0, G.Q5_1, G.Q8_0, G.Q4_K, G.Q5_K, G.Q6_K])
 def test_host_dequant_matches_restatement(t):
     rng = np.random.default_rng(t)
-    x = (rng.standard_normal(32 * 257) * np.exp(rng.uniform(-6, 3, 32 * 257))).astype(np.float32)
+    x = (rng.standard_normal(256 * 33) * np.exp(rng.uniform(-6, 3, 256 * 33))).astype(np.float32)
     raw = G.quantize(x, t)
     assert len(raw) == (x.size // G.BLOCK[t][0]) * G.BLOCK[t][1]
     ref = G.dequantize(raw, t, x.size)
     assert np.array_equal(_host_dequant(raw, t, x.size), ref)
     # random bytes too (every code / high bit pattern), finite f16 scales
     blk, nbytes = G.BLOCK[t]
-    if blk == 32:
+    if blk > 1:
         junk = bytearray(rng.integers(0, 256, 64 * nbytes, dtype=np.uint8).tobytes())
+        halves = {G.Q4_1: (0, 2), G.Q5_1: (0, 2), G.Q4_K: (0, 2), G.Q5_K: (0, 2), G.Q6_K: (208,)}.get(t, (0,))
         for b in range(64):
-            junk[b * nbytes:b * nbytes + 2] = _f16(float(rng.uniform(-2, 2)))
-            if t in (G.Q4_1, G.Q5_1):
-                junk[b * nbytes + 2:b * nbytes + 4] = _f16(float(rng.uniform(-2, 2)))
+            for o in halves:
+                junk[b * nbytes + o:b * nbytes + o + 2] = _f16(float(rng.uniform(-2, 2)))
         raw = bytes(junk)
-        assert np.array_equal(_host_dequant(raw, t, 64 * 32), G.dequantize(raw, t, 64 * 32))
+        assert np.array_equal(_host_dequant(raw, t, 64 * blk), G.dequantize(raw, t, 64 * blk))
+
+
+def test_known_answer_k_blocks():
+    """q4_K / q6_K blocks assembled by hand (ggml-quants.h block_q4_K, block_q6_K)."""
+    # q4_K: d = 1, dmin = 0.5; sub-block 0 scale 2 min 1, sub-block 5 scale 17 (4 + 16) min 33 (1 + 32)
+    sc = bytearray(12)
+    sc[0], sc[4] = 2, 1
+    sc[1] |= 1 << 6           # high bits of sub-block 5's scale (scales[j - 4] >> 6)
+    sc[5] |= 2 << 6           # high bits of sub-block 5's min (scales[j] >> 6, j = 5)
+    sc[9] = 1 | (1 << 4)      # low nibbles of sub-block 5's scale / min
+    qs = bytearray(128)
+    qs[0] = 0x3 | (0x7 << 4)  # element 0: 3 (sub-block 0), element 32: 7 (sub-block 1)
+    qs[64 + 5] = 0x9 << 4     # element 128 + 32 + 5 = 165 (sub-block 5, high nibble): 9
+    raw = _f16(1.0) + _f16(0.5) + bytes(sc) + bytes(qs)
+    v = G.dequantize(raw, G.Q4_K, 256)
+    assert v[0] == 2 * 3 - 0.5 and v[1] == -0.5
+    assert v[165] == 17 * 9 - 0.5 * 33
+    assert np.array_equal(_host_dequant(raw, G.Q4_K, 256), v)
+    # q6_K: d = 0.25; 16-element sub-block 0 has scale 4, sub-block 9 (elements 144..159) -2;
+    # codes are 6 bits minus 32
+    ql, qh, s6 = bytearray(128), bytearray(64), bytearray(16)
+    s6[0], s6[9] = 4, 0xFE
+    ql[0], qh[0] = 0xF, 0x3  # element 0: 0xF | 3 << 4 = 63
+    ql[64 + 16] = 0x5        # element 128 + 16 = 144 (second half, l = 16): low nibble 5
+    raw = bytes(ql) + bytes(qh) + bytes(s6) + _f16(0.25)
+    v = G.dequantize(raw, G.Q6_K, 256)
+    assert v[0] == 0.25 * 4 * 31 and v[144] == 0.25 * -2 * (5 - 32) and v[1] == 0.25 * 4 * -32
+    assert np.array_equal(_host_dequant(raw, G.Q6_K, 256), v)
 
 
 def test_quantizer_round_trip_error():
-    x = np.random.default_rng(0).uniform(-1, 1, 32 * 64).astype(np.float32)
+    x = np.random.default_rng(0).uniform(-1, 1, 256 * 8).astype(np.float32)
     for t, tol in ((G.F16, 1e-3), (G.Q8_0, 1 / 127), (G.Q5_1, 2 / 31), (G.Q5_0, 1 / 16 + 1e-3),
-                   (G.Q4_1, 2 / 15), (G.Q4_0, 1 / 8 + 1e-3)):
+                   (G.Q4_1, 2 / 15), (G.Q4_0, 1 / 8 + 1e-3), (G.Q6_K, 0.02), (G.Q5_K, 0.04), (G.Q4_K, 0.08)):
         y = G.dequantize(G.quantize(x, t), t, x.size)
         assert np.abs(x - y).max() <= tol, t
 
 
 def test_unsupported_type_rejected():
-    assert _lib().spt_debug_ggml_dequant(12, b"\0" * 256, 256, (C.c_float * 256)()) != 0  # q4_K
+    assert _lib().spt_debug_ggml_dequant(10, b"\0" * 256, 256, (C.c_float * 256)()) != 0  # q2_K
 
 
 # ---------------------------------------------------------------- files and tokenizer
@@ -189,11 +217,16 @@ def test_bad_files_fail_to_load(tmp_path):
     p.write_bytes(data[: len(data) // 2])  # truncated vocabulary
     st, msg = _ctx_create(str(p))
     assert st == L.SPT_ERR_LOAD and "truncated" in msg
-    # a tensor of an unsupported type (q4_K)
-    tail = struct.pack("<iii", 2, 4, 12) + struct.pack("<2i", 256, 4) + b"abcd" + b"\0" * 576
+    # a tensor of an unsupported type (q3_K)
+    tail = struct.pack("<iii", 2, 4, 11) + struct.pack("<2i", 256, 4) + b"abcd" + b"\0" * 440
     p.write_bytes(data + tail)
     st, msg = _ctx_create(str(p))
-    assert st == L.SPT_ERR_LOAD and "unsupported ggml type 12" in msg
+    assert st == L.SPT_ERR_LOAD and "unsupported ggml type 11" in msg
+    # a K-quant row that is not a multiple of the 256-element block
+    tail = struct.pack("<iii", 2, 4, 13) + struct.pack("<2i", 384, 2) + b"abcd" + b"\0" * 528
+    p.write_bytes(data + tail)
+    st, msg = _ctx_create(str(p))
+    assert st == L.SPT_ERR_LOAD and "multiple of the block" in msg
     # a tensor whose data runs past the end of the file
     tail = struct.pack("<iii", 1, 4, 0) + struct.pack("<i", 64) + b"abcd" + b"\0" * 100
     p.write_bytes(data + tail)

@@ -32,13 +32,14 @@ def _engine_dtype_tids(dims):
 
 class ModelFile:
     def __init__(self, tmp, cfg, wtype, n_enc=None, n_dec=None, **kw):
-        self.dims = O.dims_for(cfg, n_enc, n_dec)
+        self.dims = O.dims_for(cfg, n_enc, n_dec) if isinstance(cfg, str) else cfg
         base = O.Model(self.dims, SEED, O.W_F32)
         self.sp = O.special_tokens(self.dims.n_vocab)
         self.vocab = G.synth_vocab(self.sp["eot"])
         codes = [c.decode() for c in (_lib().spt_language_code(i) for i in range(100))]
         self.full_vocab = self.vocab + G.special_names(self.dims.n_vocab, len(self.vocab), self.sp, codes)
-        self.path = str(tmp / f"ggml-{cfg}-{wtype}.bin")
+        tag = cfg if isinstance(cfg, str) else f"d{cfg.d}"
+        self.path = str(tmp / f"ggml-{tag}-{wtype}.bin")
         self.deq = G.write_model(self.path, self.dims, O.mel_filters(self.dims.n_mels), self.vocab, base.tensors(),
                                  wtype, **kw)
         base.close()
@@ -117,6 +118,27 @@ def test_quantized_file_f32(tmp_path, wtype):
     e.unload_model()
 
 
+@pytest.mark.parametrize("wtype", [G.Q5_K, G.Q4_K, G.Q6_K])
+def test_k_quant_file_f32(tmp_path, wtype):
+    """K-quants (256-element super-blocks: the catalog's breeze-asr-q5_k) need rows that are
+    multiples of 256: base geometry (512 wide, 8 heads), 2 + 2 layers, f32 engine."""
+    mf = ModelFile(tmp_path, O.Dims(80, 512, 8, 2, 2, 51865, 1500, 448), wtype)
+    e = _engine(mf.path)
+    for tid in (10, 102, 111, 113, 5013, 5054):
+        w = mf.deq[tid].astype(np.float64)
+        a, s = e.weight_checksum(tid)
+        assert a == pytest.approx(np.abs(w).sum(), rel=1e-10), tid
+        assert s == pytest.approx(w.sum(), rel=1e-8, abs=1e-6), tid
+    om = mf.oracle()
+    x = O.synth_audio(8)
+    n = 8
+    r = e.transcribe_samples(x, _params(ignore_eot=True, max_new_tokens=n))
+    enc = om.encode(O.mel(x, 80))
+    tk, t1, t2 = om.decode(enc, O.default_prompt(mf.dims.n_vocab), n, FLAGS)
+    _check_greedy(np.array(r.tokens), r.top1, tk, t1, t2)
+    e.unload_model()
+
+
 def test_f16_file_bf16_engine(tmp_path):
     """bf16 engine, large-v3 geometry (128 mels, 1280 wide, 2 + 2 layers), f16 file."""
     mf = ModelFile(tmp_path, "large-v3", G.F16, 2, 2)
@@ -162,6 +184,14 @@ def test_initial_prompt(tiny_f32):
     tk, t1, t2 = om.decode(enc, O.default_prompt(tiny_f32.dims.n_vocab, past=ids), n, FLAGS)
     _check_greedy(np.array(a.tokens), a.top1, tk, t1, t2)
     e.unload_model()
+
+
+def test_f32_engine_width_limit(tmp_path):
+    """The f32 engine (a parity mode) stages LayerNorm'd decoder rows of at most 1024 f32 values;
+    wider models load in bf16 -- and a wider f32 request fails at load, not mid-transcription."""
+    from spittle_amd import TranscriptionError
+    with pytest.raises(TranscriptionError, match="f32 engine"):
+        _engine("synthetic:large-v3:enc=1:dec=1", "f32")
 
 
 def test_missing_or_misshapen_tensor(tmp_path):
