@@ -145,7 +145,7 @@ def main():
     eng = WhisperEngine(WhisperModelParams(dtype=args.dtype, device=local, max_batch=B, seed=1234))
     eng.load_model(args.model)
     info = eng.info()
-    params = WhisperInferenceParams(language="en", ignore_eot=True, max_new_tokens=args.decode_steps)
+    params = WhisperInferenceParams(language="en", no_timestamps=True, temperature_inc=0.0, ignore_eot=True, max_new_tokens=args.decode_steps)
     lens = [pcm.shape[1]] * B
 
     def step():

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 2
+#define SPT_ABI_VERSION 3
 
 typedef enum {
     SPT_OK = 0,
@@ -51,6 +51,7 @@ typedef enum { SPT_DTYPE_F32 = 0, SPT_DTYPE_BF16 = 1 } spt_dtype;
 #define SPT_SUPPRESS_BLANK  1u  /* whisper_full_params.suppress_blank (default on) */
 #define SPT_NO_TIMESTAMPS   2u  /* whisper_full_params.no_timestamps */
 #define SPT_IGNORE_EOT      4u  /* benchmark protocol: keep decoding past <|endoftext|> */
+#define SPT_SUPPRESS_NST    8u  /* whisper_full_params.suppress_non_speech_tokens (ggml models) */
 
 typedef struct {
     int32_t dtype;        /* spt_dtype: weights + activations (accumulation is always f32) */
@@ -65,26 +66,52 @@ typedef struct {
                                     (whisper_lang_auto_detect on the utterance's first 30 s) */
     int32_t translate;           /* task <|translate|> instead of <|transcribe|> */
     const char* initial_prompt;  /* jargon prompt text (src-tauri/src/jargon.rs:594); ggml models */
-    uint32_t flags;              /* SPT_SUPPRESS_BLANK | SPT_NO_TIMESTAMPS | SPT_IGNORE_EOT */
-    int32_t max_new_tokens;      /* generated tokens per 30 s window (<= 220 like whisper.cpp) */
-    float temperature;           /* only 0 (greedy) is implemented */
-    int32_t beam_size;           /* only 1 (greedy) is implemented */
+    uint32_t flags;              /* SPT_SUPPRESS_BLANK | SPT_NO_TIMESTAMPS | SPT_SUPPRESS_NST |
+                                    SPT_IGNORE_EOT; default SPT_SUPPRESS_BLANK (whisper_full's
+                                    defaults: timestamps on) */
+    int32_t max_new_tokens;      /* fast path: generated tokens per 30 s window (<= 220);
+                                    whisper_full path: whisper_full_params.max_tokens (0 = none) */
+    float temperature;           /* initial temperature (0 = greedy) */
+    int32_t beam_size;           /* only 1 (greedy sampling strategy) is implemented */
     const int32_t* forced_tokens;/* test hook (teacher forcing): [batch][n_forced] or NULL */
     int32_t n_forced;
     const int32_t* prompt_tokens;/* whisper_full_params.prompt_tokens: decoded before [sot ...] as
                                     [prev] + the last min(224, n) of them; NULL = none */
     int32_t n_prompt_tokens;
+    /* ABI 3: whisper_full's window loop (timestamps, segments, temperature fallback).  A call
+     * takes the device-resident no-timestamp greedy fast path when SPT_NO_TIMESTAMPS is set and
+     * temperature_inc == 0 and temperature == 0; every other call runs whisper_full. */
+    float temperature_inc;       /* fallback step (0.2); 0 = no fallback */
+    int32_t best_of;             /* sampled decoders per window at temperature > 0 (5) */
+    float entropy_thold;         /* a decoder whose last 32 tokens' entropy is lower fails (2.4) */
+    float logprob_thold;         /* fall back when the average log-probability is lower (-1.0) */
+    float max_initial_ts;        /* the first timestamp is at most this many seconds (1.0) */
+    int32_t reserved0;
+    uint64_t seed;               /* temperature sampling stream */
 } spt_infer_params;
 
 typedef struct {
-    char* text;             /* the text tokens' strings; for synthetic models the ids as "[id]" */
-    int32_t* tokens;        /* generated token ids (EOT included, stops after it) */
-    float* top1;            /* suppressed logit of the chosen token, per step */
-    float* top2;            /* runner-up suppressed logit, per step */
+    int64_t t0, t1;              /* whisper_full_get_segment_t0 / t1: 10 ms units */
+    char* text;                  /* whisper_full_get_segment_text */
+    int32_t i0, n_tokens;        /* the segment's tokens in spt_result.tokens */
+} spt_segment;
+
+typedef struct {
+    char* text;             /* fast path: the text tokens' strings; whisper_full path: the segment
+                               texts joined and trimmed (transcribe-rs TranscriptionResult.text);
+                               synthetic models spell tokens as "[id]" */
+    int32_t* tokens;        /* token ids: fast path every generated token (EOT included, stops
+                               after it); whisper_full path each window's chosen decoder's result */
+    float* top1;            /* fast path: suppressed logit of the token; whisper_full: its log-prob */
+    float* top2;            /* fast path: runner-up suppressed logit; whisper_full: its timestamp id */
     int32_t n_tokens;
-    int32_t n_windows;      /* 30 s windows the input was split into */
+    int32_t n_windows;      /* 30 s windows decoded */
     int32_t language;       /* language index decoded with (whisper.cpp order, spt_language_code);
                                -1 for English-only models */
+    int32_t n_segments;     /* whisper_full path (0 on the fast path) */
+    spt_segment* segments;
+    int32_t n_fallbacks;    /* temperature fallbacks taken: decodes repeated at a higher temperature */
+    int32_t reserved0;
 } spt_result;
 
 typedef struct {

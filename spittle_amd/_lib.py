@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(HERE, "libspittle_hip.so")
 SPT_OK, SPT_ERR_INVALID_ARG, SPT_ERR_LOAD, SPT_ERR_DEVICE, SPT_ERR_OOM, SPT_ERR_UNSUPPORTED, SPT_ERR_INTERNAL = range(7)
 STATUS_NAMES = {0: "OK", 1: "INVALID_ARG", 2: "LOAD", 3: "DEVICE", 4: "OOM", 5: "UNSUPPORTED", 6: "INTERNAL"}
 SPT_DTYPE_F32, SPT_DTYPE_BF16 = 0, 1
-SPT_SUPPRESS_BLANK, SPT_NO_TIMESTAMPS, SPT_IGNORE_EOT = 1, 2, 4
+SPT_SUPPRESS_BLANK, SPT_NO_TIMESTAMPS, SPT_IGNORE_EOT, SPT_SUPPRESS_NST = 1, 2, 4, 8
 
 # every symbol include/spittle_hip.h declares
 EXPORTS = [
@@ -38,13 +38,22 @@ class InferParams(C.Structure):
     _fields_ = [("language", C.c_char_p), ("translate", C.c_int32), ("initial_prompt", C.c_char_p),
                 ("flags", C.c_uint32), ("max_new_tokens", C.c_int32), ("temperature", C.c_float),
                 ("beam_size", C.c_int32), ("forced_tokens", C.POINTER(C.c_int32)), ("n_forced", C.c_int32),
-                ("prompt_tokens", C.POINTER(C.c_int32)), ("n_prompt_tokens", C.c_int32)]
+                ("prompt_tokens", C.POINTER(C.c_int32)), ("n_prompt_tokens", C.c_int32),
+                ("temperature_inc", C.c_float), ("best_of", C.c_int32), ("entropy_thold", C.c_float),
+                ("logprob_thold", C.c_float), ("max_initial_ts", C.c_float), ("reserved0", C.c_int32),
+                ("seed", C.c_uint64)]
+
+
+class Segment(C.Structure):
+    _fields_ = [("t0", C.c_int64), ("t1", C.c_int64), ("text", C.c_char_p), ("i0", C.c_int32),
+                ("n_tokens", C.c_int32)]
 
 
 class Result(C.Structure):
     _fields_ = [("text", C.c_char_p), ("tokens", C.POINTER(C.c_int32)), ("top1", C.POINTER(C.c_float)),
                 ("top2", C.POINTER(C.c_float)), ("n_tokens", C.c_int32), ("n_windows", C.c_int32),
-                ("language", C.c_int32)]
+                ("language", C.c_int32), ("n_segments", C.c_int32), ("segments", C.POINTER(Segment)),
+                ("n_fallbacks", C.c_int32), ("reserved0", C.c_int32)]
 
 
 class ModelInfo(C.Structure):

@@ -19,6 +19,7 @@
 #include "../../include/spittle_hip.h"
 #include "common.h"
 #include "engine.h"
+#include "full.h"
 #include "ggml_file.h"
 #include "vocab.h"
 
@@ -55,6 +56,40 @@ spt_status classify(const std::exception& e) {
     return SPT_ERR_INVALID_ARG;
 }
 
+// whisper_full: initial_prompt is tokenised (whisper_tokenize) only when no prompt_tokens are
+// given; either way the tokens become the prompt_past
+spt_status prompt_tokens_of(spt_ctx* c, const spt_infer_params* p, std::vector<int32_t>* out) {
+    out->clear();
+    if (p->prompt_tokens && p->n_prompt_tokens > 0) {
+        out->assign(p->prompt_tokens, p->prompt_tokens + p->n_prompt_tokens);
+    } else if (p->initial_prompt && p->initial_prompt[0]) {
+        if (!c->vocab)
+            return fail(c, SPT_ERR_UNSUPPORTED,
+                        "initial_prompt text needs the tokenizer vocabulary of a ggml model; pass prompt_tokens");
+        const std::vector<int> t = c->vocab->tokenize(p->initial_prompt, nullptr);
+        out->assign(t.begin(), t.end());
+    }
+    for (int32_t t : *out)
+        if (t < 0 || t >= c->eng->dims().n_vocab) return fail(c, SPT_ERR_INVALID_ARG, "prompt token out of the vocabulary");
+    return SPT_OK;
+}
+
+// language of a request: >= 0 the fixed language token, -1 auto-detect, -2 English-only model
+spt_status lang_of(spt_ctx* c, const spt_infer_params* p, int* lang_tok) {
+    const spt::Specials sp = spt::specials_for(c->eng->dims().n_vocab);
+    if (sp.n_langs <= 0) { *lang_tok = -2; return SPT_OK; }
+    if (!p->language || !p->language[0] || std::string(p->language) == "auto") { *lang_tok = -1; return SPT_OK; }
+    const int lid = spt::lang_id(p->language);
+    if (lid < 0 || lid >= sp.n_langs) return fail(c, SPT_ERR_INVALID_ARG, std::string("unknown language '") + p->language + "'");
+    *lang_tok = sp.sot + 1 + lid;
+    return SPT_OK;
+}
+
+// the device-resident greedy no-timestamp protocol, or whisper_full's window loop
+bool full_mode(const spt_infer_params* p) {
+    return !(p->flags & SPT_NO_TIMESTAMPS) || p->temperature_inc > 0.0f || p->temperature != 0.0f;
+}
+
 // whisper_full's prompt_init: [sot] (+ [lang, task] for multilingual) + [notimestamps]; its
 // prompt_past ([prev] + the last n_text_ctx / 2 prompt tokens) goes to rq->prefix.  With no
 // language (the app's "auto", settings.rs:925) *auto is set and the caller fills rq->lang_tok.
@@ -66,19 +101,9 @@ spt_status build_request(spt_ctx* c, const spt_infer_params* p, spt::DecodeReque
     const spt::Specials sp = spt::specials_for(dm.n_vocab);
     *autolang = false;
     if (p->beam_size > 1) return fail(c, SPT_ERR_UNSUPPORTED, "beam search is not implemented (greedy only)");
-    if (p->temperature != 0.0f) return fail(c, SPT_ERR_UNSUPPORTED, "only temperature 0 (greedy) is implemented");
-    // whisper_full: initial_prompt is tokenised (whisper_tokenize) only when no prompt_tokens
-    // are given; either way the tokens become the prompt_past
     std::vector<int32_t> ptoks;
-    if (p->prompt_tokens && p->n_prompt_tokens > 0) {
-        ptoks.assign(p->prompt_tokens, p->prompt_tokens + p->n_prompt_tokens);
-    } else if (p->initial_prompt && p->initial_prompt[0]) {
-        if (!c->vocab)
-            return fail(c, SPT_ERR_UNSUPPORTED,
-                        "initial_prompt text needs the tokenizer vocabulary of a ggml model; pass prompt_tokens");
-        const std::vector<int> t = c->vocab->tokenize(p->initial_prompt, nullptr);
-        ptoks.assign(t.begin(), t.end());
-    }
+    spt_status st = prompt_tokens_of(c, p, &ptoks);
+    if (st != SPT_OK) return st;
     rq->prompt.clear();
     rq->prefix.clear();
     rq->lang_tok.clear();
@@ -105,8 +130,7 @@ spt_status build_request(spt_ctx* c, const spt_infer_params* p, spt::DecodeReque
         rq->prompt.push_back(sp.sot + 1 + lid);  // replaced per sequence when auto-detecting
         rq->prompt.push_back(p->translate ? sp.translate : sp.transcribe);
     }
-    if (p->flags & SPT_NO_TIMESTAMPS) rq->prompt.push_back(sp.not_);
-    else return fail(c, SPT_ERR_UNSUPPORTED, "timestamp decoding is not implemented (set SPT_NO_TIMESTAMPS)");
+    rq->prompt.push_back(sp.not_);  // the fast path is the no-timestamp protocol
     int n = p->max_new_tokens > 0 ? p->max_new_tokens : 220;
     const int used = (int)(rq->prefix.size() + rq->prompt.size());
     if (used + n > dm.n_text_ctx + 1) n = dm.n_text_ctx + 1 - used;
@@ -150,6 +174,85 @@ spt_result* make_result(int n_windows, int language, std::vector<int>* acc_tok, 
     }
     memcpy(r->text, text->c_str(), text->size() + 1);
     return r;
+}
+
+// transcribe-rs joins the segment texts and trims the result (str::trim: ASCII whitespace here)
+std::string trimmed(const std::string& s) {
+    const char* ws = " \t\n\r\v\f";
+    const size_t a = s.find_first_not_of(ws);
+    if (a == std::string::npos) return std::string();
+    return s.substr(a, s.find_last_not_of(ws) - a + 1);
+}
+
+spt_result* make_full_result(const spt::FullResult& f, const spt::Specials& sp) {
+    std::vector<int> tok = f.tokens;
+    std::vector<float> a = f.plog, b = f.tid;
+    std::string text = trimmed(f.text);
+    spt_result* r = make_result(f.n_windows, lang_index(f.lang_tok, sp), &tok, &a, &b, &text);
+    if (!r) return nullptr;
+    r->n_fallbacks = f.n_fallbacks;
+    const size_t ns = f.segments.size();
+    r->segments = (spt_segment*)calloc(ns ? ns : 1, sizeof(spt_segment));
+    if (!r->segments) { spt_result_free(r); return nullptr; }
+    r->n_segments = (int32_t)ns;
+    for (size_t i = 0; i < ns; ++i) {
+        const spt::FullSegment& s = f.segments[i];
+        spt_segment& o = r->segments[i];
+        o.t0 = s.t0; o.t1 = s.t1; o.i0 = s.i0; o.n_tokens = s.n;
+        o.text = (char*)malloc(s.text.size() + 1);
+        if (!o.text) { spt_result_free(r); return nullptr; }
+        memcpy(o.text, s.text.c_str(), s.text.size() + 1);
+    }
+    return r;
+}
+
+// whisper_full (full.cpp) over host utterances
+spt_status run_full(spt_ctx* c, const float* const* pcm, const size_t* n_samples, size_t batch,
+                    const spt_infer_params* p, spt_result** out) {
+    if (p->beam_size > 1) return fail(c, SPT_ERR_UNSUPPORTED, "beam search is not implemented (greedy only)");
+    if (p->forced_tokens || (p->flags & SPT_IGNORE_EOT))
+        return fail(c, SPT_ERR_INVALID_ARG, "forced tokens / SPT_IGNORE_EOT are fast-path (no-timestamp) hooks");
+    if ((p->flags & SPT_SUPPRESS_NST) && !c->vocab)
+        return fail(c, SPT_ERR_UNSUPPORTED, "suppressing non-speech tokens needs the vocabulary of a ggml model");
+    if (p->temperature < 0.0f || p->temperature_inc < 0.0f) return fail(c, SPT_ERR_INVALID_ARG, "negative temperature");
+    std::vector<int32_t> ptoks;
+    spt_status st = prompt_tokens_of(c, p, &ptoks);
+    if (st != SPT_OK) return st;
+    int lang_tok;
+    st = lang_of(c, p, &lang_tok);
+    if (st != SPT_OK) return st;
+    spt::FullParams fp;
+    fp.no_timestamps = (p->flags & SPT_NO_TIMESTAMPS) != 0;
+    fp.suppress_blank = (p->flags & SPT_SUPPRESS_BLANK) != 0;
+    fp.suppress_nst = (p->flags & SPT_SUPPRESS_NST) != 0;
+    fp.translate = p->translate != 0;
+    fp.temperature = p->temperature;
+    fp.temperature_inc = p->temperature_inc;
+    fp.best_of = p->best_of > 0 ? p->best_of : 5;
+    fp.entropy_thold = p->entropy_thold;
+    fp.logprob_thold = p->logprob_thold;
+    fp.max_initial_ts = p->max_initial_ts;
+    fp.max_tokens = std::max(0, p->max_new_tokens);
+    fp.seed = p->seed;
+    std::vector<const float*> ptr(batch);
+    std::vector<int> ns(batch);
+    for (size_t u = 0; u < batch; ++u) {
+        if (n_samples[u] > (size_t)INT32_MAX / 2) return fail(c, SPT_ERR_INVALID_ARG, "utterance too long");
+        ptr[u] = pcm[u];
+        ns[u] = (int)n_samples[u];
+    }
+    const spt::Specials sp = spt::specials_for(c->eng->dims().n_vocab);
+    std::vector<spt::FullResult> res;
+    spt::whisper_full_batch(*c->eng, c->vocab.get(), ptr, ns, fp, std::vector<int>(ptoks.begin(), ptoks.end()),
+                            lang_tok >= 0 ? lang_tok : -1, &res);
+    for (size_t u = 0; u < batch; ++u) {
+        out[u] = make_full_result(res[u], sp);
+        if (!out[u]) {
+            for (size_t v = 0; v < u; ++v) { spt_result_free(out[v]); out[v] = nullptr; }
+            return fail(c, SPT_ERR_OOM, "host allocation failed");
+        }
+    }
+    return SPT_OK;
 }
 
 // shared driver: windows (device or host) -> per-utterance results
@@ -227,7 +330,7 @@ spt_status run_windows(spt_ctx* c, std::vector<Window>& win, size_t n_utt, const
 
 extern "C" {
 
-const char* spt_version(void) { return "spittle_amd 0.3.0 (gfx950, ABI 2)"; }
+const char* spt_version(void) { return "spittle_amd 0.4.0 (gfx950, ABI 3)"; }
 
 const char* spt_language_code(int32_t lang_id) { return spt::lang_code(lang_id); }
 
@@ -244,10 +347,15 @@ void spt_default_infer_params(spt_infer_params* p) {
     if (!p) return;
     memset(p, 0, sizeof(*p));
     p->language = "en";
-    p->flags = SPT_SUPPRESS_BLANK | SPT_NO_TIMESTAMPS;
+    p->flags = SPT_SUPPRESS_BLANK;  // whisper_full_default_params: timestamps on
     p->max_new_tokens = 220;
     p->temperature = 0.0f;
     p->beam_size = 1;
+    p->temperature_inc = 0.2f;
+    p->best_of = 5;
+    p->entropy_thold = 2.4f;
+    p->logprob_thold = -1.0f;
+    p->max_initial_ts = 1.0f;
 }
 
 spt_status spt_ctx_create(const char* model_spec, const spt_model_params* params, spt_ctx** out, char* err,
@@ -332,6 +440,20 @@ spt_status spt_ctx_info(const spt_ctx* ctx, spt_model_info* info) {
 spt_status spt_transcribe_batch(spt_ctx* ctx, const float* const* pcm, const size_t* n_samples, size_t batch,
                                 const spt_infer_params* params, spt_result** out) {
     if (!ctx || !out || (batch && (!pcm || !n_samples))) return fail(ctx, SPT_ERR_INVALID_ARG, "null argument");
+    spt_infer_params dflt;
+    spt_default_infer_params(&dflt);
+    if (!params) params = &dflt;
+    if (full_mode(params)) {
+        for (size_t u = 0; u < batch; ++u) {
+            out[u] = nullptr;
+            if (n_samples[u] && !pcm[u]) return fail(ctx, SPT_ERR_INVALID_ARG, "null pcm");
+        }
+        try {
+            return batch ? run_full(ctx, pcm, n_samples, batch, params, out) : SPT_OK;
+        } catch (const std::exception& e) {
+            return fail(ctx, classify(e), e.what());
+        }
+    }
     std::vector<Window> win;
     std::vector<size_t> empty;
     for (size_t u = 0; u < batch; ++u) {
@@ -374,6 +496,9 @@ spt_status spt_transcribe_batch_device(spt_ctx* ctx, const float* pcm_dev, size_
     if (!ctx || !out || !pcm_dev || !n_samples || batch == 0) return fail(ctx, SPT_ERR_INVALID_ARG, "null argument");
     if (batch > (size_t)ctx->eng->max_batch()) return fail(ctx, SPT_ERR_INVALID_ARG, "batch exceeds max_batch");
     if (stride < (size_t)kWindow) return fail(ctx, SPT_ERR_INVALID_ARG, "device stride must be >= 480000");
+    if (params && full_mode(params))
+        return fail(ctx, SPT_ERR_UNSUPPORTED,
+                    "device windows take the no-timestamp greedy protocol (SPT_NO_TIMESTAMPS, temperature_inc 0)");
     spt::DecodeRequest rq;
     bool autolang = false;
     spt_status s = build_request(ctx, params, &rq, &autolang);
@@ -416,6 +541,8 @@ spt_status spt_transcribe_batch_device(spt_ctx* ctx, const float* pcm_dev, size_
 
 void spt_result_free(spt_result* r) {
     if (!r) return;
+    for (int32_t i = 0; i < r->n_segments && r->segments; ++i) free(r->segments[i].text);
+    free(r->segments);
     free(r->text);
     free(r->tokens);
     free(r->top1);

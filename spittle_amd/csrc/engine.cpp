@@ -562,6 +562,10 @@ void Engine::alloc_workspace() {
             g.dx2 = (float*)c.take(R * d * 4);
             g.pend = (float*)c.take((int64_t)kMaxPend * R * d * 4);
             g.xpart = (float*)c.take((int64_t)R * dm_.n_head * 4 * 66 * 4);
+            g.seek = (int*)c.take(B * 4);
+            g.seek_end = (int*)c.take(B * 4);
+            g.ts_state = (int*)c.take(B * 16);
+            g.prm = (TsParams*)c.take(sizeof(TsParams));
         }
         zero_ = (float*)c.take(R * d * 4);  // never written: the "no pending slab" operand
         if (!pass) {
@@ -739,6 +743,19 @@ void Engine::enqueue_head(DecGroup& g, int Tq, const DecodeRequest& rq, int out_
     a.blank1 = blank ? 220 : -1;
     a.part = g.part; a.n_tiles = n_tiles;
     gemv(dt_, GV_LOGITS, A_LN, a, st);
+    if (rq.full) {
+        TsArgs t{};
+        t.logits = g.logits; t.ldl = dm_.n_vocab;
+        t.n_vocab = dm_.n_vocab; t.eot = sp.eot; t.beg = sp.beg; t.blank = rq.blank_tok;
+        t.suppress = sup; t.prm = g.prm; t.seek = g.seek; t.seek_end = g.seek_end; t.state = g.ts_state;
+        t.forced = rq.n_forced > 0 ? g.forced : nullptr; t.forced_len = rq.n_forced;
+        t.next_tok = g.tok_in; t.out_tok = g.out_tok; t.out_plog = g.out_t1; t.out_tid = g.out_t2; t.out_cap = out_cap;
+        t.done = g.done;
+        t.emb = tok_emb_; t.pos = dec_pos_; t.d = d; t.ctx = ctx; t.Tq = Tq; t.x = g.dx;
+        t.ds = g.ds; t.arrive = g.arrive;
+        dec_finalize_ts(dt_, t, B, st);
+        return;
+    }
     FinalizeArgs f{};
     f.part = g.part; f.n_tiles = n_tiles;
     f.eot = sp.eot; f.ignore_eot = (rq.flags & 4u) ? 1 : 0; f.n_vocab = dm_.n_vocab;
@@ -750,10 +767,11 @@ void Engine::enqueue_head(DecGroup& g, int Tq, const DecodeRequest& rq, int out_
     dec_finalize(dt_, f, B, st);
 }
 
-void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1, float* top2, int* lang_out) {
+void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1, float* top2, int* lang_out,
+                        int* ts_state_out) {
     const int Tq = (int)rq.prompt.size();
     const int ctx = dm_.n_text_ctx;
-    const int P = (int)rq.prefix.size();
+    const int P = rq.row_prefix.empty() ? (int)rq.prefix.size() : (int)rq.row_prefix[0].size();
     if (Tq < 1 || Tq > 4) throw std::runtime_error("prompt must have 1..4 tokens");
     if (B * Tq > 64) throw std::runtime_error("batch x prompt rows exceed 64");
     if (P > ctx / 2 + 1) throw std::runtime_error("prompt prefix longer than n_text_ctx / 2 + 1");
@@ -765,20 +783,33 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
     if (rq.n_forced > ctx) throw std::runtime_error("too many forced tokens");
     const int out_cap = rq.n_steps;
     const Specials sp = specials_for(dm_.n_vocab);
-    // always-suppressed ids (whisper_process_logits, no-timestamp greedy subset)
-    const uint32_t sflags = rq.flags & 2u;
-    if (suppress_flags_ != sflags) {
+    // always-suppressed ids (whisper_process_logits); the fast path also masks the timestamps
+    // here, the whisper_full path applies its timestamp rules per step (k_sample.hip)
+    const uint32_t sflags = (rq.flags & 2u) | (rq.full ? 0x100u : 0u);
+    if (suppress_flags_ != sflags || suppress_extra_ != rq.extra_suppress) {
         const int V = dm_.n_vocab;
         host_suppress_.assign(V / 32 + 1, 0u);
         auto set = [&](int i) { if (i >= 0 && i < V) host_suppress_[i >> 5] |= 1u << (i & 31); };
         set(sp.not_);
-        if (rq.flags & 2u)
+        if ((rq.flags & 2u) && !rq.full)
             for (int i = sp.beg; i < V; ++i) set(i);
         set(sp.sot); set(sp.nosp); set(sp.solm); set(sp.translate); set(sp.transcribe); set(sp.prev);
         for (int i = 0; i < sp.n_langs; ++i) set(sp.sot + 1 + i);
+        for (int i : rq.extra_suppress) set(i);
         HIP_CHECK(hipMemcpyAsync(suppress_, host_suppress_.data(), host_suppress_.size() * 4, hipMemcpyHostToDevice, st_));
         HIP_CHECK(hipStreamSynchronize(st_));
         suppress_flags_ = sflags;
+        suppress_extra_ = rq.extra_suppress;
+    }
+    if (rq.full && ((int)rq.seek.size() != B || (int)rq.seek_end.size() != B))
+        throw std::runtime_error("whisper_full decoding needs seek / seek_end per sequence");
+    if (!rq.row_prefix.empty()) {
+        if ((int)rq.row_prefix.size() != B) throw std::runtime_error("row_prefix needs one prefix per sequence");
+        for (const auto& r : rq.row_prefix) {
+            if (r.size() != rq.row_prefix[0].size()) throw std::runtime_error("row prefixes must have equal lengths");
+            for (int t : r)
+                if (t < 0 || t >= dm_.n_vocab) throw std::runtime_error("prompt token out of the vocabulary");
+        }
     }
     // split the batch over the decode groups; each waits for the encoder / cross-K/V
     const int G = std::min(n_groups_, B);
@@ -792,11 +823,16 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         act.push_back(&g);
         HIP_CHECK(hipStreamWaitEvent(g.st, ev_[6], 0));
         // host sources of this call's token uploads (kept alive in the group until the next call)
-        g.host_tok.assign((size_t)g.B * (1 + 4 * ((rq.prefix.size() + 3) / 4 + 1)), 0);
+        g.host_tok.assign((size_t)g.B * (1 + 4 * ((P + 3) / 4 + 1)), 0);
         g.host_used = 0;
         if (rq.n_forced > 0)
             HIP_CHECK(hipMemcpyAsync(g.forced, rq.forced + (size_t)g.b0 * rq.n_forced, (size_t)g.B * rq.n_forced * 4,
                                      hipMemcpyHostToDevice, g.st));
+        if (rq.full) {  // pageable sources: copied before the call returns
+            HIP_CHECK(hipMemcpyAsync(g.seek, rq.seek.data() + g.b0, g.B * 4, hipMemcpyHostToDevice, g.st));
+            HIP_CHECK(hipMemcpyAsync(g.seek_end, rq.seek_end.data() + g.b0, g.B * 4, hipMemcpyHostToDevice, g.st));
+            HIP_CHECK(hipMemcpyAsync(g.prm, &rq.ts, sizeof(TsParams), hipMemcpyHostToDevice, g.st));
+        }
     }
     auto upload_tokens = [&](DecGroup& g, const std::function<int(int, int)>& tok, int n) {  // [g.B][n]
         int* h = g.host_tok.data() + g.host_used;
@@ -805,12 +841,17 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         g.host_used += g.B * n;
         HIP_CHECK(hipMemcpyAsync(g.tok_in, h, (size_t)g.B * n * 4, hipMemcpyHostToDevice, g.st));
     };
+    ts_init_.clear();  // a member: the source of asynchronous copies outlives this function
+    for (int b = 0; b < B; ++b) ts_init_.insert(ts_init_.end(), {0, 3000, 0, 0});
     auto reset_outputs = [&](DecGroup& g) {
         HIP_CHECK(hipMemsetAsync(g.done, 0, g.B * 4, g.st));
         HIP_CHECK(hipMemsetAsync(g.out_tok, 0xFF, (size_t)g.B * out_cap * 4, g.st));
         fill_f32(g.out_t1, (int64_t)g.B * out_cap, -INFINITY, g.st);
         fill_f32(g.out_t2, (int64_t)g.B * out_cap, -INFINITY, g.st);
         dec_reset(g.ds, g.arrive, g.st);
+        if (rq.full)  // WHISPER_DECODER_INIT: seek_delta starts at a whole window (3000 frames)
+            HIP_CHECK(hipMemcpyAsync(g.ts_state, ts_init_.data() + (size_t)g.b0 * 4, g.B * 16, hipMemcpyHostToDevice,
+                                     g.st));
     };
     // language auto-detection (whisper_lang_auto_detect_with_state): one pass on [sot] with every
     // non-language token suppressed; the argmax is the language token
@@ -826,7 +867,7 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
             HIP_CHECK(hipMemcpy(suppress_lang_, m.data(), m.size() * 4, hipMemcpyHostToDevice));
             suppress_lang_ready_ = true;
         }
-        DecodeRequest dq;  // no forcing, no blank rule, EOT irrelevant
+        DecodeRequest dq;  // no forcing, no blank rule, EOT irrelevant; the fast head
         dq.flags = 4u;
         for (DecGroup* g : act) {
             reset_outputs(*g);
@@ -856,10 +897,11 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         reset_outputs(g);
         // whisper_full prompt_past ([prev] + prompt tokens): prefilled in chunks of <= 4 rows per
         // sequence through the decoder layers only (no logits), positions 0..P-1
-        const int P = (int)rq.prefix.size();
+        const bool rows = !rq.row_prefix.empty();
+        const int P = rows ? (int)rq.row_prefix[0].size() : (int)rq.prefix.size();
         for (int c0 = 0; c0 < P; c0 += 4) {
             const int n = std::min(4, P - c0);
-            upload_tokens(g, [&](int, int t) { return rq.prefix[c0 + t]; }, n);
+            upload_tokens(g, [&](int b, int t) { return rows ? rq.row_prefix[b][c0 + t] : rq.prefix[c0 + t]; }, n);
             dec_embed(dt_, g.tok_in, g.B * n, n, dm_.d, tok_emb_, dec_pos_, g.ds, g.dx, g.st);
             enqueue_layers(g, B, n);
             dec_advance(g.ds, n, g.st);
@@ -886,7 +928,7 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
     } else if (rq.n_steps > 1) {
         std::vector<hipGraphExec_t> ex;
         for (DecGroup* g : act) {
-            const GraphKey key{g->B, out_cap, rq.n_forced, rq.flags};
+            const GraphKey key{g->B, out_cap, rq.n_forced, rq.flags, rq.full};
             auto it = g->graphs.find(key);
             if (it == g->graphs.end()) {
                 hipGraph_t graph;
@@ -922,13 +964,17 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         HIP_CHECK(hipMemcpyAsync(tokens + off, g->out_tok, n, hipMemcpyDeviceToHost, g->st));
         if (top1) HIP_CHECK(hipMemcpyAsync(top1 + off, g->out_t1, n, hipMemcpyDeviceToHost, g->st));
         if (top2) HIP_CHECK(hipMemcpyAsync(top2 + off, g->out_t2, n, hipMemcpyDeviceToHost, g->st));
+        if (ts_state_out && rq.full)
+            HIP_CHECK(hipMemcpyAsync(ts_state_out + (size_t)g->b0 * 4, g->ts_state, (size_t)g->B * 16,
+                                     hipMemcpyDeviceToHost, g->st));
         HIP_CHECK(hipEventRecord(g->ev, g->st));
         HIP_CHECK(hipStreamWaitEvent(st_, g->ev, 0));
     }
 }
 
 void Engine::transcribe_device(const float* pcm_dev, int64_t stride, const int* n_samples, int B,
-                               const DecodeRequest& rq, int* tokens, float* top1, float* top2, int* lang_out) {
+                               const DecodeRequest& rq, int* tokens, float* top1, float* top2, int* lang_out,
+                               int* ts_state_out) {
     select();
     if (B < 1 || B > max_batch_) throw std::runtime_error("batch exceeds the context's max_batch");
     for (int b = 0; b < B; ++b)
@@ -943,7 +989,7 @@ void Engine::transcribe_device(const float* pcm_dev, int64_t stride, const int* 
     HIP_CHECK(hipEventRecord(ev_[3], st_));
     run_cross_kv(B);
     HIP_CHECK(hipEventRecord(ev_[4], st_));
-    run_decode(B, rq, tokens, top1, top2, lang_out);
+    run_decode(B, rq, tokens, top1, top2, lang_out, ts_state_out);
     HIP_CHECK(hipEventRecord(ev_[5], st_));
     HIP_CHECK(hipStreamSynchronize(st_));
     HIP_CHECK(hipGetLastError());
@@ -973,11 +1019,11 @@ void Engine::stage_pcm(const float* const* pcm, const int* n, int B) {
 }
 
 void Engine::transcribe_host(const float* const* pcm, const int* n_samples, int B, const DecodeRequest& rq,
-                             int* tokens, float* top1, float* top2, int* lang_out) {
+                             int* tokens, float* top1, float* top2, int* lang_out, int* ts_state_out) {
     select();
     if (B < 1 || B > max_batch_) throw std::runtime_error("batch exceeds the context's max_batch");
     stage_pcm(pcm, n_samples, B);
-    transcribe_device(pcm_, 480000, n_samples, B, rq, tokens, top1, top2, lang_out);
+    transcribe_device(pcm_, 480000, n_samples, B, rq, tokens, top1, top2, lang_out, ts_state_out);
 }
 
 // ----------------------------------------------------------------------------- debug hooks

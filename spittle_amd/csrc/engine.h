@@ -37,6 +37,15 @@ struct DecodeRequest {
     uint32_t flags = 3;         // SUPPRESS_BLANK | NO_TIMESTAMPS
     const int32_t* forced = nullptr;
     int n_forced = 0;
+    // whisper_full decoding (k_sample.hip): timestamps, temperature sampling, per-decoder
+    // bookkeeping.  Off: the no-timestamp greedy fast path.  On: tokens as usual, top1 = the
+    // token's log-probability (plog), top2 = its timestamp id (tid, as a float).
+    bool full = false;
+    TsParams ts{};
+    std::vector<int> seek, seek_end;           // [B] 10 ms frames
+    std::vector<std::vector<int>> row_prefix;  // per-sequence prompt_past (equal lengths); else prefix
+    std::vector<int> extra_suppress;           // e.g. the non-speech tokens of the vocabulary
+    int blank_tok = 220;                       // " " (suppress_blank)
 };
 
 struct Timings {
@@ -63,11 +72,13 @@ public:
     // pcm_dev: B windows of <= 480000 samples at pcm_dev + b * stride (device memory)
     // tokens/top1/top2: host [B][n_steps]
     // lang_out (optional, [B]): the language token each sequence was decoded with (-1: none)
+    // ts_state_out (optional, [B][4], whisper_full mode): has_ts, seek_delta, result_len, status
+    // (0 running, 1 completed, 2 failed) of each sequence's decoder
     void transcribe_device(const float* pcm_dev, int64_t stride, const int* n_samples, int B, const DecodeRequest& rq,
-                           int* tokens, float* top1, float* top2, int* lang_out = nullptr);
+                           int* tokens, float* top1, float* top2, int* lang_out = nullptr, int* ts_state_out = nullptr);
     // host PCM convenience (stages into the engine's pcm buffer)
     void transcribe_host(const float* const* pcm, const int* n_samples, int B, const DecodeRequest& rq, int* tokens,
-                         float* top1, float* top2, int* lang_out = nullptr);
+                         float* top1, float* top2, int* lang_out = nullptr, int* ts_state_out = nullptr);
 
     void debug_mel(const float* pcm_host, int n, float* out_host);
     void debug_encode(const float* mel_host, float* out_host);
@@ -79,7 +90,9 @@ private:
     struct GraphKey {
         int B, out_cap, n_forced;
         uint32_t flags;
+        bool full;
         bool operator<(const GraphKey& o) const {
+            if (full != o.full) return full < o.full;
             if (B != o.B) return B < o.B;
             if (out_cap != o.out_cap) return out_cap < o.out_cap;
             if (n_forced != o.n_forced) return n_forced < o.n_forced;
@@ -104,6 +117,8 @@ private:
         float* dx2 = nullptr;         // second residual buffer (ping-pong with dx)
         float* pend = nullptr;        // pending partial slabs [kMaxPend][R][d]
         float* xpart = nullptr;       // cross-attention chunk partials [R][H][<=4][66]
+        int *seek = nullptr, *seek_end = nullptr, *ts_state = nullptr;  // whisper_full decoding
+        TsParams* prm = nullptr;
         std::map<GraphKey, hipGraphExec_t> graphs;
         std::vector<int> host_tok;    // host sources of the call's token uploads
         size_t host_used = 0;
@@ -120,7 +135,8 @@ private:
     void run_mel(const float* pcm_dev, int64_t stride, int B, float* dbg);
     void run_encoder(int B);
     void run_cross_kv(int B);
-    void run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1, float* top2, int* lang_out);
+    void run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1, float* top2, int* lang_out,
+                    int* ts_state_out);
     void enqueue_decoder_pass(DecGroup& g, int B_total, int Tq, const DecodeRequest& rq, int out_cap);
     float* enqueue_layers(DecGroup& g, int B_total, int Tq);
     void enqueue_head(DecGroup& g, int Tq, const DecodeRequest& rq, int out_cap, float* xc, const uint32_t* sup,
@@ -177,6 +193,8 @@ private:
 
     std::vector<uint32_t> host_suppress_;
     uint32_t suppress_flags_ = ~0u;
+    std::vector<int> suppress_extra_;
+    std::vector<int> ts_init_;
 
     Timings tm_;
 };

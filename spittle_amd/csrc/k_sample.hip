@@ -1,0 +1,245 @@
+// k_sample.hip -- whisper_full's token selection for the timestamp / temperature decode
+// (the no-timestamp greedy protocol keeps the top-2 partial path of k_dec.hip).
+//
+// One 1024-thread workgroup per sequence reads that sequence's logits row (L2-resident, just
+// written by the logits GEMV) and restates whisper.cpp (~1.7.x, whisper-rs-sys 0.11.1;
+// /root/reference/src-tauri/Cargo.lock:8156-8174, not vendored):
+//   whisper_process_logits: logits / temperature; the static suppression mask (sot, nosp,
+//     solm, task, prev, language and optionally non-speech tokens, [not], and every timestamp
+//     under no_timestamps); [eot] and " " at the first step (suppress_blank); timestamps in
+//     pairs (after a timestamp that follows a timestamp no timestamp may come; after a lone
+//     one only a timestamp or [eot]); the first timestamp <= max_initial_ts; timestamps never
+//     before the last one (has_ts: tid < seek_delta / 2 masked); log-softmax; "if the summed
+//     probability of the timestamps beats every text token, sample a timestamp".
+//   whisper_sample_token: greedy = first maximum; temperature > 0 = a draw from the softmax
+//     (a counter-based stream per (seed, sequence, step) replaces std::mt19937 +
+//     std::discrete_distribution: the distribution is the same, the draws are not); plog =
+//     the chosen token's log-probability before the timestamp rule's text mask; tid = the
+//     most probable timestamp (the token itself when it is one).
+//   whisper_full's per-token bookkeeping of one decoder: seek_delta / result_len / has_ts on
+//     timestamps (failed when time would run backwards), end of segment on [eot], max_tokens
+//     or the end of the audio (failed when no timestamp was produced), no_timestamps
+//     completion (result_len = i + 1, seek_delta = 3000), and the repetition guard at
+//     i == n_max - 1.
+// The chosen (or forced) token is embedded for the next pass and the step advanced exactly
+// as dec_finalize does.
+#include "common.h"
+#include "kernels.h"
+
+namespace spt {
+
+namespace {
+
+constexpr int TW = 1024;  // threads per sequence
+
+__device__ __forceinline__ float u01(uint64_t seed, int b, int step) {
+    uint64_t z = seed * 0x9E3779B97F4A7C15ULL + ((uint64_t)b << 32) + (uint64_t)step + 0x632BE59BD9B4E019ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z ^= z >> 31;
+    return (float)(uint32_t)(z >> 40) * (1.0f / 16777216.0f);  // [0, 1)
+}
+
+struct MaxI { float v; int i; };
+__device__ __forceinline__ MaxI max_merge(MaxI a, MaxI b) {
+    return (b.v > a.v || (b.v == a.v && b.i < a.i)) ? b : a;
+}
+
+template <typename T>
+__global__ __launch_bounds__(TW) void finalize_ts_kernel(TsArgs a) {
+    __shared__ MaxI s_m[2][TW / 64];
+    __shared__ float s_s[2][TW / 64];
+    __shared__ float s_scan[TW];
+    __shared__ int s_pick, s_tok;
+    __shared__ float s_bc[4];  // M_all, LSE_all, M_after, ts_rule
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int step = a.ds->step;
+    const TsParams& P = *a.prm;
+    const int V = a.n_vocab, beg = a.beg, eot = a.eot;
+    const float* lg = a.logits + (size_t)b * a.ldl;
+    int* S = a.state + 4 * b;  // has_ts, seek_delta, result_len, status (0 run, 1 done, 2 failed)
+    const bool live = step < a.out_cap && !a.done[b];
+    if (live) {
+        const int oi0 = b * a.out_cap;
+        const int last = step > 0 ? a.out_tok[oi0 + step - 1] : -1;
+        const int pen = step > 1 ? a.out_tok[oi0 + step - 2] : -1;
+        const bool last_ts = step > 0 && last >= beg;
+        const bool pen_ts = step < 2 || pen >= beg;
+        const int has_ts = S[0], seek_delta = S[1];
+        auto masked = [&](int n) -> bool {
+            if ((a.suppress[n >> 5] >> (n & 31)) & 1u) return true;
+            if (step == 0 && P.suppress_blank && (n == eot || n == a.blank)) return true;
+            if (n >= beg) {
+                if (P.no_ts) return true;
+                if (last_ts && pen_ts) return true;
+                if (step == 0 && P.max_initial >= 0 && n > beg + P.max_initial) return true;
+                if (has_ts && n < beg + seek_delta / 2) return true;
+            } else if (n < eot && last_ts && !pen_ts) {
+                return true;
+            }
+            return false;
+        };
+        auto val = [&](int n) { return P.temperature > 0.0f ? lg[n] / P.temperature : lg[n]; };
+        // pass 1: maxima (first index on ties) of the text [0, beg) and timestamp [beg, V) ranges
+        MaxI mt{-INFINITY, 0x7fffffff}, ms{-INFINITY, 0x7fffffff};
+        for (int n = tid; n < V; n += TW) {
+            if (masked(n)) continue;
+            const MaxI c{val(n), n};
+            if (n < beg) mt = max_merge(mt, c);
+            else ms = max_merge(ms, c);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            mt = max_merge(mt, MaxI{__shfl_xor(mt.v, o, 64), __shfl_xor(mt.i, o, 64)});
+            ms = max_merge(ms, MaxI{__shfl_xor(ms.v, o, 64), __shfl_xor(ms.i, o, 64)});
+        }
+        if (lane == 0) { s_m[0][wv] = mt; s_m[1][wv] = ms; }
+        __syncthreads();
+        mt = s_m[0][0];
+        ms = s_m[1][0];
+        for (int w = 1; w < TW / 64; ++w) { mt = max_merge(mt, s_m[0][w]); ms = max_merge(ms, s_m[1][w]); }
+        const float M = fmaxf(mt.v, ms.v);
+        // pass 2: sum exp over everything unmasked (log-softmax) and over the timestamps
+        float sa = 0.0f, st = 0.0f;
+        if (M > -INFINITY)
+            for (int n = tid; n < V; n += TW) {
+                if (masked(n)) continue;
+                const float v = val(n);
+                sa += expf(v - M);
+                if (n >= beg) st += expf(v - ms.v);
+            }
+        sa = wave_sum(sa);
+        st = wave_sum(st);
+        if (lane == 0) { s_s[0][wv] = sa; s_s[1][wv] = st; }
+        __syncthreads();
+        if (tid == 0) {
+            float za = 0.0f, zt = 0.0f;
+            for (int w = 0; w < TW / 64; ++w) { za += s_s[0][w]; zt += s_s[1][w]; }
+            const float lse = logf(za) + M;
+            // timestamp_logprob > max_text_token_logprob (both relative to the same LSE)
+            const float ts_lp = zt > 0.0f ? logf(zt) + ms.v - lse : -INFINITY;
+            const float tx_lp = mt.v - lse;
+            const bool rule = ms.v > -INFINITY && ts_lp > tx_lp;
+            s_bc[0] = M;
+            s_bc[1] = lse;
+            s_bc[2] = rule ? ms.v : M;
+            s_bc[3] = rule ? 1.0f : 0.0f;
+            int pick;
+            if (rule) pick = ms.i;
+            else pick = (ms.v > mt.v) ? ms.i : mt.i;
+            s_pick = M > -INFINITY ? pick : -2;
+        }
+        __syncthreads();
+        if (P.temperature > 0.0f && s_pick >= 0) {
+            // a draw from softmax over what survived the timestamp rule: contiguous chunks, a
+            // block scan of their sums, then one thread walks the chunk the draw lands in
+            const bool rule = s_bc[3] != 0.0f;
+            const float M2 = s_bc[2];
+            const int C = (V + TW - 1) / TW, n0 = tid * C, n1 = min(V, n0 + C);
+            float z = 0.0f;
+            for (int n = n0; n < n1; ++n)
+                if (!masked(n) && !(rule && n < beg)) z += expf(val(n) - M2);
+            s_scan[tid] = z;
+            __syncthreads();
+            for (int o = 1; o < TW; o <<= 1) {  // inclusive Hillis-Steele scan
+                const float add = tid >= o ? s_scan[tid - o] : 0.0f;
+                __syncthreads();
+                s_scan[tid] += add;
+                __syncthreads();
+            }
+            const float total = s_scan[TW - 1];
+            const float u = u01(P.seed, b, step) * total;
+            const float lo = tid ? s_scan[tid - 1] : 0.0f, hi = s_scan[tid];
+            if (total > 0.0f && u >= lo && (u < hi || tid == TW - 1)) {
+                float c = lo;
+                int last_ok = -1;
+                for (int n = n0; n < n1; ++n) {
+                    if (masked(n) || (rule && n < beg)) continue;
+                    last_ok = n;
+                    c += expf(val(n) - M2);
+                    if (u < c) break;
+                }
+                if (last_ok >= 0) s_pick = last_ok;
+            }
+            __syncthreads();
+        }
+        if (tid == 0) {
+            const int oi = oi0 + step;
+            int tok = s_pick;
+            if (tok < 0 || tok >= V) {  // every logit masked or non-finite: the sequence fails
+                a.out_tok[oi] = -2;
+                a.out_plog[oi] = __builtin_nanf("");
+                a.out_tid[oi] = 0.0f;
+                S[3] = 2;
+                a.done[b] = 1;
+            } else {
+                const float plog = val(tok) - s_bc[1];
+                int tid_ts = tok >= beg ? tok : (ms.v > -INFINITY ? ms.i : 0);
+                a.out_tok[oi] = tok;
+                a.out_plog[oi] = plog;
+                a.out_tid[oi] = (float)tid_ts;  // exact: ids < 2^24
+                // whisper_full: one decoder's bookkeeping for token i = step
+                const int i = step;
+                int hts = S[0], sd = S[1], rl = S[2], status = 0;
+                const int seek = a.seek[b], seek_end = a.seek_end[b];
+                if (tok > beg) {
+                    const int sdn = 2 * (tok - beg);
+                    if (hts && sd > sdn && rl < i) status = 2;  // time would run backwards
+                    else { sd = sdn; rl = i + 1; hts = 1; }
+                }
+                if (status == 0 && (tok == eot || (P.max_tokens > 0 && i >= P.max_tokens) ||
+                                    (hts && seek + sd + 100 >= seek_end))) {
+                    if (rl == 0 && !P.no_ts) {
+                        if (seek + sd + 100 >= seek_end) rl = i + 1;
+                        else status = 2;
+                    }
+                    if (status == 0) {
+                        if (P.no_ts) { rl = i + 1; sd = 3000; }
+                        status = 1;
+                    }
+                }
+                if (status == 0 && i == P.n_max - 1 && (rl == 0 || sd < 1500)) status = 2;  // repetition guard
+                S[0] = hts; S[1] = sd; S[2] = rl; S[3] = status;
+                if (status != 0) a.done[b] = 1;
+            }
+        }
+    } else if (tid == 0 && step < a.out_cap) {
+        const int oi = b * a.out_cap + step;
+        a.out_tok[oi] = -1;
+        a.out_plog[oi] = -INFINITY;
+        a.out_tid[oi] = -1.0f;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int nxt = (live && step < a.out_cap) ? a.out_tok[b * a.out_cap + step] : eot;
+        if (live && a.forced && step < a.forced_len) nxt = a.forced[b * a.forced_len + step];
+        if (nxt < 0 || nxt >= V) nxt = eot;
+        a.next_tok[b] = nxt;
+        s_tok = nxt;
+    }
+    __syncthreads();
+    const int tok = s_tok;
+    const int pos0 = a.ds->pos0;
+    const int pn = min(pos0 + a.Tq, a.ctx - 1);
+    const T* e = (const T*)a.emb + (size_t)tok * a.d;
+    const float* pp = a.pos + (size_t)pn * a.d;
+    for (int i = tid; i < a.d; i += TW) a.x[(size_t)b * a.d + i] = to_f<T>(e[i]) + pp[i];
+    if (tid == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == (unsigned)gridDim.x - 1) {
+            a.ds->pos0 = pos0 + a.Tq;
+            a.ds->step = step + 1;
+            __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+}  // namespace
+
+void dec_finalize_ts(int dtype, const TsArgs& a, int B, hipStream_t st) {
+    if (dtype == DT_BF16) hipLaunchKernelGGL(finalize_ts_kernel<bf16>, dim3(B), dim3(TW), 0, st, a);
+    else hipLaunchKernelGGL(finalize_ts_kernel<float>, dim3(B), dim3(TW), 0, st, a);
+    SPT_LAUNCH_CHECK();
+}
+
+}  // namespace spt

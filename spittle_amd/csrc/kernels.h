@@ -126,6 +126,34 @@ struct FinalizeArgs {
 // argmax reduce + record + next-token embed + step advance (replaces embed/argmax/advance)
 void dec_finalize(int dtype, const FinalizeArgs& a, int B, hipStream_t st);
 void dec_reset(DecState* ds, unsigned* arrive, hipStream_t st);
+
+// whisper_full decoding parameters of one call (device memory: read by graph-captured launches)
+struct TsParams {
+    float temperature;    // 0: greedy
+    int suppress_blank;   // [eot] and " " at the first step
+    int no_ts;            // no_timestamps: every timestamp token suppressed
+    int max_initial;      // first timestamp <= beg + max_initial (round(max_initial_ts / 0.02)); < 0 off
+    int n_max;            // steps per window (n_text_ctx / 2 - 4): the repetition guard
+    int max_tokens;       // > 0: end the segment after this many tokens
+    unsigned long long seed;
+};
+struct TsArgs {
+    const float* logits; int ldl;        // [B][ldl] raw logits of this step
+    int n_vocab, eot, beg, blank;        // blank: the " " token
+    const uint32_t* suppress;            // static suppression bits
+    const TsParams* prm;
+    const int* seek; const int* seek_end;  // [B] window start / audio end, 10 ms frames
+    int* state;                          // [B][4] has_ts, seek_delta, result_len, status
+    const int* forced; int forced_len;
+    int* next_tok;
+    int* out_tok; float* out_plog; float* out_tid; int out_cap;  // [B][out_cap]
+    int* done;
+    const void* emb; const float* pos; int d, ctx, Tq;
+    float* x;
+    DecState* ds; unsigned* arrive;
+};
+// whisper_process_logits + whisper_sample_token + per-decoder bookkeeping (k_sample.hip)
+void dec_finalize_ts(int dtype, const TsArgs& a, int B, hipStream_t st);
 // pos0 += n (after a prefill pass that produces no token)
 void dec_advance(DecState* ds, int n, hipStream_t st);
 

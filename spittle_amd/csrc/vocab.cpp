@@ -36,6 +36,11 @@ const std::string& Vocab::str(int id) const {
     return (id >= 0 && id < (int)id_to_tok_.size()) ? id_to_tok_[id] : empty;
 }
 
+int Vocab::id(const std::string& tok) const {
+    auto it = tok_to_id_.find(tok);
+    return it == tok_to_id_.end() ? -1 : it->second;
+}
+
 std::vector<int> Vocab::tokenize(const std::string& text, int* n_unknown) const {
     // GPT-2's pre-tokenisation pattern as whisper.cpp states it for std::regex (ECMAScript,
     // "C" locale classes: bytes >= 0x80 are neither alpha nor digit nor space)

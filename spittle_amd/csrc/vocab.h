@@ -19,6 +19,7 @@ public:
     Vocab(const std::vector<std::string>& file_tokens, int n_vocab, const Specials& sp);
     int size() const { return (int)id_to_tok_.size(); }
     const std::string& str(int id) const;  // "" when out of range
+    int id(const std::string& tok) const;  // token_to_id; -1 when absent
     // whisper_tokenize: split with the GPT-2 pre-tokenisation pattern, then cover each piece
     // with the longest vocabulary entries from the left.  Bytes no entry covers are skipped
     // (whisper.cpp logs "unknown token" and goes on); *n_unknown counts them.

@@ -50,12 +50,19 @@ class WhisperInferenceParams:
     # whisper_full_params.prompt_tokens: token ids decoded before [sot ...] (what initial_prompt
     # becomes after tokenization)
     prompt_tokens: Optional[Sequence[int]] = None
-    # whisper_full_params the app leaves at their defaults
+    # whisper_full_params the app leaves at their defaults (whisper_full_default_params)
     suppress_blank: bool = True
-    no_timestamps: bool = True
-    max_new_tokens: int = 220
+    suppress_non_speech_tokens: bool = False
+    no_timestamps: bool = False
+    max_new_tokens: int = 220           # fast path: tokens per window; whisper_full: max_tokens
     temperature: float = 0.0
+    temperature_inc: float = 0.2        # fallback step; 0 = none
+    best_of: int = 5
+    entropy_thold: float = 2.4
+    logprob_thold: float = -1.0
+    max_initial_ts: float = 1.0
     beam_size: int = 1
+    seed: int = 0
     # benchmark / test hooks
     ignore_eot: bool = False
     forced_tokens: Optional[np.ndarray] = None  # [batch][n] teacher forcing
@@ -63,9 +70,11 @@ class WhisperInferenceParams:
 
 @dataclass
 class TranscriptionSegment:
-    start: float
+    start: float            # seconds (whisper_full_get_segment_t0 / 100, as transcribe-rs)
     end: float
     text: str
+    i0: int = 0             # the segment's tokens: TranscriptionResult.tokens[i0:i0 + n_tokens]
+    n_tokens: int = 0
 
 
 @dataclass
@@ -77,6 +86,7 @@ class TranscriptionResult:
     top2: Optional[np.ndarray] = None
     n_windows: int = 0
     language: Optional[str] = None      # ISO-639-1 code decoded with (detected or given)
+    n_fallbacks: int = 0                # temperature fallbacks taken (repeated decodes)
 
 
 def _infer_params(p: Optional[WhisperInferenceParams], keep: list) -> L.InferParams:
@@ -86,10 +96,17 @@ def _infer_params(p: Optional[WhisperInferenceParams], keep: list) -> L.InferPar
     ip.translate = int(bool(p.translate))
     ip.initial_prompt = p.initial_prompt.encode() if p.initial_prompt else None
     ip.flags = (L.SPT_SUPPRESS_BLANK if p.suppress_blank else 0) | \
-               (L.SPT_NO_TIMESTAMPS if p.no_timestamps else 0) | (L.SPT_IGNORE_EOT if p.ignore_eot else 0)
+               (L.SPT_NO_TIMESTAMPS if p.no_timestamps else 0) | (L.SPT_IGNORE_EOT if p.ignore_eot else 0) | \
+               (L.SPT_SUPPRESS_NST if p.suppress_non_speech_tokens else 0)
     ip.max_new_tokens = int(p.max_new_tokens)
     ip.temperature = float(p.temperature)
     ip.beam_size = int(p.beam_size)
+    ip.temperature_inc = float(p.temperature_inc)
+    ip.best_of = int(p.best_of)
+    ip.entropy_thold = float(p.entropy_thold)
+    ip.logprob_thold = float(p.logprob_thold)
+    ip.max_initial_ts = float(p.max_initial_ts)
+    ip.seed = int(p.seed)
     if p.forced_tokens is not None:
         f = np.ascontiguousarray(p.forced_tokens, dtype=np.int32)
         keep.append(f)
@@ -111,8 +128,14 @@ def _take_result(rp) -> TranscriptionResult:
     t2 = np.ctypeslib.as_array(r.top2, shape=(n,)).copy() if n else np.zeros(0, np.float32)
     lib = L.load()
     code = lib.spt_language_code(r.language) if r.language >= 0 else None
-    res = TranscriptionResult(text=(r.text or b"").decode("utf-8", "replace"), segments=[], tokens=toks, top1=t1,
-                              top2=t2, n_windows=r.n_windows, language=code.decode() if code else None)
+    segs = []
+    for i in range(r.n_segments):
+        s = r.segments[i]
+        segs.append(TranscriptionSegment(start=s.t0 / 100.0, end=s.t1 / 100.0,
+                                         text=(s.text or b"").decode("utf-8", "replace"), i0=s.i0, n_tokens=s.n_tokens))
+    res = TranscriptionResult(text=(r.text or b"").decode("utf-8", "replace"), segments=segs, tokens=toks, top1=t1,
+                              top2=t2, n_windows=r.n_windows, language=code.decode() if code else None,
+                              n_fallbacks=r.n_fallbacks)
     lib.spt_result_free(rp)
     return res
 

@@ -10,6 +10,7 @@ import pytest
 from spittle_amd import _lib as L
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+HEADER = os.path.join(ROOT, "include", "spittle_hip.h")
 
 
 def _header_symbols():
@@ -36,16 +37,33 @@ def test_version_and_defaults():
     ip = L.InferParams()
     lib.spt_default_infer_params(C.byref(ip))
     assert ip.language == b"en" and ip.beam_size == 1 and ip.max_new_tokens == 220
-    assert ip.flags == L.SPT_SUPPRESS_BLANK | L.SPT_NO_TIMESTAMPS
+    # whisper_full_default_params: timestamps on, temperature fallback 0.2 / best_of 5
+    assert ip.flags == L.SPT_SUPPRESS_BLANK
+    assert (ip.temperature, ip.best_of, ip.logprob_thold, ip.max_initial_ts) == (0.0, 5, -1.0, 1.0)
+    assert abs(ip.temperature_inc - 0.2) < 1e-7 and abs(ip.entropy_thold - 2.4) < 1e-6
 
 
-def test_struct_layouts_match_header():
-    # sizes of the ABI structs as the C compiler lays them out (x86-64 SysV)
-    assert C.sizeof(L.ModelParams) == 24
-    assert C.sizeof(L.InferParams) == 72
-    assert C.sizeof(L.Result) == 48
-    assert C.sizeof(L.ModelInfo) == 56
-    assert C.sizeof(L.Timings) == 56
+def test_struct_layouts_match_header(tmp_path):
+    """Every ctypes mirror has the size and field offsets gcc gives the header's structs."""
+    import subprocess
+    structs = {"spt_model_params": L.ModelParams, "spt_infer_params": L.InferParams, "spt_result": L.Result,
+               "spt_segment": L.Segment, "spt_model_info": L.ModelInfo, "spt_timings": L.Timings}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f in py._fields_:
+            lines.append(f'printf("{cname} {f[0]} %zu\\n", offsetof({cname}, {f[0]}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", str(src), "-o", str(exe)], check=True)
+    got = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    for line in filter(None, got):
+        cname, field, val = line.split()
+        py = structs[cname]
+        want = C.sizeof(py) if field == "size" else getattr(py, field).offset
+        assert int(val) == want, (cname, field, val, want)
 
 
 def test_language_codes():

@@ -67,6 +67,8 @@ def _engine(path, dtype="f32", max_batch=2):
 def _params(**kw):
     from spittle_amd import WhisperInferenceParams
     kw.setdefault("language", "en")
+    kw.setdefault("no_timestamps", True)  # the device-resident greedy protocol (no fallback)
+    kw.setdefault("temperature_inc", 0.0)
     return WhisperInferenceParams(**kw)
 
 
