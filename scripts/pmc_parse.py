@@ -5,12 +5,13 @@ stores). Units: FETCH_SIZE / WRITE_SIZE are KiB."""
 import csv
 import glob
 import json
+import re
 import sys
 from collections import defaultdict
 
 tag = sys.argv[1] if len(sys.argv) > 1 else "r1"
 SEL = {
-    "dec_cross_attn": lambda n: "cross_attn_kernel<unsigned short, 1>" in n,
+    "dec_cross_attn": lambda n: re.search(r"cross_attn_kernel<unsigned short, 1[,>]", n) is not None,
     "dec_logits": lambda n: "gemv_kernel<unsigned short, 4," in n,
     "enc_fc1_gemm": lambda n: "gemm256_kernel<1>" in n,
 }

@@ -20,6 +20,9 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <stdio.h>
+#include <stdlib.h>
+
 #include <algorithm>
 
 namespace spt {
@@ -476,9 +479,9 @@ template <> struct KVChunk<float> {
 // key (8 dims each, fully coalesced 16-byte sweeps of the K/V rows), online softmax in exp2
 // space; raw K/V chunks ping-pong so the next block streams in during the current one.
 // qv is pre-scaled by log2(e)/8.  Leaves (m, l, o) per query in the calling lanes.
-template <typename T, int NQ>
+template <typename T, int NQ, int NI_ = 0, int NW = AW>
 struct AttnWave {
-    static constexpr int NI = (sizeof(T) == 2) ? (NQ == 1 ? 8 : 4) : (NQ == 1 ? 4 : 2);
+    static constexpr int NI = NI_ > 0 ? NI_ : (sizeof(T) == 2) ? (NQ == 1 ? 8 : 4) : (NQ == 1 ? 4 : 2);
     static constexpr int KB = 8 * NI;  // keys per block
     KVChunk<T> kA[NI], vA[NI], kB[NI], vB[NI];
     float m[NQ], l[NQ], o[NQ][8];
@@ -545,17 +548,17 @@ struct AttnWave {
             m[t] = mn;
         }
     }
-    // blocks blk0 + w, blk0 + w + AW, ... below nblk; the first block may already be in flight
+    // blocks blk0 + w, blk0 + w + NW, ... below nblk; the first block may already be in flight
     __device__ __forceinline__ void run(int blk, int nblk, bool first_loaded, const float (&qv)[NQ][8],
                                         const int (&lim)[NQ], int Tq) {
         if (blk < nblk && !first_loaded) load_blk(kA, vA, blk);
         while (blk < nblk) {
-            int nb = blk + AW;
+            int nb = blk + NW;
             if (nb < nblk) load_blk(kB, vB, nb);
             process(kA, vA, blk * KB, qv, lim, Tq);
             blk = nb;
             if (blk >= nblk) break;
-            nb = blk + AW;
+            nb = blk + NW;
             if (nb < nblk) load_blk(kA, vA, nb);
             process(kB, vB, blk * KB, qv, lim, Tq);
             blk = nb;
@@ -591,17 +594,17 @@ struct AttnWave {
     }
 };
 
-// workgroup merge of the AW waves' (m, l, o) for query t, element e -> (M, L, O)
-template <int NQ>
+// workgroup merge of the NW waves' (m, l, o) for query t, element e -> (M, L, O)
+template <int NQ, int NW = AW>
 __device__ __forceinline__ void attn_merge(const float (*s_m)[NQ], const float (*s_l)[NQ], const float (*s_o)[NQ][64],
                                            int t, int e, float& M, float& L, float& O) {
     M = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < AW; ++w) M = fmaxf(M, s_m[w][t]);
+    for (int w = 0; w < NW; ++w) M = fmaxf(M, s_m[w][t]);
     L = 0.f;
     O = 0.f;
 #pragma unroll
-    for (int w = 0; w < AW; ++w) {
+    for (int w = 0; w < NW; ++w) {
         if (s_m[w][t] == -INFINITY) continue;
         const float f = exp2f(s_m[w][t] - M);
         L += s_l[w][t] * f;
@@ -649,16 +652,19 @@ __global__ __launch_bounds__(64 * AW) void self_attn_kernel(const T* __restrict_
 // kv: [2][B_layout][H][T_enc][64] at the group's first sequence.  (A fused LayerNorm + cross-Q
 // projection prologue and key-chunk splits were measured slower on MI355X: r1
 // exp_fused_xattn_pending_slabs.txt.)
-template <typename T, int NQ, bool SPLIT>
-__global__ __launch_bounds__(64 * AW) void cross_attn_kernel(const T* __restrict__ q, const T* __restrict__ kv,
+// 4 keys per lane for the bf16 single-query (decode step) case: lower register pressure, more
+// waves resident per CU (r1 exp10: 15.9 -> 15.0 us per layer cache-cold)
+template <typename T, int NQ, bool SPLIT, int NW = AW, int NIX = (sizeof(T) == 2 && NQ == 1) ? 4 : 0>
+__global__ __launch_bounds__(64 * NW) void cross_attn_kernel(const T* __restrict__ q, const T* __restrict__ kv,
                                                              int B_layout, int H, int T_enc, int Tq,
                                                              T* __restrict__ out, float* __restrict__ part) {
-    __shared__ float s_m[AW][NQ], s_l[AW][NQ];
-    __shared__ float s_o[AW][NQ][64];
+    typedef AttnWave<T, NQ, NIX, NW> W;
+    __shared__ float s_m[NW][NQ], s_l[NW][NQ];
+    __shared__ float s_o[NW][NQ][64];
     const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane & 7;
     const size_t kvo = ((size_t)b * H + h) * (size_t)T_enc * 64 + 8 * g;
-    AttnWave<T, NQ> aw;
+    W aw;
     aw.init(kv + kvo, kv + (size_t)B_layout * H * T_enc * 64 + kvo, T_enc, lane);
     float qv[NQ][8];
     int lim[NQ];
@@ -671,7 +677,7 @@ __global__ __launch_bounds__(64 * AW) void cross_attn_kernel(const T* __restrict
         lim[t] = T_enc;
     }
     // SPLIT: this workgroup's chunk of the key blocks (gridDim.y chunks, block-aligned)
-    const int nblk_all = cdiv(T_enc, AttnWave<T, NQ>::KB);
+    const int nblk_all = cdiv(T_enc, W::KB);
     const int S = SPLIT ? (int)gridDim.y : 1, sp = SPLIT ? (int)blockIdx.y : 0;
     const int per = cdiv(nblk_all, S), blk0 = sp * per, nblk = min(nblk_all, blk0 + per);
     aw.run(blk0 + wid, nblk, false, qv, lim, Tq);
@@ -680,7 +686,7 @@ __global__ __launch_bounds__(64 * AW) void cross_attn_kernel(const T* __restrict
     if (tid < 64 * Tq) {
         const int t = tid >> 6, e = tid & 63;
         float M, L, O;
-        attn_merge<NQ>(s_m, s_l, s_o, t, e, M, L, O);
+        attn_merge<NQ, NW>(s_m, s_l, s_o, t, e, M, L, O);
         if constexpr (SPLIT) {  // partial {o[64], m, l} for the output projection's merge prologue
             float* pp = part + ((((size_t)(b * Tq + t)) * H + h) * S + sp) * 66;
             pp[e] = O;
