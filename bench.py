@@ -81,7 +81,7 @@ def cpu_baseline(model_spec: str, sample_steps: int, decode_steps: int) -> dict:
 
 DOMINANT = "dec_cross_attn"  # largest share of device time (profiles/*_kernel_stats.csv)
 KERNEL_NAMES = {
-    "dec_cross_attn": "cross_attn_kernel<bf16,1,false,8,4> (decoder cross-attention, 1 layer)",
+    "dec_cross_attn": "cross_attn_kernel<bf16,1> (4 keys/lane) (decoder cross-attention, 1 layer)",
     "dec_logits": "gemv_kernel<bf16,GV_LOGITS,A_LN> (final LN + logits + top-2)",
     "dec_fc1": "gemv_kernel<bf16,GV_BIAS_GELU,A_LN> (decoder LN + fc1 + GELU)",
     "enc_fc1_gemm": "gemm256_kernel<EPI_BIAS_GELU> (encoder fc1, 256x256 tile)",

@@ -479,9 +479,11 @@ template <> struct KVChunk<float> {
 // key (8 dims each, fully coalesced 16-byte sweeps of the K/V rows), online softmax in exp2
 // space; raw K/V chunks ping-pong so the next block streams in during the current one.
 // qv is pre-scaled by log2(e)/8.  Leaves (m, l, o) per query in the calling lanes.
+// keys per lane: 4 for bf16 (r1 exp10 / exp11: lower register pressure and more resident waves
+// beat deeper per-lane prefetch for both the cross- and the self-attention step), 2 for f32 prompts
 template <typename T, int NQ, int NI_ = 0, int NW = AW>
 struct AttnWave {
-    static constexpr int NI = NI_ > 0 ? NI_ : (sizeof(T) == 2) ? (NQ == 1 ? 8 : 4) : (NQ == 1 ? 4 : 2);
+    static constexpr int NI = NI_ > 0 ? NI_ : (sizeof(T) == 2) ? 4 : (NQ == 1 ? 4 : 2);
     static constexpr int KB = 8 * NI;  // keys per block
     KVChunk<T> kA[NI], vA[NI], kB[NI], vB[NI];
     float m[NQ], l[NQ], o[NQ][8];
@@ -614,7 +616,7 @@ __device__ __forceinline__ void attn_merge(const float (*s_m)[NQ], const float (
 
 // Self-attention over the cache (keys 0..pos0+t), one workgroup per (b, h).
 // q rows: q + (b*Tq + t)*q_ld + h*64; K/V rows of (b, h): base + ((kv*B + b)*H + h)*ctx*64.
-template <typename T, int NQ>
+template <typename T, int NQ, int NIX = 0>
 __global__ __launch_bounds__(64 * AW) void self_attn_kernel(const T* __restrict__ q, int q_ld,
                                                             const T* __restrict__ kv, int B, int H, int ctx, int Tq,
                                                             const DecState* __restrict__ ds, T* __restrict__ out) {
@@ -624,7 +626,7 @@ __global__ __launch_bounds__(64 * AW) void self_attn_kernel(const T* __restrict_
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane & 7;
     const int pos0 = ds->pos0;
     const int n_keys = pos0 + Tq;
-    AttnWave<T, NQ> aw;
+    AttnWave<T, NQ, NIX> aw;
     aw.init(kv + (((size_t)0 * B + b) * H + h) * (size_t)ctx * 64 + 8 * g,
             kv + (((size_t)1 * B + b) * H + h) * (size_t)ctx * 64 + 8 * g, n_keys, lane);
     float qv[NQ][8];
@@ -637,7 +639,7 @@ __global__ __launch_bounds__(64 * AW) void self_attn_kernel(const T* __restrict_
         for (int e = 0; e < 8; ++e) qv[t][e] = to_f<T>(qr[e]) * kLog2Scale;
         lim[t] = pos0 + tt + 1;
     }
-    aw.run(wid, cdiv(n_keys, AttnWave<T, NQ>::KB), false, qv, lim, Tq);
+    aw.run(wid, cdiv(n_keys, AttnWave<T, NQ, NIX>::KB), false, qv, lim, Tq);
     aw.to_lds(s_m, s_l, s_o, wid, lane);
     __syncthreads();
     if (tid < 64 * Tq) {
@@ -652,9 +654,7 @@ __global__ __launch_bounds__(64 * AW) void self_attn_kernel(const T* __restrict_
 // kv: [2][B_layout][H][T_enc][64] at the group's first sequence.  (A fused LayerNorm + cross-Q
 // projection prologue and key-chunk splits were measured slower on MI355X: r1
 // exp_fused_xattn_pending_slabs.txt.)
-// 4 keys per lane for the bf16 single-query (decode step) case: lower register pressure, more
-// waves resident per CU (r1 exp10: 15.9 -> 15.0 us per layer cache-cold)
-template <typename T, int NQ, bool SPLIT, int NW = AW, int NIX = (sizeof(T) == 2 && NQ == 1) ? 4 : 0>
+template <typename T, int NQ, bool SPLIT, int NW = AW, int NIX = 0>
 __global__ __launch_bounds__(64 * NW) void cross_attn_kernel(const T* __restrict__ q, const T* __restrict__ kv,
                                                              int B_layout, int H, int T_enc, int Tq,
                                                              T* __restrict__ out, float* __restrict__ part) {
