@@ -72,15 +72,16 @@ typedef struct {
     int32_t max_new_tokens;      /* fast path: generated tokens per 30 s window (<= 220);
                                     whisper_full path: whisper_full_params.max_tokens (0 = none) */
     float temperature;           /* initial temperature (0 = greedy) */
-    int32_t beam_size;           /* only 1 (greedy sampling strategy) is implemented */
+    int32_t beam_size;           /* 1: greedy; 2..8: beam search at temperature 0 (one decoder row
+                                    per beam: <= max_batch; whisper_full path) */
     const int32_t* forced_tokens;/* test hook (teacher forcing): [batch][n_forced] or NULL */
     int32_t n_forced;
     const int32_t* prompt_tokens;/* whisper_full_params.prompt_tokens: decoded before [sot ...] as
                                     [prev] + the last min(224, n) of them; NULL = none */
     int32_t n_prompt_tokens;
     /* ABI 3: whisper_full's window loop (timestamps, segments, temperature fallback).  A call
-     * takes the device-resident no-timestamp greedy fast path when SPT_NO_TIMESTAMPS is set and
-     * temperature_inc == 0 and temperature == 0; every other call runs whisper_full. */
+     * takes the device-resident no-timestamp greedy fast path when SPT_NO_TIMESTAMPS is set,
+     * temperature_inc == 0, temperature == 0 and beam_size <= 1; every other call runs whisper_full. */
     float temperature_inc;       /* fallback step (0.2); 0 = no fallback */
     int32_t best_of;             /* sampled decoders per window at temperature > 0 (5) */
     float entropy_thold;         /* a decoder whose last 32 tokens' entropy is lower fails (2.4) */

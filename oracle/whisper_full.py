@@ -36,6 +36,7 @@ class Params:
     logprob_thold: float = -1.0
     n_max_text_ctx: int = 16384
     translate: bool = False
+    beam_size: int = 1
 
 
 @dataclass
@@ -110,6 +111,49 @@ def pick(lg: np.ndarray, step: int, toks: list, w: Window, p: Params, sp: dict, 
     return i, plog, tid, float(margin)
 
 
+def topk(lg: np.ndarray, step: int, toks: list, w: Window, p: Params, sp: dict, smask: np.ndarray, k: int,
+         blank: int = 220, max_initial: int = 50):
+    """beam candidates of one decoder: the k best processed logits (after the timestamp rule,
+    ties: lower id) as (id, logprob, tid), plus the smallest gap around the k-th place."""
+    eot, beg = sp["eot"], sp["beg"]
+    v = lg.astype(np.float64).copy()
+    mask = smask.copy()
+    if step == 0 and p.suppress_blank:
+        mask[eot] = mask[blank] = True
+    if p.no_timestamps:
+        mask[beg:] = True
+    last_ts = len(toks) > 0 and toks[-1] >= beg
+    pen_ts = len(toks) < 2 or toks[-2] >= beg
+    if last_ts:
+        if pen_ts:
+            mask[beg:] = True
+        else:
+            mask[:eot] = True
+    if step == 0 and max_initial >= 0:
+        mask[beg + max_initial + 1:] = True
+    if w.has_ts:
+        mask[beg:beg + w.seek_delta // 2] = True
+    v[mask] = -np.inf
+    M = v.max()
+    lse = np.log(np.exp(v[np.isfinite(v)] - M).sum()) + M
+    mt, ms = v[:beg].max(), v[beg:].max()
+    margin = np.inf
+    rule = False
+    if np.isfinite(ms):
+        tsl = np.log(np.exp(v[beg:][np.isfinite(v[beg:])] - ms).sum()) + ms
+        rule = tsl > mt
+        margin = abs(tsl - mt)
+    cand = v.copy()
+    if rule:
+        cand[:beg] = -np.inf
+    order = np.lexsort((np.arange(len(cand)), -cand))[:k + 1]
+    tid = int(np.argmax(v[beg:])) + beg if np.isfinite(ms) else 0
+    out = [(int(i), float(v[i] - lse), int(i) if i >= beg else tid) for i in order[:k] if np.isfinite(cand[i])]
+    if len(order) > k and np.isfinite(cand[order[k]]):
+        margin = min(margin, cand[order[k - 1]] - cand[order[k]])
+    return out, float(margin)
+
+
 def bookkeep(w: Window, tok: int, i: int, seek: int, seek_end: int, p: Params, sp: dict, n_max: int) -> None:
     eot, beg = sp["eot"], sp["beg"]
     if tok > beg:
@@ -151,6 +195,55 @@ def decode_window(m: O.Model, enc: np.ndarray, prompt: list, seek: int, seek_end
     return w
 
 
+def decode_window_beam(m: O.Model, enc: np.ndarray, prompt: list, seek: int, seek_end: int, p: Params,
+                       n_steps: int, blank: int = 220) -> list:
+    """whisper_full's beam search at temperature 0 (see spittle_amd/csrc/full.cpp run_beam):
+    returns the K decoders (Windows; margin = the smallest candidate gap of the step)."""
+    import copy
+    sp = O.special_tokens(m.dims.n_vocab)
+    smask = static_mask(m.dims.n_vocab, sp)
+    n_max = m.dims.n_text_ctx // 2 - 4
+    K = p.beam_size
+    decs = [Window() for _ in range(K)]
+    sums = [0.0] * K
+    for i in range(n_steps):
+        cands = []
+        gap = np.inf
+        for d in range(K):
+            w = decs[d]
+            if w.status:
+                continue
+            toks = [s.tok for s in w.steps]
+            lg = m.logits(enc, prompt + toks)
+            out, mg = topk(lg, i, toks, w, p, sp, smask, K, blank)
+            gap = min(gap, mg)
+            for tok, lp, tid in out:
+                cands.append((d, sums[d] + lp, tok, lp, tid))
+        if not cands:
+            break
+        cands.sort(key=lambda c: (-c[1], c[0]))
+        new, new_sums, cur = list(decs), list(sums), 0
+        for d in range(K):
+            if decs[d].status:
+                continue
+            if cur >= len(cands):
+                cur = 0
+            c = cands[cur]
+            cur += 1
+            while len(cands) > cur and cands[cur][1] == c[1] and i > 0:
+                cur += 1
+            w = copy.deepcopy(decs[c[0]])
+            w.steps.append(Step(c[2], c[3], c[4], gap))
+            new[d], new_sums[d] = w, c[1]
+        for d in range(K):
+            if decs[d].status == 0:
+                bookkeep(new[d], new[d].steps[-1].tok, i, seek, seek_end, p, sp, n_max)
+        decs, sums = new, new_sums
+        if all(w.status for w in decs):
+            break
+    return decs
+
+
 def n_len_org(n: int) -> int:
     return 1 + int((n + 200 - 400) / N_LEN_HOP)  # C integer division (toward zero)
 
@@ -183,22 +276,37 @@ def transcribe(m: O.Model, pcm: np.ndarray, p: Params, prompt=(), lang_tok: int 
         chunk = pcm[seek * N_LEN_HOP: seek * N_LEN_HOP + 480000]
         enc = m.encode(O.mel(chunk, m.dims.n_mels))
         steps = min(n_max, m.dims.n_text_ctx + 1 - len(pf) - len(init))
-        w = decode_window(m, enc, pf + init, seek, seek_end, pp, steps)
+        if p.beam_size > 1:
+            decs = decode_window_beam(m, enc, pf + init, seek, seek_end, pp, steps)
+        else:
+            decs = [decode_window(m, enc, pf + init, seek, seek_end, pp, steps)]
+
+        def scored(w):  # whisper_sequence_score + the entropy check: (failed, score)
+            if w.status == 2:
+                return True, -np.inf
+            rl = w.result_len
+            if rl == 0:
+                return False, -np.inf
+            toks_ = [s.tok for s in w.steps]
+            cnt = {}
+            for t in toks_[max(0, rl - 32):rl]:
+                cnt[t] = cnt.get(t, 0) + 1
+            n = sum(cnt.values())
+            ent = -sum(c / n * np.log(c / n) for c in cnt.values())
+            if rl > 32 and ent < p.entropy_thold:
+                return True, -np.inf
+            return False, sum(s.plog for s in w.steps[:rl]) / rl
+
+        best, best_score = 0, -np.inf
+        flags = [scored(w) for w in decs]
+        for d, (f, sc) in enumerate(flags):
+            if not f and best_score < sc:
+                best, best_score = d, sc
+        w = decs[best]
+        failed = flags[best][0]
         wins.append((seek, w))
         toks = [s.tok for s in w.steps]
         tids = [s.tid for s in w.steps]
-        failed = w.status == 2
-        if not failed:
-            rl = w.result_len
-            if rl > 0:
-                lp = sum(s.plog for s in w.steps[:rl])
-                cnt = {}
-                for t in toks[max(0, rl - 32):rl]:
-                    cnt[t] = cnt.get(t, 0) + 1
-                n = sum(cnt.values())
-                ent = -sum(c / n * np.log(c / n) for c in cnt.values())
-                if rl > 32 and ent < p.entropy_thold:
-                    failed = True
         n_keep = len(toks) if failed else min(w.result_len, len(toks))
         toks, tids = toks[:n_keep], tids[:n_keep]
         base = len(all_toks)

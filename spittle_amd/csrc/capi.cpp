@@ -87,7 +87,7 @@ spt_status lang_of(spt_ctx* c, const spt_infer_params* p, int* lang_tok) {
 
 // the device-resident greedy no-timestamp protocol, or whisper_full's window loop
 bool full_mode(const spt_infer_params* p) {
-    return !(p->flags & SPT_NO_TIMESTAMPS) || p->temperature_inc > 0.0f || p->temperature != 0.0f;
+    return !(p->flags & SPT_NO_TIMESTAMPS) || p->temperature_inc > 0.0f || p->temperature != 0.0f || p->beam_size > 1;
 }
 
 // whisper_full's prompt_init: [sot] (+ [lang, task] for multilingual) + [notimestamps]; its
@@ -209,7 +209,9 @@ spt_result* make_full_result(const spt::FullResult& f, const spt::Specials& sp) 
 // whisper_full (full.cpp) over host utterances
 spt_status run_full(spt_ctx* c, const float* const* pcm, const size_t* n_samples, size_t batch,
                     const spt_infer_params* p, spt_result** out) {
-    if (p->beam_size > 1) return fail(c, SPT_ERR_UNSUPPORTED, "beam search is not implemented (greedy only)");
+    if (p->beam_size > 8) return fail(c, SPT_ERR_INVALID_ARG, "beam_size must be at most 8");
+    if (p->beam_size > c->eng->max_batch())
+        return fail(c, SPT_ERR_INVALID_ARG, "beam_size exceeds the context's max_batch (one row per beam)");
     if (p->forced_tokens || (p->flags & SPT_IGNORE_EOT))
         return fail(c, SPT_ERR_INVALID_ARG, "forced tokens / SPT_IGNORE_EOT are fast-path (no-timestamp) hooks");
     if ((p->flags & SPT_SUPPRESS_NST) && !c->vocab)
@@ -229,6 +231,7 @@ spt_status run_full(spt_ctx* c, const float* const* pcm, const size_t* n_samples
     fp.temperature = p->temperature;
     fp.temperature_inc = p->temperature_inc;
     fp.best_of = p->best_of > 0 ? p->best_of : 5;
+    fp.beam_size = std::max(1, p->beam_size);
     fp.entropy_thold = p->entropy_thold;
     fp.logprob_thold = p->logprob_thold;
     fp.max_initial_ts = p->max_initial_ts;

@@ -171,6 +171,7 @@ void Engine::release() {
     }
     if (warena_) (void)hipFree(warena_);
     if (aarena_) (void)hipFree(aarena_);
+    if (kvtmp_) (void)hipFree(kvtmp_);
     for (void* p : {(void*)hann_, (void*)sinv_, (void*)cosv_, (void*)filt_, (void*)grp_})
         if (p) (void)hipFree(p);
     for (auto& e : ev_) (void)hipEventDestroy(e);
@@ -178,6 +179,7 @@ void Engine::release() {
     groups_.clear();
     ev_.clear();
     warena_ = aarena_ = nullptr;
+    kvtmp_ = nullptr;
     hann_ = sinv_ = cosv_ = filt_ = nullptr;
     grp_ = nullptr;
     st_ = nullptr;
@@ -566,6 +568,13 @@ void Engine::alloc_workspace() {
             g.seek_end = (int*)c.take(B * 4);
             g.ts_state = (int*)c.take(B * 16);
             g.prm = (TsParams*)c.take(sizeof(TsParams));
+            g.beam_row = (int*)c.take(B * 16);
+            g.beam_step = (int*)c.take(64);
+            g.beam_src = (int*)c.take(B * 4);
+            g.beam_ident = (int*)c.take(B * 4);
+            g.cand_id = (int*)c.take(B * 8 * 4);
+            g.cand_lp = (float*)c.take(B * 8 * 4);
+            g.beam_tid = (int*)c.take(B * 4);
         }
         zero_ = (float*)c.take(R * d * 4);  // never written: the "no pending slab" operand
         if (!pass) {
@@ -743,6 +752,16 @@ void Engine::enqueue_head(DecGroup& g, int Tq, const DecodeRequest& rq, int out_
     a.blank1 = blank ? 220 : -1;
     a.part = g.part; a.n_tiles = n_tiles;
     gemv(dt_, GV_LOGITS, A_LN, a, st);
+    if (rq.beam_k > 0) {  // candidates for the host's beam bookkeeping; no token is chosen here
+        BeamArgs bm{};
+        bm.logits = g.logits; bm.ldl = dm_.n_vocab;
+        bm.n_vocab = dm_.n_vocab; bm.eot = sp.eot; bm.beg = sp.beg; bm.blank = rq.blank_tok;
+        bm.suppress = sup; bm.prm = g.prm; bm.row = g.beam_row; bm.step = g.beam_step; bm.k = rq.beam_k;
+        bm.cand_id = g.cand_id; bm.cand_lp = g.cand_lp; bm.tid = g.beam_tid;
+        dec_beam_topk(bm, B, st);
+        dec_advance(g.ds, Tq, st);
+        return;
+    }
     if (rq.full) {
         TsArgs t{};
         t.logits = g.logits; t.ldl = dm_.n_vocab;
@@ -908,7 +927,21 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         }
         upload_tokens(g, [&](int b, int t) { return (t == 1 && lang[b] >= 0) ? lang[b] : rq.prompt[t]; }, Tq);
         dec_embed(dt_, g.tok_in, g.B * Tq, Tq, dm_.d, tok_emb_, dec_pos_, g.ds, g.dx, g.st);
+        if (rq.beam_k > 0) {  // the first step's state: no tokens yet
+            beam_host_.assign((size_t)g.B * 4 + 1, 0);
+            for (int b = 0; b < g.B; ++b) beam_host_[b * 4 + 3] = 3000;
+            HIP_CHECK(hipMemcpyAsync(g.beam_row, beam_host_.data(), (size_t)g.B * 16, hipMemcpyHostToDevice, g.st));
+            HIP_CHECK(hipMemcpyAsync(g.beam_step, beam_host_.data() + (size_t)g.B * 4, 4, hipMemcpyHostToDevice, g.st));
+        }
         enqueue_decoder_pass(g, B, Tq, rq, out_cap);  // prompt pass produces token 0
+    }
+    if (rq.beam_k > 0) {  // beam search continues step by step from the host (beam_next)
+        tm_.n_decode_passes = 1;
+        for (DecGroup* g : act) {
+            HIP_CHECK(hipEventRecord(g->ev, g->st));
+            HIP_CHECK(hipStreamWaitEvent(st_, g->ev, 0));
+        }
+        return;
     }
     int passes = 1;
     static const bool no_graph = getenv("SPT_NO_GRAPH") != nullptr;  // eager passes (profilers, debugging)
@@ -1024,6 +1057,67 @@ void Engine::transcribe_host(const float* const* pcm, const int* n_samples, int 
     if (B < 1 || B > max_batch_) throw std::runtime_error("batch exceeds the context's max_batch");
     stage_pcm(pcm, n_samples, B);
     transcribe_device(pcm_, 480000, n_samples, B, rq, tokens, top1, top2, lang_out, ts_state_out);
+}
+
+// ----------------------------------------------------------------------------- beam search
+void Engine::read_cands(int B, BeamCands* out) {
+    DecGroup& g = groups_[0];
+    out->id.resize((size_t)B * 8);
+    out->lp.resize((size_t)B * 8);
+    out->tid.resize(B);
+    HIP_CHECK(hipMemcpyAsync(out->id.data(), g.cand_id, (size_t)B * 32, hipMemcpyDeviceToHost, g.st));
+    HIP_CHECK(hipMemcpyAsync(out->lp.data(), g.cand_lp, (size_t)B * 32, hipMemcpyDeviceToHost, g.st));
+    HIP_CHECK(hipMemcpyAsync(out->tid.data(), g.beam_tid, (size_t)B * 4, hipMemcpyDeviceToHost, g.st));
+    HIP_CHECK(hipStreamSynchronize(g.st));
+}
+
+void Engine::beam_begin(const float* const* pcm, const int* n_samples, int B, const DecodeRequest& rq, BeamCands* out,
+                        int* lang_out) {
+    select();
+    if (rq.beam_k < 1 || rq.beam_k > 8) throw std::runtime_error("beam size must be in 1..8");
+    if (n_groups_ != 1) throw std::runtime_error("beam search needs one decode group");
+    if (!kvtmp_) {
+        const size_t bytes = (size_t)dm_.n_dec * 2 * max_batch_ * dm_.n_head * dm_.n_text_ctx * 64 * esz_;
+        if (hipMalloc(&kvtmp_, bytes) != hipSuccess) {
+            kvtmp_ = nullptr;
+            throw std::runtime_error("out of device memory for the beam search scratch");
+        }
+    }
+    beam_rq_ = rq;
+    beam_B_ = B;
+    std::vector<int> tok((size_t)B * rq.n_steps);
+    transcribe_host(pcm, n_samples, B, rq, tok.data(), nullptr, nullptr, lang_out, nullptr);
+    std::vector<int> ident(B);
+    for (int b = 0; b < B; ++b) ident[b] = b;
+    HIP_CHECK(hipMemcpy(groups_[0].beam_ident, ident.data(), B * 4, hipMemcpyHostToDevice));
+    read_cands(B, out);
+}
+
+void Engine::beam_next(const int* src, const int* tokens, const int* rowstate, int step, BeamCands* out) {
+    select();
+    const int B = beam_B_;
+    if (B < 1) throw std::runtime_error("beam_next without beam_begin");
+    DecGroup& g = groups_[0];
+    for (int b = 0; b < B; ++b)
+        if (src[b] < 0 || src[b] >= B || tokens[b] < 0 || tokens[b] >= dm_.n_vocab)
+            throw std::runtime_error("beam_next: bad source row or token");
+    // host sources stay alive until the step's results are read back (synchronous below)
+    beam_host_.assign(src, src + B);
+    beam_host_.insert(beam_host_.end(), tokens, tokens + B);
+    beam_host_.insert(beam_host_.end(), rowstate, rowstate + (size_t)B * 4);
+    beam_host_.push_back(step);
+    const int* h = beam_host_.data();
+    HIP_CHECK(hipMemcpyAsync(g.beam_src, h, B * 4, hipMemcpyHostToDevice, g.st));
+    HIP_CHECK(hipMemcpyAsync(g.tok_in, h + B, B * 4, hipMemcpyHostToDevice, g.st));
+    HIP_CHECK(hipMemcpyAsync(g.beam_row, h + 2 * B, (size_t)B * 16, hipMemcpyHostToDevice, g.st));
+    HIP_CHECK(hipMemcpyAsync(g.beam_step, h + 6 * B, 4, hipMemcpyHostToDevice, g.st));
+    // reorder the self-K/V rows (positions < pos0) through the scratch, then feed the tokens
+    dec_kv_gather(dt_, g.skv, kvtmp_, g.beam_src, dm_.n_dec, B, dm_.n_head, dm_.n_text_ctx, g.ds, g.st);
+    dec_kv_gather(dt_, kvtmp_, g.skv, g.beam_ident, dm_.n_dec, B, dm_.n_head, dm_.n_text_ctx, g.ds, g.st);
+    dec_embed(dt_, g.tok_in, B, 1, dm_.d, tok_emb_, dec_pos_, g.ds, g.dx, g.st);
+    float* x = enqueue_layers(g, B, 1);
+    enqueue_head(g, 1, beam_rq_, beam_rq_.n_steps, x, suppress_, (beam_rq_.flags & 1u) != 0);
+    read_cands(B, out);
 }
 
 // ----------------------------------------------------------------------------- debug hooks

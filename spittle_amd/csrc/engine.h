@@ -46,6 +46,14 @@ struct DecodeRequest {
     std::vector<std::vector<int>> row_prefix;  // per-sequence prompt_past (equal lengths); else prefix
     std::vector<int> extra_suppress;           // e.g. the non-speech tokens of the vocabulary
     int blank_tok = 220;                       // " " (suppress_blank)
+    int beam_k = 0;                            // > 0: beam search, host-driven (beam_begin / beam_next)
+};
+
+// per-row beam candidates of one step (k <= 8 per row)
+struct BeamCands {
+    std::vector<int> id;     // [B][8], -1 = none
+    std::vector<float> lp;   // [B][8] log-probabilities
+    std::vector<int> tid;    // [B] most probable timestamp
 };
 
 struct Timings {
@@ -79,6 +87,14 @@ public:
     // host PCM convenience (stages into the engine's pcm buffer)
     void transcribe_host(const float* const* pcm, const int* n_samples, int B, const DecodeRequest& rq, int* tokens,
                          float* top1, float* top2, int* lang_out = nullptr, int* ts_state_out = nullptr);
+
+    // beam search (whisper_full, beam strategy): mel, encoder, cross K/V, prefix and prompt pass
+    // of B decoder rows (rq.beam_k candidates each) -> the first step's candidates; then one
+    // step per call: row b continues row src[b]'s sequence with tokens[b]; rowstate [B][4] =
+    // last token, previous token, has_ts, seek_delta; step = index of the token being chosen
+    void beam_begin(const float* const* pcm, const int* n_samples, int B, const DecodeRequest& rq, BeamCands* out,
+                    int* lang_out);
+    void beam_next(const int* src, const int* tokens, const int* rowstate, int step, BeamCands* out);
 
     void debug_mel(const float* pcm_host, int n, float* out_host);
     void debug_encode(const float* mel_host, float* out_host);
@@ -119,6 +135,9 @@ private:
         float* xpart = nullptr;       // cross-attention chunk partials [R][H][<=4][66]
         int *seek = nullptr, *seek_end = nullptr, *ts_state = nullptr;  // whisper_full decoding
         TsParams* prm = nullptr;
+        int *beam_row = nullptr, *beam_step = nullptr, *beam_src = nullptr, *beam_ident = nullptr;  // beam search
+        int *cand_id = nullptr, *beam_tid = nullptr;
+        float* cand_lp = nullptr;
         std::map<GraphKey, hipGraphExec_t> graphs;
         std::vector<int> host_tok;    // host sources of the call's token uploads
         size_t host_used = 0;
@@ -195,6 +214,11 @@ private:
     uint32_t suppress_flags_ = ~0u;
     std::vector<int> suppress_extra_;
     std::vector<int> ts_init_;
+    DecodeRequest beam_rq_;      // the request of the beam search in progress
+    int beam_B_ = 0;
+    void* kvtmp_ = nullptr;      // self-K/V reorder scratch (allocated on first beam search)
+    std::vector<int> beam_host_;  // host sources of the per-step uploads
+    void read_cands(int B, BeamCands* out);
 
     Timings tm_;
 };

@@ -51,6 +51,119 @@ void score(DecOut& d, const FullParams& p) {
     if (rl > 32 && entropy < p.entropy_thold) d.failed = true;
 }
 
+// one decoder's bookkeeping after token tok at step i (the kernel's rule, k_sample.hip)
+void bookkeep(DecOut& d, int tok, int i, int seek, int seek_end, const FullParams& p, const Specials& sp, int n_max,
+              bool& has_ts) {
+    if (tok > sp.beg) {
+        const int sdn = 2 * (tok - sp.beg);
+        if (has_ts && d.seek_delta > sdn && d.result_len < i) { d.status = 2; return; }
+        d.seek_delta = sdn;
+        d.result_len = i + 1;
+        has_ts = true;
+    }
+    if (tok == sp.eot || (p.max_tokens > 0 && i >= p.max_tokens) || (has_ts && seek + d.seek_delta + 100 >= seek_end)) {
+        if (d.result_len == 0 && !p.no_timestamps) {
+            if (seek + d.seek_delta + 100 >= seek_end) d.result_len = i + 1;
+            else { d.status = 2; return; }
+        }
+        if (p.no_timestamps) { d.result_len = i + 1; d.seek_delta = 3000; }
+        d.status = 1;
+        return;
+    }
+    if (i == n_max - 1 && (d.result_len == 0 || d.seek_delta < 1500)) d.status = 2;  // repetition guard
+}
+
+// whisper_full's beam search at temperature 0 over nj utterances x K decoder rows (row j*K + d):
+// each step every live decoder proposes its K best candidates (device, k_sample.hip
+// beam_topk_kernel); the candidates of one utterance are ranked by cumulative log-probability
+// (ties: lower decoder index), each live decoder takes the next one (from the second step on,
+// skipping candidates whose sum equals the one just taken), its self-K/V row follows the source
+// decoder, and the per-decoder bookkeeping runs on the new last token
+void run_beam(Engine& e, const DecodeRequest& rq, const std::vector<const float*>& ptr, const std::vector<int>& ns,
+              int nj, int K, const std::vector<int>& seek, const std::vector<int>& seek_end, const FullParams& p,
+              const Specials& sp, int n_max, std::vector<std::vector<DecOut>>* outs, std::vector<int>* lang) {
+    const int B = nj * K;
+    struct Dec {
+        DecOut o;
+        bool has_ts = false;
+        double sum_all = 0.0;
+    };
+    std::vector<Dec> dec(B);
+    for (Dec& d : dec) d.o.seek_delta = 3000;
+    BeamCands c;
+    lang->assign(B, -1);
+    e.beam_begin(ptr.data(), ns.data(), B, rq, &c, lang->data());
+    struct Cand {
+        int src;
+        Dec d;
+    };
+    std::vector<int> src(B), tok(B), row((size_t)B * 4);
+    for (int i = 0; i < rq.n_steps; ++i) {
+        bool any = false;
+        for (int j = 0; j < nj; ++j) {
+            std::vector<Cand> cs;
+            for (int dd = 0; dd < K; ++dd) {
+                const int r = j * K + dd;
+                const Dec& d = dec[r];
+                if (d.o.status != 0) continue;
+                for (int q = 0; q < K; ++q) {
+                    const int id = c.id[(size_t)r * 8 + q];
+                    if (id < 0) continue;
+                    Cand cd{r, d};
+                    cd.d.o.tok.push_back(id);
+                    cd.d.o.plog.push_back(c.lp[(size_t)r * 8 + q]);
+                    cd.d.o.tid.push_back((float)(id >= sp.beg ? id : c.tid[r]));
+                    cd.d.sum_all += c.lp[(size_t)r * 8 + q];
+                    cs.push_back(std::move(cd));
+                }
+            }
+            std::stable_sort(cs.begin(), cs.end(), [](const Cand& a, const Cand& b) {
+                if (a.d.sum_all != b.d.sum_all) return a.d.sum_all > b.d.sum_all;
+                return a.src < b.src;
+            });
+            size_t cur = 0;
+            std::vector<Dec> next(dec.begin() + j * K, dec.begin() + (j + 1) * K);
+            for (int dd = 0; dd < K; ++dd) {
+                const int r = j * K + dd;
+                src[r] = r;
+                if (dec[r].o.status != 0 || cs.empty()) continue;
+                if (cur >= cs.size()) cur = 0;
+                const Cand& pick = cs[cur++];
+                while (cs.size() > cur && cs[cur].d.sum_all == pick.d.sum_all && i > 0) ++cur;
+                next[dd] = pick.d;
+                src[r] = pick.src;
+            }
+            for (int dd = 0; dd < K; ++dd) {
+                const int r = j * K + dd;
+                Dec& d = next[dd];
+                if (dec[r].o.status == 0 && !cs.empty()) {
+                    bookkeep(d.o, d.o.tok.back(), i, seek[r], seek_end[r], p, sp, n_max, d.has_ts);
+                    if (d.o.status == 0) any = true;
+                }
+            }
+            for (int dd = 0; dd < K; ++dd) dec[j * K + dd] = std::move(next[dd]);
+        }
+        if (!any || i + 1 >= rq.n_steps) break;
+        for (int r = 0; r < B; ++r) {
+            const DecOut& o = dec[r].o;
+            const int n = (int)o.tok.size();
+            tok[r] = n > 0 ? o.tok[n - 1] : sp.eot;
+            row[r * 4 + 0] = n > 0 ? o.tok[n - 1] : -1;
+            row[r * 4 + 1] = n > 1 ? o.tok[n - 2] : -1;
+            row[r * 4 + 2] = dec[r].has_ts ? 1 : 0;
+            row[r * 4 + 3] = o.seek_delta;
+        }
+        e.beam_next(src.data(), tok.data(), row.data(), i + 1, &c);
+    }
+    outs->assign(nj, std::vector<DecOut>());
+    for (int j = 0; j < nj; ++j)
+        for (int dd = 0; dd < K; ++dd) {
+            DecOut o = dec[j * K + dd].o;
+            o.failed = o.status == 2;
+            (*outs)[j].push_back(std::move(o));
+        }
+}
+
 }  // namespace
 
 std::vector<int> non_speech_tokens(const Vocab& v) {
@@ -133,7 +246,8 @@ void whisper_full_batch(Engine& e, const Vocab* vocab, const std::vector<const f
         std::vector<int> pending = act;
         for (size_t it = 0; it < temps.size() && !pending.empty(); ++it) {
             const float t_cur = temps[it];
-            const int ndec = t_cur > 0.0f ? ndec_hot : 1;
+            const bool beam = p.beam_size > 1 && t_cur == 0.0f;  // WHISPER_SAMPLING_BEAM_SEARCH
+            const int ndec = beam ? std::min(p.beam_size, cap) : t_cur > 0.0f ? ndec_hot : 1;
             // prompt_past conditioning: [prev] + the last min(n_max_text_ctx, n_text_ctx / 2) tokens
             std::map<int, std::vector<int>> prefix;
             for (int u : pending) {
@@ -185,6 +299,21 @@ void whisper_full_batch(Engine& e, const Vocab* vocab, const std::vector<const f
                             if (P > 0) rq.row_prefix.push_back(prefix[u]);
                             if (multi) rq.lang_tok.push_back(us[u].lang >= 0 ? us[u].lang : -(j * ndec + 1));
                         }
+                    }
+                    if (beam) {
+                        rq.beam_k = ndec;
+                        std::vector<std::vector<DecOut>> bo;
+                        std::vector<int> lang;
+                        run_beam(e, rq, ptr, ns, nj, ndec, rq.seek, rq.seek_end, p, sp, n_max, &bo, &lang);
+                        for (int j = 0; j < nj; ++j) {
+                            const int u = grp[g0 + j];
+                            if (multi && us[u].lang < 0) {
+                                us[u].lang = lang[j * ndec];
+                                (*out)[u].lang_tok = us[u].lang;
+                            }
+                            res[u] = std::move(bo[j]);
+                        }
+                        continue;
                     }
                     const int S = rq.n_steps;
                     std::vector<int> tok((size_t)B * S), lang(B, -1), state((size_t)B * 4);

@@ -22,7 +22,7 @@ namespace spt {
 class Engine;
 class Vocab;
 
-struct FullParams {  // whisper_full_params (greedy strategy)
+struct FullParams {  // whisper_full_params
     bool no_timestamps = false;
     bool suppress_blank = true;
     bool suppress_nst = false;    // suppress_non_speech_tokens (needs a vocabulary)
@@ -30,6 +30,7 @@ struct FullParams {  // whisper_full_params (greedy strategy)
     float temperature = 0.0f;
     float temperature_inc = 0.2f;  // 0: no fallback
     int best_of = 5;               // decoders per window at temperature > 0
+    int beam_size = 1;             // > 1: beam search at temperature 0 (WHISPER_SAMPLING_BEAM_SEARCH)
     float entropy_thold = 2.4f;
     float logprob_thold = -1.0f;
     float max_initial_ts = 1.0f;

@@ -234,7 +234,136 @@ __global__ __launch_bounds__(TW) void finalize_ts_kernel(TsArgs a) {
     }
 }
 
+// Beam search (whisper_full, WHISPER_SAMPLING_BEAM_SEARCH at temperature 0): the same
+// whisper_process_logits rules for each decoder row, then its k best candidates by processed
+// logit (ties: lower id) with their log-probabilities (before the timestamp rule's text mask)
+// and the row's most probable timestamp.  Decoder state comes from the host per step: row
+// state {last token, previous token, has_ts, seek_delta}, step index.
+__global__ __launch_bounds__(TW) void beam_topk_kernel(BeamArgs a) {
+    __shared__ MaxI s_m[2][TW / 64];
+    __shared__ float s_s[TW / 64];
+    __shared__ MaxI s_k[TW / 64];
+    __shared__ int s_ids[8];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int step = a.step[0];
+    const TsParams& P = *a.prm;
+    const int V = a.n_vocab, beg = a.beg, eot = a.eot;
+    const float* lg = a.logits + (size_t)b * a.ldl;
+    const int last = a.row[4 * b + 0], pen = a.row[4 * b + 1], has_ts = a.row[4 * b + 2], seek_delta = a.row[4 * b + 3];
+    const bool last_ts = step > 0 && last >= beg;
+    const bool pen_ts = step < 2 || pen >= beg;
+    auto masked = [&](int n) -> bool {
+        if ((a.suppress[n >> 5] >> (n & 31)) & 1u) return true;
+        if (step == 0 && P.suppress_blank && (n == eot || n == a.blank)) return true;
+        if (n >= beg) {
+            if (P.no_ts) return true;
+            if (last_ts && pen_ts) return true;
+            if (step == 0 && P.max_initial >= 0 && n > beg + P.max_initial) return true;
+            if (has_ts && n < beg + seek_delta / 2) return true;
+        } else if (n < eot && last_ts && !pen_ts) {
+            return true;
+        }
+        return false;
+    };
+    MaxI mt{-INFINITY, 0x7fffffff}, ms{-INFINITY, 0x7fffffff};
+    for (int n = tid; n < V; n += TW) {
+        if (masked(n)) continue;
+        const MaxI c{lg[n], n};
+        if (n < beg) mt = max_merge(mt, c);
+        else ms = max_merge(ms, c);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mt = max_merge(mt, MaxI{__shfl_xor(mt.v, o, 64), __shfl_xor(mt.i, o, 64)});
+        ms = max_merge(ms, MaxI{__shfl_xor(ms.v, o, 64), __shfl_xor(ms.i, o, 64)});
+    }
+    if (lane == 0) { s_m[0][wv] = mt; s_m[1][wv] = ms; }
+    __syncthreads();
+    mt = s_m[0][0];
+    ms = s_m[1][0];
+    for (int w = 1; w < TW / 64; ++w) { mt = max_merge(mt, s_m[0][w]); ms = max_merge(ms, s_m[1][w]); }
+    const float M = fmaxf(mt.v, ms.v);
+    float sa = 0.0f, st = 0.0f;
+    if (M > -INFINITY)
+        for (int n = tid; n < V; n += TW) {
+            if (masked(n)) continue;
+            sa += expf(lg[n] - M);
+            if (n >= beg) st += expf(lg[n] - ms.v);
+        }
+    sa = wave_sum(sa);
+    st = wave_sum(st);
+    __shared__ float s_t[TW / 64];
+    if (lane == 0) { s_s[wv] = sa; s_t[wv] = st; }
+    __syncthreads();
+    float za = 0.0f, zt = 0.0f;
+    for (int w = 0; w < TW / 64; ++w) { za += s_s[w]; zt += s_t[w]; }
+    const float lse = logf(za) + M;
+    const float ts_lp = zt > 0.0f ? logf(zt) + ms.v - lse : -INFINITY;
+    const bool rule = ms.v > -INFINITY && ts_lp > mt.v - lse;
+    // k rounds of a block argmax over the candidates not taken yet
+    const int k = a.k;
+    for (int r = 0; r < k; ++r) {
+        MaxI c{-INFINITY, 0x7fffffff};
+        for (int n = tid; n < V; n += TW) {
+            if (masked(n) || (rule && n < beg)) continue;
+            bool taken = false;
+            for (int q = 0; q < r; ++q) taken = taken || s_ids[q] == n;
+            if (!taken) c = max_merge(c, MaxI{lg[n], n});
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c = max_merge(c, MaxI{__shfl_xor(c.v, o, 64), __shfl_xor(c.i, o, 64)});
+        if (lane == 0) s_k[wv] = c;
+        __syncthreads();
+        if (tid == 0) {
+            MaxI m = s_k[0];
+            for (int w = 1; w < TW / 64; ++w) m = max_merge(m, s_k[w]);
+            const bool ok = m.v > -INFINITY && m.i < V;
+            s_ids[r] = ok ? m.i : -1;
+            a.cand_id[b * 8 + r] = ok ? m.i : -1;
+            a.cand_lp[b * 8 + r] = ok ? lg[m.i] - lse : -INFINITY;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) a.tid[b] = ms.v > -INFINITY ? ms.i : 0;
+}
+
+// self-K/V rows of the next beam step: dst row b <- src row src[b], positions [0, n_pos)
+template <typename T>
+__global__ __launch_bounds__(256) void kv_gather_kernel(const T* __restrict__ src, T* __restrict__ dst,
+                                                        const int* __restrict__ rows, int L, int B, int H, int ctx,
+                                                        const DecState* __restrict__ ds) {
+    const int n_pos = ds->pos0;
+    const int64_t per = (int64_t)n_pos * 64 / (16 / sizeof(T));  // 16-byte chunks per (l, kv, b, h)
+    const int64_t total = (int64_t)L * 2 * B * H * per;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int64_t c = i % per;
+        int64_t r = i / per;
+        const int h = (int)(r % H); r /= H;
+        const int b = (int)(r % B); r /= B;  // r = l * 2 + kv
+        const int64_t dst_off = ((r * B + b) * H + h) * (int64_t)ctx * 64;
+        const int64_t src_off = ((r * B + rows[b]) * H + h) * (int64_t)ctx * 64;
+        ((uint4*)(dst + dst_off))[c] = ((const uint4*)(src + src_off))[c];
+    }
+}
+
 }  // namespace
+
+void dec_beam_topk(const BeamArgs& a, int B, hipStream_t st) {
+    if (a.k < 1 || a.k > 8) throw std::runtime_error("beam_topk: 1..8 candidates");
+    hipLaunchKernelGGL(beam_topk_kernel, dim3(B), dim3(TW), 0, st, a);
+    SPT_LAUNCH_CHECK();
+}
+
+void dec_kv_gather(int dtype, const void* src, void* dst, const int* rows, int L, int B, int H, int ctx,
+                   const DecState* ds, hipStream_t st) {
+    if (dtype == DT_BF16)
+        hipLaunchKernelGGL(kv_gather_kernel<bf16>, dim3(2048), dim3(256), 0, st, (const bf16*)src, (bf16*)dst, rows, L, B,
+                           H, ctx, ds);
+    else
+        hipLaunchKernelGGL(kv_gather_kernel<float>, dim3(2048), dim3(256), 0, st, (const float*)src, (float*)dst, rows, L,
+                           B, H, ctx, ds);
+    SPT_LAUNCH_CHECK();
+}
 
 void dec_finalize_ts(int dtype, const TsArgs& a, int B, hipStream_t st) {
     if (dtype == DT_BF16) hipLaunchKernelGGL(finalize_ts_kernel<bf16>, dim3(B), dim3(TW), 0, st, a);

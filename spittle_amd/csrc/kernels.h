@@ -154,6 +154,22 @@ struct TsArgs {
 };
 // whisper_process_logits + whisper_sample_token + per-decoder bookkeeping (k_sample.hip)
 void dec_finalize_ts(int dtype, const TsArgs& a, int B, hipStream_t st);
+// beam search: the k best processed candidates of each decoder row (k_sample.hip)
+struct BeamArgs {
+    const float* logits; int ldl;
+    int n_vocab, eot, beg, blank;
+    const uint32_t* suppress;
+    const TsParams* prm;
+    const int* row;    // [B][4] last token, previous token, has_ts, seek_delta
+    const int* step;   // [1] index of the token being chosen
+    int k;             // 1..8
+    int* cand_id; float* cand_lp;  // [B][8]
+    int* tid;          // [B] most probable timestamp (0: none)
+};
+void dec_beam_topk(const BeamArgs& a, int B, hipStream_t st);
+// self-K/V cache rows for the next beam step: dst row b <- src row rows[b], positions < pos0
+void dec_kv_gather(int dtype, const void* src, void* dst, const int* rows, int L, int B, int H, int ctx,
+                   const DecState* ds, hipStream_t st);
 // pos0 += n (after a prefill pass that produces no token)
 void dec_advance(DecState* ds, int n, hipStream_t st);
 

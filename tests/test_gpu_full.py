@@ -122,3 +122,29 @@ def test_no_timestamps_fallback_path(tiny):
         p = W.Params(no_timestamps=True, max_tokens=20)
         wins, segs, toks, _ = W.transcribe(om, x, p)
         _compare(r, wins, segs, toks)
+
+
+@pytest.mark.parametrize("beam,seconds,seed", [(3, 8, 90), (5, 20, 91)])
+def test_beam_search(tiny, beam, seconds, seed):
+    """beam_size > 1 (WHISPER_SAMPLING_BEAM_SEARCH at temperature 0): each live decoder proposes
+    its beam_size best candidates, the utterance's candidates are ranked by cumulative
+    log-probability, decoders take them in order, K/V rows follow their source decoder; the best
+    non-failed decoder by average log-probability wins."""
+    e, om = tiny
+    x = O.synth_audio(seed, int(seconds * 16000))
+    r = e.transcribe_samples(x, _params(beam_size=beam, max_new_tokens=16))
+    wins, segs, toks, kept = W.transcribe(om, x, W.Params(max_tokens=16, beam_size=beam))
+    if _compare(r, wins, segs, toks):
+        for i, s in enumerate(kept):
+            assert abs(r.top1[i] - s.plog) < GAP and int(r.top2[i]) == s.tid, i
+    g = e.transcribe_samples(x, _params(beam_size=1, max_new_tokens=16))
+    assert g.n_windows >= 1 and r.n_windows >= 1
+
+
+def test_beam_needs_rows():
+    from spittle_amd import TranscriptionError, WhisperEngine, WhisperModelParams
+    e = WhisperEngine(WhisperModelParams(dtype="f32", max_batch=2, seed=SEED))
+    e.load_model("synthetic:tiny.en:enc=1:dec=1")
+    with pytest.raises(TranscriptionError, match="beam_size exceeds"):
+        e.transcribe_samples(O.synth_audio(1, 32000), _params(beam_size=3))
+    e.unload_model()
