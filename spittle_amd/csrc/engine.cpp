@@ -131,10 +131,10 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     if ((3 * cp_ * esz_) % 128) cp_ = ((dm_.n_mels + 127) / 128) * 128;
     if (const char* g = getenv("SPT_DECODE_GROUPS")) n_groups_ = std::max(1, std::min(2, atoi(g)));
     if (const char* v = getenv("SPT_XATTN_SPLIT")) xsplit_ = std::max(1, std::min(4, atoi(v)));
-    // cross-attention key split / waves per workgroup: fixed per engine (never per batch)
-    // projection K splits (self-out: 2, fc2: 4; fixed per engine, never per batch). The pending-
-    // slab count a LayerNorm prologue sums is a kernel template constant: 2 after the self-out
-    // projection, 4 after fc2.
+    // cross-attention key split: fixed per engine (never per batch).  Projection K splits
+    // (self-out: 2, fc2: 2; r1 exp14 measured fc2 at 2 slightly faster per layer than 4: the
+    // next QKV LayerNorm prologue sums fewer slabs) are fixed per engine too; the pending-slab
+    // count a LayerNorm prologue sums is a kernel template constant.
     select();
     HIP_CHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     ev_.resize(8);

@@ -402,10 +402,12 @@ void gemv_launch_cfg(const GemvArgs& a, hipStream_t st) {
 // the (mode, A source) pairs the decoder uses
 #define SPT_GV_PAIRS(X)                 \
     X(GV_QKV_CACHE, LN_SRC(0))          \
+    X(GV_QKV_CACHE, LN_SRC(2))          \
     X(GV_QKV_CACHE, LN_SRC(4))          \
     X(GV_BIAS, LN_SRC(2))               \
     X(GV_BIAS_GELU, LN_SRC(0))          \
     X(GV_LOGITS, LN_SRC(0))             \
+    X(GV_LOGITS, LN_SRC(2))             \
     X(GV_LOGITS, LN_SRC(4))             \
     X(GV_PARTIAL, A_DIRECT)             \
     X(GV_BIAS_RESID, A_DIRECT)          \

@@ -205,9 +205,10 @@ int main(int argc, char** argv) {
         };
         // the engine's layer (Engine::enqueue_decoder_pass): 8 launches, pending slabs after the
         // self-out (2) and fc2 (4) projections; the chain starts with fc2's 4 slabs pending
+        const int fs = getenv("FC2S") ? atoi(getenv("FC2S")) : 4;  // fc2 K split (pending slabs)
         auto layer = [&](const Chain& c, hipStream_t s) {
             float *xc = c.x, *xo = c.x2;
-            int np = 4;
+            int np = fs;
             auto ln_input = [&](GemvArgs& a) {
                 a.A = xc;
                 for (int p = 0; p < kMaxPend; ++p) a.pend[p] = p < np ? c.pend + (size_t)p * B * d : zero;
@@ -243,7 +244,7 @@ int main(int argc, char** argv) {
             consumed();
             a = GemvArgs{};
             a.A = c.ff; a.lda = 4 * d; a.R = B; a.W = w2; a.N = d; a.K = 4 * d; a.bias = b4;
-            a.C = c.pend; a.ldc = d; a.c_split = (int64_t)B * d; a.ksplit = 4; np = 4;
+            a.C = c.pend; a.ldc = d; a.c_split = (int64_t)B * d; a.ksplit = fs; np = fs;
             gemv(dt, GV_PARTIAL, A_DIRECT, a, s);
         };
         const double bytes = (14.0 * d * d) * esz + 2.0 * B * H * (T + 129) * 64 * esz;
