@@ -205,10 +205,11 @@ int main(int argc, char** argv) {
         };
         // the engine's layer (Engine::enqueue_decoder_pass): 8 launches, pending slabs after the
         // self-out (2) and fc2 (4) projections; the chain starts with fc2's 4 slabs pending
-        const int fs = getenv("FC2S") ? atoi(getenv("FC2S")) : 4;  // fc2 K split (pending slabs)
+        const int fs = getenv("FC2S") ? atoi(getenv("FC2S")) : 2;  // fc2 K split (pending slabs)
+        const int sos = getenv("SOS") ? atoi(getenv("SOS")) : 2;   // self-out K split
         auto layer = [&](const Chain& c, hipStream_t s) {
             float *xc = c.x, *xo = c.x2;
-            int np = fs;
+            int np = fs > 1 ? fs : 0;
             auto ln_input = [&](GemvArgs& a) {
                 a.A = xc;
                 for (int p = 0; p < kMaxPend; ++p) a.pend[p] = p < np ? c.pend + (size_t)p * B * d : zero;
@@ -225,8 +226,13 @@ int main(int argc, char** argv) {
             dec_self_attn(dt, c.q, c.skv, B, H, ctx, 1, c.ds, c.ao, s);
             a = GemvArgs{};
             a.A = c.ao; a.lda = d; a.R = B; a.W = wo; a.N = d; a.K = d; a.bias = b4;
-            a.C = c.pend; a.ldc = d; a.c_split = (int64_t)B * d; a.ksplit = 2; np = 2;
-            gemv(dt, GV_PARTIAL, A_DIRECT, a, s);
+            if (sos > 1) {
+                a.C = c.pend; a.ldc = d; a.c_split = (int64_t)B * d; a.ksplit = sos; np = sos;
+                gemv(dt, GV_PARTIAL, A_DIRECT, a, s);
+            } else {  // straight into the residual
+                a.C = xc; a.ldc = d;
+                gemv(dt, GV_BIAS_RESID, A_DIRECT, a, s);
+            }
             a = GemvArgs{};
             ln_input(a); a.lda = d; a.ln_w = lnw; a.ln_b = lnb; a.R = B;
             a.W = wq; a.N = d; a.K = d; a.bias = b4; a.C = c.q; a.ldc = d;
@@ -244,8 +250,13 @@ int main(int argc, char** argv) {
             consumed();
             a = GemvArgs{};
             a.A = c.ff; a.lda = 4 * d; a.R = B; a.W = w2; a.N = d; a.K = 4 * d; a.bias = b4;
-            a.C = c.pend; a.ldc = d; a.c_split = (int64_t)B * d; a.ksplit = fs; np = fs;
-            gemv(dt, GV_PARTIAL, A_DIRECT, a, s);
+            if (fs > 1) {
+                a.C = c.pend; a.ldc = d; a.c_split = (int64_t)B * d; a.ksplit = fs; np = fs;
+                gemv(dt, GV_PARTIAL, A_DIRECT, a, s);
+            } else {
+                a.C = xc; a.ldc = d;
+                gemv(dt, GV_BIAS_RESID, A_DIRECT, a, s);
+            }
         };
         const double bytes = (14.0 * d * d) * esz + 2.0 * B * H * (T + 129) * 64 * esz;
         Chain c0 = mk(0);
