@@ -99,7 +99,9 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16* __restric
         for (int r = 0; r < 16; ++r) mloc = fmaxf(mloc, fmaxf(s[0][r], s[1][r]));
         mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
         const float m_new = fmaxf(m_run, mloc);
-        const float alpha = exp2f((m_run - m_new) * kScaleLog2);
+        // v_exp_f32 directly: exp2f's denormal-range fix-up (cmp / cndmask / ldexp per score)
+        // only matters for probabilities below 2^-126 of the running maximum
+        const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * kScaleLog2);
         const float mc = m_new * kScaleLog2;
         float lsum = 0.f;
         bf16x8 pf[2][2];
@@ -107,7 +109,7 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16* __restric
         for (int kt2 = 0; kt2 < 2; ++kt2)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float p = exp2f(s[kt2][r] * kScaleLog2 - mc);
+                const float p = __builtin_amdgcn_exp2f(s[kt2][r] * kScaleLog2 - mc);
                 lsum += p;
                 pf[kt2][r >> 3][r & 7] = (short)f2bf(p);
             }
