@@ -27,6 +27,13 @@ __device__ __forceinline__ void glds16(const void* g, SPT_LDS void* l) {
     __builtin_amdgcn_global_load_lds((const void*)g, l, 16, 0, 0);
 }
 
+// one v_max3_f32 (the compiler does not form it from fmaxf chains here)
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+    float r;
+    asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 __device__ __forceinline__ int key_of(int kt2, int r, int hf) { return 32 * kt2 + (r & 3) + 8 * (r >> 2) + 4 * hf; }
 
 // -------------------------------------------------------------------- bf16
@@ -96,23 +103,34 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16* __restric
         }
         float mloc = -INFINITY;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) mloc = fmaxf(mloc, fmaxf(s[0][r], s[1][r]));
+        for (int r = 0; r < 16; ++r) mloc = max3f(mloc, s[0][r], s[1][r]);
         mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
         const float m_new = fmaxf(m_run, mloc);
         // v_exp_f32 directly: exp2f's denormal-range fix-up (cmp / cndmask / ldexp per score)
         // only matters for probabilities below 2^-126 of the running maximum
         const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * kScaleLog2);
         const float mc = m_new * kScaleLog2;
-        float lsum = 0.f;
+        // scores in pairs: packed f32 FMA / add (v_pk_fma_f32, v_pk_add_f32) and one
+        // v_cvt_pk_bf16_f32 per pair straight into the P^T fragment dwords
+        const f32x2 sc2 = {kScaleLog2, kScaleLog2}, mc2 = {-mc, -mc};
+        f32x2 ls2 = {0.f, 0.f};
+        union { bf16x8 v; uint32_t w[4]; } pu[2][2];
+#pragma unroll
+        for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+                const f32x2 sv = {s[kt2][r], s[kt2][r + 1]};
+                const f32x2 t = __builtin_elementwise_fma(sv, sc2, mc2);
+                const f32x2 pv = {__builtin_amdgcn_exp2f(t[0]), __builtin_amdgcn_exp2f(t[1])};
+                ls2 += pv;
+                pu[kt2][r >> 3].w[(r & 7) >> 1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pv, bf16x2v));
+            }
+        const float lsum = ls2[0] + ls2[1];
         bf16x8 pf[2][2];
 #pragma unroll
         for (int kt2 = 0; kt2 < 2; ++kt2)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float p = __builtin_amdgcn_exp2f(s[kt2][r] * kScaleLog2 - mc);
-                lsum += p;
-                pf[kt2][r >> 3][r & 7] = (short)f2bf(p);
-            }
+            for (int sp = 0; sp < 2; ++sp) pf[kt2][sp] = pu[kt2][sp].v;
         l_run = l_run * alpha + lsum;
         m_run = m_new;
 #pragma unroll
