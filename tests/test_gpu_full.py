@@ -148,3 +148,30 @@ def test_beam_needs_rows():
     with pytest.raises(TranscriptionError, match="beam_size exceeds"):
         e.transcribe_samples(O.synth_audio(1, 32000), _params(beam_size=3))
     e.unload_model()
+
+
+def test_full_batch_invariance(tiny):
+    """whisper_full over a batch of utterances (different lengths, so different seek paths)
+    gives each utterance the result it gets alone."""
+    e, _ = tiny
+    xs = [O.synth_audio(100, 9 * 16000), O.synth_audio(101, 40 * 16000), O.synth_audio(102, 3 * 16000)]
+    p = _params(max_new_tokens=12)
+    batch = e.transcribe_batch(xs, p)
+    for x, rb in zip(xs, batch):
+        ra = e.transcribe_samples(x, p)
+        assert ra.tokens == rb.tokens and ra.text == rb.text and ra.n_windows == rb.n_windows
+        assert [(s.start, s.end, s.text) for s in ra.segments] == [(s.start, s.end, s.text) for s in rb.segments]
+
+
+def test_full_language_autodetect():
+    """language=None on the whisper_full path detects once per utterance (first window) and
+    reports the same language as the fast path's detection."""
+    from spittle_amd import WhisperEngine, WhisperModelParams
+    e = WhisperEngine(WhisperModelParams(dtype="f32", max_batch=4, seed=SEED))
+    e.load_model("synthetic:tiny:enc=2:dec=3")
+    xs = [O.synth_audio(110 + i, 12 * 16000) for i in range(2)]
+    full = e.transcribe_batch(xs, _params(language=None, max_new_tokens=8))
+    fast = e.transcribe_batch(xs, _params(language=None, no_timestamps=True, ignore_eot=True, max_new_tokens=2))
+    for a, b in zip(full, fast):
+        assert a.language is not None and a.language == b.language
+    e.unload_model()

@@ -204,3 +204,43 @@ def test_missing_or_misshapen_tensor(tmp_path):
     mf = ModelFile(tmp_path, "tiny.en", G.F16, 1, 1, override={"encoder.blocks.0.mlp.0.weight": (G.F16, [384, 384])})
     with pytest.raises(TranscriptionError, match="encoder.blocks.0.mlp.0.weight has 147456 elements"):
         _engine(mf.path)
+
+
+NST = ["\"", "#", "(", ")", "*", "+", "/", ":", ";", "<", "=", ">", "@", "[", "\\", "]", "^", "_", "`", "{", "|",
+       "}", "~", "「", "」", "『", "』", "<<", ">>", "<<<", ">>>", "--", "---", "-(", "-[", "('", "(\"", "((", "))",
+       "(((", ")))", "[[", "]]", "{{", "}}", "♪♪", "♪♪♪", "♩", "♪", "♫", "♬", "♭", "♮", "♯"]
+
+
+def test_whisper_full_with_vocabulary(tiny_f32):
+    """The whisper_full path on a ggml model: suppress_non_speech_tokens keeps every non-speech
+    token (whisper_process_logits' list, with and without a leading space, plus " -" and " '")
+    out of the result; initial_prompt equals passing its tokens; segment texts are vocabulary
+    strings and the result text is their trimmed concatenation."""
+    e = _engine(tiny_f32.path)
+    ids = {}
+    for i, w in enumerate(tiny_f32.full_vocab):
+        ids[w] = i  # later duplicates win, as in the loader
+    nst = set()
+    for t in NST:
+        for w in (t.encode(), b" " + t.encode()):
+            if w in ids:
+                nst.add(ids[w])
+    for w in (b" -", b" '"):
+        if w in ids:
+            nst.add(ids[w])
+    assert len(nst) > 10
+    from spittle_amd import WhisperInferenceParams
+    x = O.synth_audio(120, 15 * 16000)
+    base = dict(language="en", temperature_inc=0.0, max_new_tokens=30)
+    r = e.transcribe_samples(x, WhisperInferenceParams(suppress_non_speech_tokens=True, **base))
+    assert not (set(r.tokens) & nst)
+    prompt = "Kubernetes, PostgreSQL, gRPC"
+    a = e.transcribe_samples(x, WhisperInferenceParams(initial_prompt=prompt, **base))
+    b = e.transcribe_samples(x, WhisperInferenceParams(prompt_tokens=e.tokenize(prompt), **base))
+    assert a.tokens == b.tokens and a.text == b.text
+    eot = tiny_f32.sp["eot"]
+    for s in a.segments:
+        toks = a.tokens[s.i0:s.i0 + s.n_tokens]
+        assert s.text == b"".join(tiny_f32.full_vocab[t] for t in toks if t < eot).decode("utf-8", "replace")
+    assert a.text == "".join(s.text for s in a.segments).strip()
+    e.unload_model()
