@@ -706,21 +706,22 @@ __global__ __launch_bounds__(64 * NW) void cross_attn_kernel(const T* __restrict
 // Per sequence: reduce the logits tiles' top-2, record the token, choose the next
 // input (argmax or forced), embed it for the next pass; the last block advances
 // the step state (every block reads it before arriving).
+constexpr int FIN_T = 1024;  // finalize threads per sequence: the 3.2k top-2 partials in ~3 loads each
 template <typename T>
-__global__ __launch_bounds__(256) void finalize_kernel(FinalizeArgs a) {
-    __shared__ TopP s_top[4];
+__global__ __launch_bounds__(FIN_T) void finalize_kernel(FinalizeArgs a) {
+    __shared__ TopP s_top[FIN_T / 64];
     __shared__ int s_tok;
     const int b = blockIdx.x, tid = threadIdx.x;
     const int step = a.ds->step, pos0 = a.ds->pos0;
     TopP t{-INFINITY, 0x7fffffff, -INFINITY, 0};
     const TopP* p = (const TopP*)a.part + (size_t)b * a.n_tiles;
-    for (int i = tid; i < a.n_tiles; i += 256) t = top_merge(t, p[i]);
+    for (int i = tid; i < a.n_tiles; i += FIN_T) t = top_merge(t, p[i]);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) t = top_merge(t, top_shfl(t, o));
     if ((tid & 63) == 0) s_top[tid >> 6] = t;
     __syncthreads();
     if (tid == 0) {
-        for (int w = 1; w < 4; ++w) t = top_merge(t, s_top[w]);
+        for (int w = 1; w < FIN_T / 64; ++w) t = top_merge(t, s_top[w]);
         // non-finite logits leave no valid winner: record the sentinel, never index with it
         if (t.i1 < 0 || t.i1 >= a.n_vocab) {
             t.i1 = -2;
@@ -751,7 +752,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(FinalizeArgs a) {
     const int pn = min(pos0 + a.Tq, a.ctx - 1);
     const T* e = (const T*)a.emb + (size_t)tok * a.d;
     const float* pp = a.pos + (size_t)pn * a.d;
-    for (int i = tid; i < a.d; i += 256) a.x[(size_t)b * a.d + i] = to_f<T>(e[i]) + pp[i];
+    for (int i = tid; i < a.d; i += FIN_T) a.x[(size_t)b * a.d + i] = to_f<T>(e[i]) + pp[i];
     if (tid == 0) {
         const unsigned prev = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         if (prev == (unsigned)gridDim.x - 1) {
@@ -852,8 +853,8 @@ void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int B_layou
 }
 
 void dec_finalize(int dtype, const FinalizeArgs& a, int B, hipStream_t st) {
-    if (dtype == DT_BF16) hipLaunchKernelGGL(finalize_kernel<bf16>, dim3(B), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(finalize_kernel<float>, dim3(B), dim3(256), 0, st, a);
+    if (dtype == DT_BF16) hipLaunchKernelGGL(finalize_kernel<bf16>, dim3(B), dim3(FIN_T), 0, st, a);
+    else hipLaunchKernelGGL(finalize_kernel<float>, dim3(B), dim3(FIN_T), 0, st, a);
 }
 
 void dec_advance(DecState* ds, int n, hipStream_t st) {
