@@ -43,6 +43,10 @@ def parse():
     ap.add_argument("--decode-steps", type=int, default=N_STEPS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-steps", type=int, default=4)
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL) for the real run; gloo only to rehearse N > 1 ranks on one GPU")
+    ap.add_argument("--no-weight-bcast", action="store_true",
+                    help="N > 1: every rank loads the model itself instead of rank 0 + RCCL broadcast")
     return ap.parse_args()
 
 
@@ -127,12 +131,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        local %= max(1, torch.cuda.device_count())  # rehearsal: several ranks on one GPU (gloo)
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
     dev = torch.device("cuda", local)
 
     from spittle_amd import WhisperEngine, WhisperInferenceParams, WhisperModelParams
-    from spittle_amd.dist import max_over_ranks, shard_range
+    from spittle_amd.dist import broadcast_weights, max_over_ranks, shard_range
     from spittle_amd.synth import synth_audio
 
     B = args.batch
@@ -142,8 +150,18 @@ def main():
     pcm_dev = torch.from_numpy(pcm).to(dev)
     torch.cuda.synchronize()
 
-    eng = WhisperEngine(WhisperModelParams(dtype=args.dtype, device=local, max_batch=B, seed=1234))
+    # N > 1: rank 0 loads (generates / dequantises) the weights, one RCCL broadcast over xGMI
+    # replicates its arena into the other ranks' engines; outside the timed region
+    bcast = world > 1 and not args.no_weight_bcast
+    eng = WhisperEngine(WhisperModelParams(dtype=args.dtype, device=local, max_batch=B, seed=1234,
+                                           external_weights=bcast and rank != 0))
     eng.load_model(args.model)
+    wload = None
+    if bcast:
+        bi = broadcast_weights(eng, device=dev)
+        bms = max_over_ranks(bi["ms"], device=dev)
+        wload = {"mode": "rank 0 load + " + ("RCCL" if args.dist_backend == "nccl" else args.dist_backend) + " broadcast", "bytes": bi["bytes"], "ms": round(bms, 3),
+                 "GB/s": round(bi["bytes"] / bms / 1e6, 1) if bms > 0 else None}
     info = eng.info()
     params = WhisperInferenceParams(language="en", no_timestamps=True, temperature_inc=0.0, ignore_eot=True, max_new_tokens=args.decode_steps)
     lens = [pcm.shape[1]] * B
@@ -192,6 +210,8 @@ def main():
             "phases_ms": {k: round(v, 3) for k, v in phases.items() if k.endswith("_ms")},
             "roofline": roof, "kernels": kernels, "cpu_baseline": cpu,
         }
+        if wload:
+            out["weight_load"] = wload
         print(json.dumps(out), flush=True)
     eng.unload_model()
     if world > 1:

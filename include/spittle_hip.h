@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 3
+#define SPT_ABI_VERSION 4
 
 typedef enum {
     SPT_OK = 0,
@@ -57,9 +57,14 @@ typedef struct {
     int32_t dtype;        /* spt_dtype: weights + activations (accumulation is always f32) */
     int32_t device;       /* HIP device ordinal */
     int32_t max_batch;    /* utterance (30 s window) capacity per call */
-    int32_t reserved;
+    uint32_t flags;       /* SPT_MODEL_* (ABI <= 3: reserved, always 0) */
     uint64_t seed;        /* synthetic weights: PRNG seed */
 } spt_model_params;
+
+/* spt_model_params.flags */
+#define SPT_MODEL_WEIGHTS_EXTERNAL 1u  /* allocate the weight arena but do not generate / dequantise
+                                          into it: spt_weights_import fills it (a multi-GPU load
+                                          where rank 0 loads and RCCL broadcasts the arena) */
 
 typedef struct {
     const char* language;        /* ISO-639-1 ("en", "zh", ...); NULL or "auto" = auto-detect
@@ -167,6 +172,18 @@ spt_status spt_tokenize(spt_ctx* ctx, const char* text, int32_t* tokens, int32_t
 const char* spt_token_to_str(const spt_ctx* ctx, int32_t id);
 
 spt_status spt_get_timings(const spt_ctx* ctx, spt_timings* t);
+
+/* Multi-GPU load: the weight arena is one device allocation whose layout is a
+ * pure function of (model, dtype), spt_model_info.weight_bytes long.  Rank 0 loads the model
+ * (file parse + device dequantisation) and exports the arena into a device buffer; the buffer
+ * is broadcast over RCCL/xGMI; every other rank, created with SPT_MODEL_WEIGHTS_EXTERNAL on the
+ * same model spec, imports it.  Both are synchronous device-to-device copies on the context's
+ * device; bytes must equal weight_bytes (else SPT_ERR_INVALID_ARG).  A context created with
+ * SPT_MODEL_WEIGHTS_EXTERNAL fails every transcription with SPT_ERR_INVALID_ARG until the
+ * import.  The reference loads each engine from disk (transcription.rs:261-276) and has no
+ * multi-device path; these two entry points exist for the replica-parallel load only. */
+spt_status spt_weights_export(spt_ctx* ctx, void* dev_dst, size_t bytes);
+spt_status spt_weights_import(spt_ctx* ctx, const void* dev_src, size_t bytes);
 
 /* Kernel probe (measurement): re-launch one hot-path kernel `iters` times on the engine
  * stream, on the buffers of the last call.  Decoder kernels (kinds 0-3) are timed between two

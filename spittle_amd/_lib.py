@@ -24,14 +24,16 @@ EXPORTS = [
     "spt_transcribe_batch_device", "spt_result_free", "spt_get_timings", "spt_debug_mel",
     "spt_debug_encode", "spt_debug_weight_checksum", "spt_probe_kernel", "spt_language_code",
     "spt_tokenize", "spt_token_to_str", "spt_debug_ggml_tokenize", "spt_debug_ggml_dequant",
+    "spt_weights_export", "spt_weights_import",
 ]
+SPT_MODEL_WEIGHTS_EXTERNAL = 1
 PROBES = {"dec_cross_attn": 0, "dec_self_attn": 1, "dec_logits": 2, "dec_fc1": 3, "enc_fc1_gemm": 4,
           "enc_attn": 5}
 
 
 class ModelParams(C.Structure):
     _fields_ = [("dtype", C.c_int32), ("device", C.c_int32), ("max_batch", C.c_int32),
-                ("reserved", C.c_int32), ("seed", C.c_uint64)]
+                ("flags", C.c_uint32), ("seed", C.c_uint64)]
 
 
 class InferParams(C.Structure):
@@ -111,7 +113,9 @@ def load():
     L.spt_debug_weight_checksum.argtypes = [vp, C.c_int32, C.POINTER(C.c_double)]
     L.spt_probe_kernel.argtypes = [vp, C.c_int32, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                    C.POINTER(C.c_int32)]
-    for fn in ("spt_ctx_info", "spt_transcribe", "spt_transcribe_batch", "spt_transcribe_batch_device",
+    L.spt_weights_export.argtypes = [vp, C.c_void_p, C.c_size_t]
+    L.spt_weights_import.argtypes = [vp, C.c_void_p, C.c_size_t]
+    for fn in ("spt_weights_export", "spt_weights_import", "spt_ctx_info", "spt_transcribe", "spt_transcribe_batch", "spt_transcribe_batch_device",
                "spt_get_timings", "spt_debug_mel", "spt_debug_encode", "spt_debug_weight_checksum",
                "spt_probe_kernel", "spt_tokenize", "spt_debug_ggml_tokenize", "spt_debug_ggml_dequant"):
         getattr(L, fn).restype = C.c_int

@@ -333,7 +333,7 @@ spt_status run_windows(spt_ctx* c, std::vector<Window>& win, size_t n_utt, const
 
 extern "C" {
 
-const char* spt_version(void) { return "spittle_amd 0.4.0 (gfx950, ABI 3)"; }
+const char* spt_version(void) { return "spittle_amd 0.5.0 (gfx950, ABI 4)"; }
 
 const char* spt_language_code(int32_t lang_id) { return spt::lang_code(lang_id); }
 
@@ -375,6 +375,10 @@ spt_status spt_ctx_create(const char* model_spec, const spt_model_params* params
         set_err(err, errlen, "bad dtype");
         return SPT_ERR_INVALID_ARG;
     }
+    if (mp.flags & ~SPT_MODEL_WEIGHTS_EXTERNAL) {
+        set_err(err, errlen, "unknown spt_model_params.flags bits");
+        return SPT_ERR_INVALID_ARG;
+    }
     spt::ModelDims dm;
     uint64_t seed = mp.seed;
     std::string perr;
@@ -411,7 +415,7 @@ spt_status spt_ctx_create(const char* model_spec, const spt_model_params* params
     if (!c) return SPT_ERR_OOM;
     try {
         c->eng.reset(new Engine(dm, mp.dtype == SPT_DTYPE_BF16 ? spt::DT_BF16 : spt::DT_F32, mp.device,
-                                mp.max_batch, seed, file.get()));
+                                mp.max_batch, seed, file.get(), (mp.flags & SPT_MODEL_WEIGHTS_EXTERNAL) != 0));
         if (file) c->vocab.reset(new spt::Vocab(file->vocab(), dm.n_vocab, spt::specials_for(dm.n_vocab)));
     } catch (const std::exception& e) {
         set_err(err, errlen, e.what());
@@ -578,6 +582,26 @@ spt_status spt_get_timings(const spt_ctx* ctx, spt_timings* t) {
     t->mel_ms = m.mel_ms; t->encoder_ms = m.encoder_ms; t->cross_kv_ms = m.cross_kv_ms; t->decode_ms = m.decode_ms;
     t->total_ms = m.total_ms; t->h2d_ms = m.h2d_ms; t->n_decode_passes = m.n_decode_passes; t->batch = m.batch;
     return SPT_OK;
+}
+
+spt_status spt_weights_export(spt_ctx* ctx, void* dev_dst, size_t bytes) {
+    if (!ctx || !dev_dst) return fail(ctx, SPT_ERR_INVALID_ARG, "null argument");
+    try {
+        ctx->eng->export_weights(dev_dst, (int64_t)bytes);
+        return SPT_OK;
+    } catch (const std::exception& e) {
+        return fail(ctx, classify(e), e.what());
+    }
+}
+
+spt_status spt_weights_import(spt_ctx* ctx, const void* dev_src, size_t bytes) {
+    if (!ctx || !dev_src) return fail(ctx, SPT_ERR_INVALID_ARG, "null argument");
+    try {
+        ctx->eng->import_weights(dev_src, (int64_t)bytes);
+        return SPT_OK;
+    } catch (const std::exception& e) {
+        return fail(ctx, classify(e), e.what());
+    }
 }
 
 spt_status spt_debug_mel(spt_ctx* ctx, const float* pcm16k, size_t n_samples, float* out) {

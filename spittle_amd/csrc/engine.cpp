@@ -119,7 +119,8 @@ struct Carver {
 
 void Engine::select() const { HIP_CHECK(hipSetDevice(dev_)); }
 
-Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64_t seed, const GgmlFile* src)
+Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64_t seed, const GgmlFile* src,
+               bool external_weights)
     : dm_(dm), dt_(dtype), dev_(device), max_batch_(max_batch), seed_(seed) {
     if (dm_.d % 128 || dm_.d / 64 != dm_.n_head) throw std::runtime_error("unsupported model width");
     if (max_batch_ < 1 || max_batch_ > 64) throw std::runtime_error("max_batch must be in 1..64");
@@ -147,8 +148,15 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     try {
         gemv_prepare(dt_);
         alloc_weights();
-        if (src) load_ggml(*src);
-        else generate_weights();
+        if (external_weights) {
+            // filled later by import_weights; clear it so a premature use reads zeros, not garbage
+            HIP_CHECK(hipMemsetAsync(warena_, 0, wbytes_, st_));
+        } else if (src) {
+            load_ggml(*src);
+        } else {
+            generate_weights();
+        }
+        weights_ready_ = !external_weights;
         upload_tables(src ? &src->mel_filters() : nullptr);
         alloc_workspace();
         HIP_CHECK(hipStreamSynchronize(st_));
@@ -186,6 +194,32 @@ void Engine::release() {
 }
 
 // ----------------------------------------------------------------------------- weights
+void Engine::require_weights() const {
+    if (!weights_ready_)
+        throw std::runtime_error("weights not loaded: the context was created with SPT_MODEL_WEIGHTS_EXTERNAL and "
+                                 "spt_weights_import has not been called");
+}
+
+void Engine::export_weights(void* dev_dst, int64_t bytes) {
+    require_weights();
+    if (!dev_dst || bytes != wbytes_)
+        throw std::runtime_error("weight export: expected " + std::to_string(wbytes_) + " bytes, got " +
+                                 std::to_string(bytes));
+    select();
+    HIP_CHECK(hipMemcpyAsync(dev_dst, warena_, (size_t)wbytes_, hipMemcpyDeviceToDevice, st_));
+    HIP_CHECK(hipStreamSynchronize(st_));
+}
+
+void Engine::import_weights(const void* dev_src, int64_t bytes) {
+    if (!dev_src || bytes != wbytes_)
+        throw std::runtime_error("weight import: expected " + std::to_string(wbytes_) + " bytes (this model and dtype), got " +
+                                 std::to_string(bytes));
+    select();
+    HIP_CHECK(hipMemcpyAsync(warena_, dev_src, (size_t)wbytes_, hipMemcpyDeviceToDevice, st_));
+    HIP_CHECK(hipStreamSynchronize(st_));
+    weights_ready_ = true;
+}
+
 void Engine::alloc_weights() {
     const int64_t d = dm_.d, dd = d * d, V = dm_.n_vocab, L = dm_.n_dec;
     enc_.resize(dm_.n_enc);
@@ -1009,6 +1043,7 @@ void Engine::transcribe_device(const float* pcm_dev, int64_t stride, const int* 
                                const DecodeRequest& rq, int* tokens, float* top1, float* top2, int* lang_out,
                                int* ts_state_out) {
     select();
+    require_weights();
     if (B < 1 || B > max_batch_) throw std::runtime_error("batch exceeds the context's max_batch");
     for (int b = 0; b < B; ++b)
         if (n_samples[b] < 0 || n_samples[b] > 480000 || (int64_t)n_samples[b] > stride)
@@ -1054,6 +1089,7 @@ void Engine::stage_pcm(const float* const* pcm, const int* n, int B) {
 void Engine::transcribe_host(const float* const* pcm, const int* n_samples, int B, const DecodeRequest& rq,
                              int* tokens, float* top1, float* top2, int* lang_out, int* ts_state_out) {
     select();
+    require_weights();
     if (B < 1 || B > max_batch_) throw std::runtime_error("batch exceeds the context's max_batch");
     stage_pcm(pcm, n_samples, B);
     transcribe_device(pcm_, 480000, n_samples, B, rq, tokens, top1, top2, lang_out, ts_state_out);
@@ -1074,6 +1110,7 @@ void Engine::read_cands(int B, BeamCands* out) {
 void Engine::beam_begin(const float* const* pcm, const int* n_samples, int B, const DecodeRequest& rq, BeamCands* out,
                         int* lang_out) {
     select();
+    require_weights();
     if (rq.beam_k < 1 || rq.beam_k > 8) throw std::runtime_error("beam size must be in 1..8");
     if (n_groups_ != 1) throw std::runtime_error("beam search needs one decode group");
     if (!kvtmp_) {
@@ -1137,6 +1174,7 @@ void Engine::debug_mel(const float* pcm_host, int n, float* out_host) {
 
 void Engine::debug_encode(const float* mel_host, float* out_host) {
     select();
+    require_weights();
     const int nm = dm_.n_mels, d = dm_.d, T = dm_.n_audio_ctx;
     std::vector<char> img((size_t)MEL_ROWS * cp_ * esz_, 0);
     for (int t = 0; t < 3000; ++t)

@@ -65,7 +65,10 @@ class Engine {
 public:
     // src == nullptr: synthetic weights from `seed`; else the weights, mel filters of a ggml file
     // (dm from ggml_dims(*src)); the file is read during construction only
-    Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64_t seed, const GgmlFile* src = nullptr);
+    // external_weights: allocate the weight arena but leave it unfilled; import_weights() (e.g.
+    // the bytes of rank 0's arena after an RCCL broadcast) makes the engine usable
+    Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64_t seed, const GgmlFile* src = nullptr,
+           bool external_weights = false);
     ~Engine();
     Engine(const Engine&) = delete;
     Engine& operator=(const Engine&) = delete;
@@ -74,6 +77,12 @@ public:
     int dtype() const { return dt_; }
     int max_batch() const { return max_batch_; }
     int64_t weight_bytes() const { return wbytes_; }
+    bool weights_ready() const { return weights_ready_; }
+    // D2D copies of the whole weight arena (device pointers on this engine's device, or any
+    // peer-accessible one); the arena layout is a pure function of (dims, dtype, n_mels padding),
+    // so two engines of one model exchange their weights byte for byte
+    void export_weights(void* dev_dst, int64_t bytes);
+    void import_weights(const void* dev_src, int64_t bytes);
     int64_t workspace_bytes() const { return abytes_; }
     const Timings& timings() const { return tm_; }
 
@@ -175,6 +184,8 @@ private:
     // ---- weights (one arena)
     char* warena_ = nullptr;
     int64_t wbytes_ = 0;
+    bool weights_ready_ = false;
+    void require_weights() const;
     struct EncL { float *ln1_w, *ln1_b; void* qkv_w; float* qkv_b; void* o_w; float* o_b; float *ln2_w, *ln2_b;
                   void* fc1_w; float* fc1_b; void* fc2_w; float* fc2_b; };
     struct DecL { float *ln1_w, *ln1_b; void* qkv_w; float* qkv_b; void* so_w; float* so_b; float *ln2_w, *ln2_b;

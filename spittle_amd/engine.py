@@ -40,6 +40,9 @@ class WhisperModelParams:
     device: int = 0
     max_batch: int = 8
     seed: int = 1234             # synthetic weights
+    # allocate the weight arena but leave it empty: import_weights() fills it (multi-GPU load,
+    # rank 0's arena broadcast over RCCL; spittle_amd.dist.broadcast_weights)
+    external_weights: bool = False
 
 
 @dataclass
@@ -160,6 +163,7 @@ class WhisperEngine:
         mp.device = int(self.params.device)
         mp.max_batch = int(self.params.max_batch)
         mp.seed = int(self.params.seed)
+        mp.flags = L.SPT_MODEL_WEIGHTS_EXTERNAL if self.params.external_weights else 0
         ctx = C.c_void_p()
         err = C.create_string_buffer(1024)
         st = self._lib.spt_ctx_create(str(model_path).encode(), C.byref(mp), C.byref(ctx), err, 1024)
@@ -220,6 +224,16 @@ class WhisperEngine:
         return [_take_result(out[i]) for i in range(n)]
 
     # -- introspection / test hooks -----------------------------------------
+    def export_weights(self, dev_ptr: int, nbytes: int) -> None:
+        """Copy the device weight arena (info()["weight_bytes"] bytes) to device memory at dev_ptr."""
+        self._need()
+        self._check(self._lib.spt_weights_export(self._ctx, C.c_void_p(dev_ptr), C.c_size_t(nbytes)))
+
+    def import_weights(self, dev_ptr: int, nbytes: int) -> None:
+        """Fill the weight arena of an external-weights engine from device memory at dev_ptr."""
+        self._need()
+        self._check(self._lib.spt_weights_import(self._ctx, C.c_void_p(dev_ptr), C.c_size_t(nbytes)))
+
     def info(self) -> dict:
         self._need()
         mi = L.ModelInfo()

@@ -72,3 +72,71 @@ def test_run_sharded_gloo_world2():
         b, e = shard_range(13, world, rank)
         assert calls[0] == [f"utt{i}" for i in range(b, e)]
         assert t == 2.0                             # max over ranks
+
+
+class _HostArenaEngine:
+    """Stand-in for WhisperEngine's weight-arena calls on CPU memory (the host logic of
+    broadcast_weights; the device copies themselves are covered by test_gpu_parity)."""
+
+    def __init__(self, nbytes, fill=None):
+        import numpy as np
+        self.arena = np.zeros(nbytes, np.uint8) if fill is None else fill.copy()
+
+    def info(self):
+        return {"weight_bytes": self.arena.size}
+
+    def export_weights(self, ptr, nbytes):
+        import ctypes
+        assert nbytes == self.arena.size
+        ctypes.memmove(ptr, self.arena.ctypes.data, nbytes)
+
+    def import_weights(self, ptr, nbytes):
+        import ctypes
+        assert nbytes == self.arena.size
+        ctypes.memmove(self.arena.ctypes.data, ptr, nbytes)
+
+
+def _bcast_worker(rank, world, port, q, sizes):
+    import numpy as np
+    import torch.distributed as dist
+    from spittle_amd.dist import broadcast_weights
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = sizes[rank]
+    src = np.random.default_rng(7).integers(0, 256, n, dtype=np.uint8)
+    eng = _HostArenaEngine(n, fill=src if rank == 0 else None)
+    try:
+        info = broadcast_weights(eng)
+        q.put((rank, "ok", bool((eng.arena == src).all()), info["bytes"]))
+    except RuntimeError as e:
+        q.put((rank, "err", str(e), 0))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run_bcast(sizes):
+    world, port = len(sizes), _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_bcast_worker, args=(r, world, port, q, sizes)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def test_broadcast_weights_gloo_world2():
+    """Rank 0's arena lands byte for byte in rank 1's (external-weights) engine."""
+    n = 3 * 1024 * 1024 + 17
+    for rank, kind, same, nbytes in _run_bcast([n, n]):
+        assert kind == "ok" and same and nbytes == n, (rank, kind, same)
+
+
+def test_broadcast_weights_size_mismatch_fails_loudly():
+    """Engines of different models (arena sizes) refuse the broadcast on every rank."""
+    for rank, kind, msg, _ in _run_bcast([4096, 8192]):
+        assert kind == "err" and "disagree" in msg, (rank, kind, msg)
