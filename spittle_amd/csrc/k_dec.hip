@@ -111,7 +111,6 @@ constexpr int attn_s(int asrc) { return asrc - 32; }
 template <typename T, int MODE, int ASRC, int RG, int NWV, int CT, int MAXJ>
 __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
     constexpr int KS = GV<T>::KS;
-    constexpr int EPL = KS / 4;          // elements per lane per super-step (64 bytes)
     constexpr int CPE = 16 / sizeof(T);  // elements per 16-byte chunk
     constexpr int KSPLIT = NWV / CT;
     constexpr bool IMG = ASRC != A_DIRECT;
@@ -128,7 +127,10 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
     const int kz = blockIdx.y, kzc = gridDim.y;
     const int nss_all = K / KS, per = (nss_all + kzc - 1) / kzc;
     const int ss0 = kz * per, ss1 = min(nss_all, ss0 + per);
-    const T* wrow = (const T*)a.W + (size_t)min(n0 + fr, a.N - 1) * K + fq * EPL;
+    // K order inside a super-step: MFMA step i, lane group fq takes the 16-byte chunk 4 i + fq,
+    // so the four lanes of a weight row read 64 contiguous bytes per load instruction (16 rows x
+    // 64 B per wave-instruction instead of 64 scattered 16-byte pieces); A uses the same order
+    const T* wrow = (const T*)a.W + (size_t)min(n0 + fr, a.N - 1) * K + fq * CPE;
 
     frag w[MAXJ][4];
     auto load_chunk = [&](int j0) {
@@ -137,7 +139,7 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
             const int ss = ss0 + ks + (j0 + j) * KSPLIT;
             if (ss < ss1) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) w[j][i] = load_w((const frag*)(wrow + (size_t)ss * KS + i * CPE));
+                for (int i = 0; i < 4; ++i) w[j][i] = load_w((const frag*)(wrow + (size_t)ss * KS + i * 4 * CPE));
             }
         }
     };
@@ -262,7 +264,7 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
         for (int j = 0; j < MAXJ; ++j) {
             const int ss = ss0 + ks + (j0 + j) * KSPLIT;
             if (ss >= ss1) break;
-            const int kb = ss * KS + fq * EPL;
+            const int kb = ss * KS + fq * CPE;
 #pragma unroll
             for (int g = 0; g < RG; ++g) {
                 const int row = g * 16 + fr;
@@ -271,9 +273,9 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         if constexpr (IMG)
-                            af[i] = *(const frag*)((const T*)smem + (size_t)row * lds_ld + kb + i * CPE);
+                            af[i] = *(const frag*)((const T*)smem + (size_t)row * lds_ld + kb + i * 4 * CPE);
                         else
-                            af[i] = *(const frag*)((const T*)a.A + (size_t)row * a.lda + a.a_row0 + kb + i * CPE);
+                            af[i] = *(const frag*)((const T*)a.A + (size_t)row * a.lda + a.a_row0 + kb + i * 4 * CPE);
                     }
                 } else {
 #pragma unroll
