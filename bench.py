@@ -202,8 +202,8 @@ def main():
             "metric": METRIC, "value": round(value, 3), "unit": "audio-sec/wall-sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
-            "data": "synthetic (BASELINE.md §3 seeded 16 kHz signal; random-init large-v3 weights)",
-            "config": {"workload": f"whisper-large-v3 30s chunks, batch {B}/GPU, greedy en, "
+            "data": f"synthetic (BASELINE.md §3 seeded 16 kHz signal; random-init {args.model.split(':', 1)[-1]} weights)",
+            "config": {"workload": f"whisper-{args.model.split(':')[-1]} 30s chunks, batch {B}/GPU, greedy en, "
                                    f"{PROMPT_LEN}-token prompt + {args.decode_steps} decode steps",
                        "model": args.model, "global_batch": world * B, "seq_len": 1500,
                        "decode_steps": args.decode_steps, "parallelism": f"replicas x{world} (utterance shards)"},
