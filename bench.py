@@ -179,8 +179,10 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
+    marks = [t0]
     for _ in range(args.steps):
-        res = step()
+        res = step()  # returns host tokens: each step ends synchronised
+        marks.append(time.perf_counter())
     barrier()
     dt = time.perf_counter() - t0
     dt = max_over_ranks(dt, device=dev)
@@ -201,6 +203,7 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "audio-sec/wall-sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "ms_per_step_median_rank0": round(float(np.median(np.diff(marks))) * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": f"synthetic (BASELINE.md §3 seeded 16 kHz signal; random-init {args.model.split(':', 1)[-1]} weights)",
             "config": {"workload": f"whisper-{args.model.split(':')[-1]} 30s chunks, batch {B}/GPU, greedy en, "
