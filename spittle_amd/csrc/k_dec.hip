@@ -431,6 +431,7 @@ void gemv_attr_all() {
     } else {
         SPT_ATTR(4, 1, 2)
         SPT_ATTR(8, 1, 2)
+        SPT_ATTR(8, 2, 3)
     }
 #undef SPT_ATTR
 }
@@ -447,6 +448,15 @@ void gemv_launch_rg(const GemvArgs& a, hipStream_t st) {
     if constexpr (MODE == GV_LOGITS) {
         gemv_launch_cfg<T, MODE, ASRC, RG, 4, 4, 4>(a, st);
     } else {
+        // Wide LayerNorm-prologue GEMVs (fc1, N = 4d >= 4096): two column tiles per workgroup,
+        // so half as many workgroups re-read the residual rows for their LayerNorm image (r1
+        // exp23: fc1 9.4 -> 8.6 us, RTFx +1.2 %; the QKV and cross-Q projections lose with it)
+        if constexpr (ASRC != A_DIRECT) {
+            if (a.N >= 4096 && nss <= 24) {
+                gemv_launch_cfg<T, MODE, ASRC, RG, 8, 2, 3>(a, st);
+                return;
+            }
+        }
         if (nss <= 8) gemv_launch_cfg<T, MODE, ASRC, RG, 4, 1, 2>(a, st);
         else if (nss <= 16) gemv_launch_cfg<T, MODE, ASRC, RG, 8, 1, 2>(a, st);
         else if constexpr (ASRC == A_DIRECT) {  // 16 waves: no room for a staged A image's registers
