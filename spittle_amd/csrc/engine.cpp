@@ -132,10 +132,10 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     if ((3 * cp_ * esz_) % 128) cp_ = ((dm_.n_mels + 127) / 128) * 128;
     if (const char* g = getenv("SPT_DECODE_GROUPS")) n_groups_ = std::max(1, std::min(2, atoi(g)));
     if (const char* v = getenv("SPT_XATTN_SPLIT")) xsplit_ = std::max(1, std::min(4, atoi(v)));
-    // cross-attention key split: fixed per engine (never per batch).  Projection K splits
-    // (self-out: 2, fc2: 2; r1 exp14 measured fc2 at 2 slightly faster per layer than 4: the
-    // next QKV LayerNorm prologue sums fewer slabs) are fixed per engine too; the pending-slab
-    // count a LayerNorm prologue sums is a kernel template constant.
+    // cross-attention key split: fixed per engine (never per batch).  The fc2 K split (2; r1
+    // exp14 measured 2 slightly faster per layer than 4: the next QKV LayerNorm prologue sums
+    // fewer slabs) is fixed per engine too; the pending-slab count a LayerNorm prologue sums is
+    // a kernel template constant.
     select();
     HIP_CHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     ev_.resize(8);
@@ -682,13 +682,14 @@ void Engine::run_cross_kv(int B) {
     gemm_nt(dt_, EPI_KVSPLIT, g, 1, st_);
 }
 
-// One decoder pass: 8 launches per layer.  The residual stream is f32 rows; the self-attention
-// output projection and fc2 split K over 2 / 4 workgroups and leave their results as pending
-// partial slabs, which the next LayerNorm prologue sums (x + slabs, fixed order) and writes to
-// the other x buffer: no read-modify-write of the residual there and 2-4x the workgroups on
-// the N = d projections (r1 ubench: self-out 4.8 -> 3.2 us, fc2 10.2 -> 5.7 us).  The cross-
-// attention output projection keeps the read-modify-write residual add, because slabs there
-// would land on the 320-workgroup fc1 LayerNorm prologue (+1.2 us per slab measured).
+// One decoder pass: 8 launches per layer.  The residual stream is f32 rows; fc2 splits K over
+// 2 workgroups and leaves its result as pending partial slabs, which the next QKV LayerNorm
+// prologue sums (x + slabs, fixed order) and writes to the other x buffer: no read-modify-write
+// of the residual there and 2x the workgroups on the N = d projection (r1 ubench: fc2 10.2 ->
+// 5.7 us).  The self- and cross-attention output projections keep the read-modify-write
+// residual add: every workgroup of the LayerNorm GEMV after them re-reads the residual rows,
+// so slabs there cost more than they save (cross-out: +1.2 us per slab on fc1; self-out:
+// r1 exp24, in place +0.4 % RTFx over 2 slabs).
 void Engine::enqueue_decoder_pass(DecGroup& g, int B_total, int Tq, const DecodeRequest& rq, int out_cap) {
     float* x = enqueue_layers(g, B_total, Tq);
     enqueue_head(g, Tq, rq, out_cap, x, suppress_, (rq.flags & 1u) != 0);
@@ -733,11 +734,12 @@ float* Engine::enqueue_layers(DecGroup& g, int B_total, int Tq) {
         gemv(dt_, GV_QKV_CACHE, A_LN, a, st);
         consumed();
         dec_self_attn(dt_, g.dq, skv_l, B, H, ctx, Tq, g.ds, g.dao, st);
-        // self-attention output projection -> pending slabs
+        // self-attention output projection, residual add in place: the cross-Q LayerNorm
+        // prologue then reads x alone (r1 exp24: +0.4 % RTFx over a 2-way K split into slabs)
         a = GemvArgs{};
         a.A = g.dao; a.lda = d; a.R = R; a.W = e.so_w; a.N = d; a.K = d; a.bias = e.so_b;
-        partial(a, so_split_);
-        gemv(dt_, GV_PARTIAL, A_DIRECT, a, st);
+        a.C = xc; a.ldc = d;
+        gemv(dt_, GV_BIAS_RESID, A_DIRECT, a, st);
         // LN2 + cross-Q projection
         a = GemvArgs{};
         ln_input(a); a.lda = d; a.ln_w = e.ln2_w; a.ln_b = e.ln2_b; a.R = R;

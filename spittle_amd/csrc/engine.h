@@ -175,7 +175,7 @@ private:
     uint64_t seed_;
     int esz_;     // bytes per weight / activation element
     int cp_;      // padded mel channels (conv1 K = 3 * cp_)
-    static constexpr int so_split_ = 2, fc2_split_ = 2;  // K splits of the self-out / fc2 projections
+    static constexpr int fc2_split_ = 2;  // K split of the fc2 projection (pending slabs)
     int xsplit_ = 1;  // cross-attention key chunks per (b, h) (merged by the output projection)
     int n_groups_ = 1;  // SPT_DECODE_GROUPS=2 splits the batch over two streams
     hipStream_t st_ = nullptr;

@@ -406,6 +406,7 @@ void gemv_launch_cfg(const GemvArgs& a, hipStream_t st) {
     X(GV_QKV_CACHE, LN_SRC(0))          \
     X(GV_QKV_CACHE, LN_SRC(2))          \
     X(GV_QKV_CACHE, LN_SRC(4))          \
+    X(GV_BIAS, LN_SRC(0))               \
     X(GV_BIAS, LN_SRC(2))               \
     X(GV_BIAS_GELU, LN_SRC(0))          \
     X(GV_LOGITS, LN_SRC(0))             \
