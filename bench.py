@@ -6,43 +6,57 @@ weights/activations (f32 accumulation), batch of 8 synthetic 30 s 16 kHz chunks
 <|notimestamps|>, a 4-token prompt and 128 forced decode steps (EOT ignored:
 random-init weights never stop).  Weights are random-init from the shared seeded
 PRNG (no checkpoints offline).  One "step" = one batched call through the C ABI
-(spt_transcribe_batch_device): PCM resident in HBM -> log-mel -> encoder ->
-cross K/V -> 132 decoder passes -> tokens on the host.
+(spt_transcribe_batch, BASELINE.md:48's span): host PCM -> H2D -> log-mel -> encoder ->
+cross K/V -> 132 decoder passes -> tokens and text on the host.  `value` is that rate;
+`value_device_resident` is the same call on PCM already in HBM
+(spt_transcribe_batch_device).
 
-N > 1: one process per GPU (torchrun), each rank transcribes its own shard of
-8 utterances (weak scaling, no data-path collective), max time over ranks.
+--gpus N (BASELINE.json configs[3]): one process per GPU.  Launched by torchrun (WORLD_SIZE
+set) each rank runs here; launched plainly, this process starts the N ranks itself
+(torch.distributed.run, before touching the GPU) and exits with their status.  Each rank
+transcribes its own shard of 8 utterances per step (weak scaling, no data-path collective);
+rank 0 loads the weights and one RCCL broadcast writes them straight into every other rank's
+weight arena; the timed region is bracketed by barriers and the max over ranks is reported.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-METRIC = "RTFx (audio-sec/wall-sec) Whisper-large-v3 30s chunks @1/2/4/8 MI355X"
 MODEL_SPEC = "synthetic:large-v3"
 CHUNK_S = 30.0
 PROMPT_LEN = 4
 N_STEPS = 128
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
 MFMA_PEAK_BF16_TFS = 2500.0  # dense bf16
+FP32_PEAK_TFS = 157.3        # f32 MFMA = vector rate
+
+
+def metric_for(model: str) -> str:
+    name = model.split(":", 1)[-1].split(":")[0]
+    return f"RTFx (audio-sec/wall-sec) Whisper-{name} 30s chunks @1/2/4/8 MI355X"
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=8, help="30 s chunks per GPU")
     ap.add_argument("--model", default=MODEL_SPEC)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--decode-steps", type=int, default=N_STEPS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-steps", type=int, default=4)
+    ap.add_argument("--no-app-latency", action="store_true", help="skip the B=1 whisper_full (app default) latency")
+    ap.add_argument("--no-probe", action="store_true", help="skip the per-kernel HIP-event probes")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL) for the real run; gloo only to rehearse N > 1 ranks on one GPU")
     ap.add_argument("--no-weight-bcast", action="store_true",
@@ -50,14 +64,61 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(model_spec: str, sample_steps: int, decode_steps: int) -> dict:
-    """CPU baseline leg: the oracle (C restatement of the whisper-rs/whisper.cpp CPU
-    path, fp32, OpenMP) on a bounded sample of the same workload: one 30 s chunk
-    through log-mel + encoder + cross K/V + `sample_steps` decoder passes; the
-    decoder time is scaled to the full prompt + decode_steps passes."""
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args) -> int:
+    """Start args.gpus ranks of this script with torch.distributed.run (one process per GPU) as
+    a child process; nothing in this process has touched the GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")  # the CPU-baseline leg sets its own thread count
+    return subprocess.call(cmd, env=env)
+
+
+def host_cpu() -> dict:
+    """CPU model and core counts of this host (the box's share is what the process may use)."""
+    model, phys = None, set()
+    try:
+        cur = {}
+        for line in open("/proc/cpuinfo"):
+            if ":" not in line:
+                if cur:
+                    phys.add((cur.get("physical id"), cur.get("core id")))
+                cur = {}
+                continue
+            k, v = (x.strip() for x in line.split(":", 1))
+            cur[k] = v
+            if k == "model name" and model is None:
+                model = v
+        if cur:
+            phys.add((cur.get("physical id"), cur.get("core id")))
+    except OSError:
+        pass
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except AttributeError:
+        allowed = os.cpu_count()
+    return {"model": model, "physical_cores": len(phys) or None, "logical_cpus": os.cpu_count(),
+            "affinity_cpus": allowed}
+
+
+def cpu_baseline(model_spec: str, decode_steps: int) -> dict:
+    """CPU baseline leg: the oracle (C restatement of the whisper-rs/whisper.cpp CPU path, fp32,
+    OpenMP over this job's CPU share) on one 30 s chunk of the same workload, end to end:
+    log-mel + encoder + cross K/V + the 4-token prompt pass + every decoder pass (no
+    extrapolation).  The GPU box gives a one-GPU job 16 host cores (OMP_NUM_THREADS=16)."""
     from oracle import oracle as O
     name = model_spec.split(":")[1]
-    threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
+    cpu = host_cpu()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(cpu["affinity_cpus"] or 1, 16)
     O.set_threads(threads)
     dims = O.dims_for(name)
     m = O.Model(dims, 1234, O.W_F32)
@@ -68,26 +129,22 @@ def cpu_baseline(model_spec: str, sample_steps: int, decode_steps: int) -> dict:
     t1 = time.perf_counter()
     enc = m.encode(mel)
     t2 = time.perf_counter()
-    O.lib()  # cross K/V is computed inside decode; time it with a 1-step decode
-    m.decode(enc, prompt, 1, O.SUPPRESS_BLANK | O.NO_TIMESTAMPS | O.IGNORE_EOT)
+    m.decode(enc, prompt, decode_steps, O.SUPPRESS_BLANK | O.NO_TIMESTAMPS | O.IGNORE_EOT)
     t3 = time.perf_counter()
-    m.decode(enc, prompt, 1 + sample_steps, O.SUPPRESS_BLANK | O.NO_TIMESTAMPS | O.IGNORE_EOT)
-    t4 = time.perf_counter()
-    per_pass = max(((t4 - t3) - (t3 - t2)) / sample_steps, 1e-9)
-    first = t3 - t2  # cross K/V + prompt pass
-    total = (t1 - t0) + (t2 - t1) + first + per_pass * (decode_steps - 1)
     m.close()
+    total = t3 - t0
     return {"value": round(CHUNK_S / total, 4), "unit": "audio-sec/wall-sec", "cores": threads, "kind": "port",
-            "sample": f"1 x 30 s chunk, {name} dims fp32: mel {t1 - t0:.2f}s + encoder {t2 - t1:.2f}s + "
-                      f"cross-KV+prompt pass {first:.2f}s + {sample_steps} timed decoder passes "
-                      f"({per_pass:.3f}s each) scaled to {decode_steps - 1}; est. {total:.1f}s per chunk"}
+            "cpu_model": cpu["model"], "host_physical_cores": cpu["physical_cores"],
+            "sample": f"1 x 30 s chunk, {name} dims fp32, {threads} OpenMP threads: mel {t1 - t0:.2f}s + encoder "
+                      f"{t2 - t1:.2f}s + cross-KV + {PROMPT_LEN}-token prompt pass + {decode_steps - 1} decoder passes "
+                      f"{t3 - t2:.2f}s = {total:.1f}s per chunk (timed whole, no extrapolation)"}
 
 
 DOMINANT = "dec_cross_attn"  # largest share of device time (profiles/*_kernel_stats.csv)
 KERNEL_NAMES = {
-    "dec_cross_attn": "cross_attn_kernel<bf16,1> (4 keys/lane) (decoder cross-attention, 1 layer)",
-    "dec_logits": "gemv_kernel<bf16,GV_LOGITS,A_LN> (final LN + logits + top-2)",
-    "dec_fc1": "gemv_kernel<bf16,GV_BIAS_GELU,A_LN> (decoder LN + fc1 + GELU)",
+    "dec_cross_attn": "cross_attn_kernel (decoder cross-attention, 1 layer)",
+    "dec_logits": "gemv_kernel<GV_LOGITS,A_LN> (final LN + logits + top-2)",
+    "dec_fc1": "gemv_kernel<GV_BIAS_GELU,A_LN> (decoder LN + fc1 + GELU)",
     "enc_fc1_gemm": "gemm256_kernel<EPI_BIAS_GELU> (encoder fc1, 256x256 tile)",
     "enc_attn": "attn_bf16_kernel (encoder flash attention, 1 layer)",
 }
@@ -121,15 +178,77 @@ def roofline(eng, iters: int = 50):
     return roof, rows
 
 
+def phase_rooflines(info: dict, phases: dict, B: int, decode_steps: int, dtype: str) -> dict:
+    """Whole-phase rooflines of the last call (HIP events per phase, engine stream):
+    encoder = algorithmic FLOPs of conv stem + blocks / encoder time vs the dense
+    MFMA peak of the dtype; decode pass = algorithmic bytes one greedy pass streams (layer
+    weights + logits matrix + every sequence's cross K/V + self K/V at the mean position) /
+    the mean pass time vs HBM peak."""
+    d, L_e, L_d, V, nm = info["d"], info["n_enc"], info["n_dec"], info["n_vocab"], info["n_mels"]
+    T, H = info["n_audio_ctx"], info["n_head"]
+    esz = 2 if dtype == "bf16" else 4
+    conv = 2 * 2 * T * d * 3 * nm + 2 * T * d * 3 * d
+    layer = 2 * T * d * 3 * d + 4 * H * T * T * 64 + 2 * T * d * d + 2 * 2 * T * d * 4 * d
+    enc_flops = B * (conv + L_e * layer)
+    peak = MFMA_PEAK_BF16_TFS if dtype == "bf16" else FP32_PEAK_TFS
+    out = {}
+    if phases.get("encoder_ms", 0) > 0:
+        tf = enc_flops / (phases["encoder_ms"] * 1e-3) / 1e12
+        out["encoder"] = {"bound": "mfma", "flops_per_call": enc_flops, "ms": round(phases["encoder_ms"], 3),
+                          "achieved": round(tf, 1), "peak": peak, "unit": "TFLOP/s", "frac": round(tf / peak, 4)}
+    n_pass = phases.get("n_decode_passes", 0)
+    if phases.get("decode_ms", 0) > 0 and n_pass > 1:
+        mean_pos = PROMPT_LEN + (decode_steps - 1) / 2.0
+        w = L_d * 14 * d * d * esz
+        logit = V * d * esz
+        cross = L_d * 2 * B * H * T * 64 * esz
+        selfkv = L_d * 2 * B * H * mean_pos * 64 * esz
+        per_pass = w + logit + cross + selfkv
+        ms = phases["decode_ms"] / n_pass
+        gbs = per_pass / (ms * 1e-3) / 1e9
+        out["decode_pass"] = {"bound": "hbm", "bytes_per_pass": int(per_pass),
+                              "bytes_split": {"layer_weights": w, "logits_matrix": logit, "cross_kv": cross,
+                                              "self_kv_mean": int(selfkv)},
+                              "ms_per_pass": round(ms, 4), "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    return out
+
+
+def app_latency(eng, dur_s=(5, 10, 30)) -> dict:
+    """The app's real call (transcription.rs:494-503): one utterance (B = 1), whisper_full with
+    its default parameters (timestamps on, temperature fallback 0.2 / best_of 5), language
+    "en", through spt_transcribe.  Random-init weights never emit EOT or confident tokens, so
+    every window decodes to its token limit and falls back through every temperature: an
+    upper bound of the app's latency; the passes it took are reported with it."""
+    from spittle_amd import WhisperInferenceParams
+    from spittle_amd.synth import synth_audio
+    out = {}
+    p = WhisperInferenceParams(language="en")
+    eng.transcribe_samples(synth_audio(2000)[:16000 * 5], p)  # warm (graphs captured)
+    for s in dur_s:
+        x = synth_audio(2000 + s)[:16000 * s]
+        t0 = time.perf_counter()
+        r = eng.transcribe_samples(x, p)
+        ms = (time.perf_counter() - t0) * 1e3
+        out[f"{s}s"] = {"ms": round(ms, 2), "windows": r.n_windows, "fallbacks": r.n_fallbacks,
+                        "tokens": len(r.tokens), "segments": len(r.segments)}
+    return out
+
+
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and world_env is None:
+        sys.exit(launch_ranks(args))
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = int(world_env or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if world > 1:
         local %= max(1, torch.cuda.device_count())  # rehearsal: several ranks on one GPU (gloo)
         torch.cuda.set_device(local)
@@ -137,6 +256,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(args.dist_backend)
+        assert dist.get_world_size() == args.gpus
     dev = torch.device("cuda", local)
 
     from spittle_amd import WhisperEngine, WhisperInferenceParams, WhisperModelParams
@@ -147,72 +267,98 @@ def main():
     # this rank's shard of the global utterance list (B per GPU: weak scaling)
     lo, hi = shard_range(world * B, world, rank)
     pcm = np.stack([synth_audio(i) for i in range(lo, hi)])
+    pcm_list = [pcm[i] for i in range(B)]
     pcm_dev = torch.from_numpy(pcm).to(dev)
     torch.cuda.synchronize()
 
     # N > 1: rank 0 loads (generates / dequantises) the weights, one RCCL broadcast over xGMI
-    # replicates its arena into the other ranks' engines; outside the timed region
+    # writes its arena into the other ranks' engines; outside the timed region
     bcast = world > 1 and not args.no_weight_bcast
     eng = WhisperEngine(WhisperModelParams(dtype=args.dtype, device=local, max_batch=B, seed=1234,
                                            external_weights=bcast and rank != 0))
+    t_load = time.perf_counter()
     eng.load_model(args.model)
+    load_ms = (time.perf_counter() - t_load) * 1e3
     wload = None
     if bcast:
         bi = broadcast_weights(eng, device=dev)
         bms = max_over_ranks(bi["ms"], device=dev)
-        wload = {"mode": "rank 0 load + " + ("RCCL" if args.dist_backend == "nccl" else args.dist_backend) + " broadcast", "bytes": bi["bytes"], "ms": round(bms, 3),
-                 "GB/s": round(bi["bytes"] / bms / 1e6, 1) if bms > 0 else None}
+        wload = {"mode": "rank 0 load + " + ("RCCL" if args.dist_backend == "nccl" else args.dist_backend) +
+                 " broadcast into the arenas (" + bi.get("path", "") + ")", "bytes": bi["bytes"], "ms": round(bms, 3),
+                 "GB/s": round(bi["bytes"] / bms / 1e6, 1) if bms > 0 else None,
+                 "rank0_load_ms": round(max_over_ranks(load_ms if rank == 0 else 0.0, device=dev), 1)}
     info = eng.info()
-    params = WhisperInferenceParams(language="en", no_timestamps=True, temperature_inc=0.0, ignore_eot=True, max_new_tokens=args.decode_steps)
+    params = WhisperInferenceParams(language="en", no_timestamps=True, temperature_inc=0.0, ignore_eot=True,
+                                    max_new_tokens=args.decode_steps)
     lens = [pcm.shape[1]] * B
 
-    def step():
-        return eng.transcribe_batch_device(pcm_dev.data_ptr(), pcm.shape[1], lens, params)
+    def step_host():  # BASELINE.md:48: host PCM buffer -> text on the host
+        return eng.transcribe_batch(pcm_list, params)
 
-    for _ in range(args.warmup):
-        step()
+    def step_dev():
+        return eng.transcribe_batch_device(pcm_dev.data_ptr(), pcm.shape[1], lens, params)
 
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
-    barrier()
-    t0 = time.perf_counter()
-    marks = [t0]
-    for _ in range(args.steps):
-        res = step()  # returns host tokens: each step ends synchronised
-        marks.append(time.perf_counter())
-    barrier()
-    dt = time.perf_counter() - t0
-    dt = max_over_ranks(dt, device=dev)
-    assert all(len(r.tokens) == args.decode_steps for r in res)
-    phases = eng.timings()
+    def timed(step):
+        for _ in range(args.warmup):
+            step()
+        barrier()
+        t0 = time.perf_counter()
+        marks = [t0]
+        res = None
+        for _ in range(args.steps):
+            res = step()  # returns host tokens and text: each step ends synchronised
+            marks.append(time.perf_counter())
+        barrier()
+        dt = max_over_ranks(time.perf_counter() - t0, device=dev)
+        assert all(len(r.tokens) == args.decode_steps for r in res)
+        return dt, float(np.median(np.diff(marks))), eng.timings()
+
+    dt, med, phases = timed(step_host)
+    dt_dev, med_dev, phases_dev = timed(step_dev)
+    rank_ms = [None] * world
+    if world > 1:
+        dist.all_gather_object(rank_ms, round(dt * 1e3 / args.steps, 3))
 
     audio_s = world * B * CHUNK_S * args.steps
     value = audio_s / dt
     ms_per_step = dt * 1000.0 / args.steps
 
-    roof = None
-    cpu = None
+    roof = kernels = None
+    cpu = app = None
     if rank == 0:
-        roof, kernels = roofline(eng)
+        if not args.no_probe:
+            roof, kernels = roofline(eng)
+        if world == 1 and not args.no_app_latency:
+            app = app_latency(eng)
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.model, args.cpu_sample_steps, args.decode_steps)
+            cpu = cpu_baseline(args.model, args.decode_steps)
     if rank == 0:
         out = {
-            "metric": METRIC, "value": round(value, 3), "unit": "audio-sec/wall-sec", "n_gpus": world,
+            "metric": metric_for(args.model), "value": round(value, 3), "unit": "audio-sec/wall-sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-            "ms_per_step_median_rank0": round(float(np.median(np.diff(marks))) * 1e3, 3),
+            "ms_per_step_median_rank0": round(med * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": f"synthetic (BASELINE.md §3 seeded 16 kHz signal; random-init {args.model.split(':', 1)[-1]} weights)",
             "config": {"workload": f"whisper-{args.model.split(':')[-1]} 30s chunks, batch {B}/GPU, greedy en, "
-                                   f"{PROMPT_LEN}-token prompt + {args.decode_steps} decode steps",
+                                   f"{PROMPT_LEN}-token prompt + {args.decode_steps} decode steps, host PCM in, text out",
                        "model": args.model, "global_batch": world * B, "seq_len": 1500,
                        "decode_steps": args.decode_steps, "parallelism": f"replicas x{world} (utterance shards)"},
+            "value_device_resident": round(audio_s / dt_dev, 3),
+            "ms_per_step_device_resident": round(dt_dev * 1000.0 / args.steps, 3),
             "phases_ms": {k: round(v, 3) for k, v in phases.items() if k.endswith("_ms")},
-            "roofline": roof, "kernels": kernels, "cpu_baseline": cpu,
+            "phases_ms_device_resident": {k: round(v, 3) for k, v in phases_dev.items() if k.endswith("_ms")},
+            "roofline": roof, "rooflines": phase_rooflines(info, phases, B, args.decode_steps, args.dtype),
+            "kernels": kernels, "cpu_baseline": cpu,
         }
+        if app:
+            out["app_call_latency_b1"] = app
+        if world > 1:
+            out["ms_per_step_per_rank"] = rank_ms
         if wload:
             out["weight_load"] = wload
         print(json.dumps(out), flush=True)

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 4
+#define SPT_ABI_VERSION 5
 
 typedef enum {
     SPT_OK = 0,
@@ -184,6 +184,27 @@ spt_status spt_get_timings(const spt_ctx* ctx, spt_timings* t);
  * multi-device path; these two entry points exist for the replica-parallel load only. */
 spt_status spt_weights_export(spt_ctx* ctx, void* dev_dst, size_t bytes);
 spt_status spt_weights_import(spt_ctx* ctx, const void* dev_src, size_t bytes);
+/* ABI 5: the arena itself (device pointer on the context's device, weight_bytes long), so a
+ * rank's collective (RCCL broadcast from rank 0) writes straight into it with no staging copy;
+ * then spt_weights_commit (synchronises the device) marks an external-weights context usable. */
+spt_status spt_weights_arena(spt_ctx* ctx, void** dev_ptr, size_t* bytes);
+spt_status spt_weights_commit(spt_ctx* ctx);
+
+/* ABI 5: replica parallelism from ONE host process over several devices, for a
+ * host that owns one engine object (the app's TranscriptionManager, transcription.rs:29-47).
+ * spt_ctx_create_replicas creates out[i] on devices[i] (distinct ordinals): devices[0] loads the
+ * model, one grouped RCCL ncclBroadcast (ncclCommInitAll communicator, xGMI) copies its weight
+ * arena into every other context's arena; *bcast_ms (optional) = the broadcast's wall time.
+ * Each out[i] is an ordinary context (destroy each with spt_ctx_destroy).
+ * spt_transcribe_batch_replicas splits a batch of utterances into n_ctx contiguous balanced
+ * shards, transcribes shard i on ctxs[i] in its own host thread (no collective on the data
+ * path) and returns out[batch] in input order; on error every result is released and ctxs[0]'s
+ * last error names the failing replica. */
+spt_status spt_ctx_create_replicas(const char* model_spec, const spt_model_params* params, const int32_t* devices,
+                                   int32_t n_devices, spt_ctx** out, double* bcast_ms, char* err, size_t errlen);
+spt_status spt_transcribe_batch_replicas(spt_ctx* const* ctxs, int32_t n_ctx, const float* const* pcm,
+                                         const size_t* n_samples, size_t batch, const spt_infer_params* params,
+                                         spt_result** out);
 
 /* Kernel probe (measurement): re-launch one hot-path kernel `iters` times on the engine
  * stream, on the buffers of the last call.  Decoder kernels (kinds 0-3) are timed between two

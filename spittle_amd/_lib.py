@@ -24,7 +24,8 @@ EXPORTS = [
     "spt_transcribe_batch_device", "spt_result_free", "spt_get_timings", "spt_debug_mel",
     "spt_debug_encode", "spt_debug_weight_checksum", "spt_probe_kernel", "spt_language_code",
     "spt_tokenize", "spt_token_to_str", "spt_debug_ggml_tokenize", "spt_debug_ggml_dequant",
-    "spt_weights_export", "spt_weights_import",
+    "spt_weights_export", "spt_weights_import", "spt_weights_arena", "spt_weights_commit",
+    "spt_ctx_create_replicas", "spt_transcribe_batch_replicas",
 ]
 SPT_MODEL_WEIGHTS_EXTERNAL = 1
 PROBES = {"dec_cross_attn": 0, "dec_self_attn": 1, "dec_logits": 2, "dec_fc1": 3, "enc_fc1_gemm": 4,
@@ -115,7 +116,14 @@ def load():
                                    C.POINTER(C.c_int32)]
     L.spt_weights_export.argtypes = [vp, C.c_void_p, C.c_size_t]
     L.spt_weights_import.argtypes = [vp, C.c_void_p, C.c_size_t]
-    for fn in ("spt_weights_export", "spt_weights_import", "spt_ctx_info", "spt_transcribe", "spt_transcribe_batch", "spt_transcribe_batch_device",
+    L.spt_weights_arena.argtypes = [vp, C.POINTER(vp), C.POINTER(C.c_size_t)]
+    L.spt_weights_commit.argtypes = [vp]
+    L.spt_ctx_create_replicas.argtypes = [C.c_char_p, C.POINTER(ModelParams), C.POINTER(C.c_int32), C.c_int32,
+                                          C.POINTER(vp), C.POINTER(C.c_double), C.c_char_p, C.c_size_t]
+    L.spt_transcribe_batch_replicas.argtypes = [C.POINTER(vp), C.c_int32, C.POINTER(fp), C.POINTER(C.c_size_t),
+                                                C.c_size_t, C.POINTER(InferParams), C.POINTER(C.POINTER(Result))]
+    for fn in ("spt_weights_arena", "spt_weights_commit", "spt_ctx_create_replicas", "spt_transcribe_batch_replicas",
+               "spt_weights_export", "spt_weights_import", "spt_ctx_info", "spt_transcribe", "spt_transcribe_batch", "spt_transcribe_batch_device",
                "spt_get_timings", "spt_debug_mel", "spt_debug_encode", "spt_debug_weight_checksum",
                "spt_probe_kernel", "spt_tokenize", "spt_debug_ggml_tokenize", "spt_debug_ggml_dequant"):
         getattr(L, fn).restype = C.c_int

@@ -25,12 +25,7 @@
 
 using spt::Engine;
 
-struct spt_ctx {
-    std::unique_ptr<Engine> eng;
-    std::unique_ptr<spt::Vocab> vocab;  // ggml models; synthetic models have none
-    std::string spec;
-    std::string err;
-};
+#include "capi_internal.h"
 
 namespace {
 
@@ -43,18 +38,25 @@ void set_err(char* buf, size_t len, const std::string& msg) {
     }
 }
 
-spt_status fail(spt_ctx* c, spt_status s, const std::string& msg) {
+}  // namespace
+
+spt_status spt_fail(spt_ctx* c, spt_status s, const std::string& msg) {
     if (c) c->err = msg;
     return s;
 }
 
-spt_status classify(const std::exception& e) {
+spt_status spt_classify(const std::exception& e) {
     if (dynamic_cast<const spt::HipError*>(&e)) return SPT_ERR_DEVICE;
     if (dynamic_cast<const std::bad_alloc*>(&e)) return SPT_ERR_OOM;
     const std::string m = e.what();
     if (m.find("out of device memory") != std::string::npos) return SPT_ERR_OOM;
     return SPT_ERR_INVALID_ARG;
 }
+
+namespace {
+
+spt_status fail(spt_ctx* c, spt_status s, const std::string& msg) { return spt_fail(c, s, msg); }
+spt_status classify(const std::exception& e) { return spt_classify(e); }
 
 // whisper_full: initial_prompt is tokenised (whisper_tokenize) only when no prompt_tokens are
 // given; either way the tokens become the prompt_past
@@ -333,7 +335,7 @@ spt_status run_windows(spt_ctx* c, std::vector<Window>& win, size_t n_utt, const
 
 extern "C" {
 
-const char* spt_version(void) { return "spittle_amd 0.5.0 (gfx950, ABI 4)"; }
+const char* spt_version(void) { return "spittle_amd 0.6.0 (gfx950, ABI 5)"; }
 
 const char* spt_language_code(int32_t lang_id) { return spt::lang_code(lang_id); }
 
@@ -503,7 +505,10 @@ spt_status spt_transcribe_batch_device(spt_ctx* ctx, const float* pcm_dev, size_
     if (!ctx || !out || !pcm_dev || !n_samples || batch == 0) return fail(ctx, SPT_ERR_INVALID_ARG, "null argument");
     if (batch > (size_t)ctx->eng->max_batch()) return fail(ctx, SPT_ERR_INVALID_ARG, "batch exceeds max_batch");
     if (stride < (size_t)kWindow) return fail(ctx, SPT_ERR_INVALID_ARG, "device stride must be >= 480000");
-    if (params && full_mode(params))
+    spt_infer_params dflt;
+    spt_default_infer_params(&dflt);
+    if (!params) params = &dflt;  // the defaults are whisper_full's (timestamps on): unsupported here
+    if (full_mode(params))
         return fail(ctx, SPT_ERR_UNSUPPORTED,
                     "device windows take the no-timestamp greedy protocol (SPT_NO_TIMESTAMPS, temperature_inc 0)");
     spt::DecodeRequest rq;

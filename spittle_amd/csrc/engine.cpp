@@ -25,40 +25,6 @@
 
 namespace spt {
 
-// ----------------------------------------------------------------------------- vocab
-Specials specials_for(int n_vocab) {
-    // whisper.cpp whisper_vocab defaults, shifted for multilingual vocabularies in
-    // whisper_model_load (language count = n_vocab - 51765 - multilingual)
-    Specials s{50256, 50257, 50357, 50358, 50359, 50360, 50361, 50362, 50363, 0};
-    const bool multi = n_vocab >= 51865;
-    const int n_langs = n_vocab - 51765 - (multi ? 1 : 0);
-    if (multi) {
-        s.eot++;
-        s.sot++;
-        const int dt = n_langs - 98;
-        s.translate += dt; s.transcribe += dt; s.solm += dt; s.prev += dt; s.nosp += dt; s.not_ += dt; s.beg += dt;
-        s.n_langs = n_langs;
-    }
-    return s;
-}
-
-static const char* const kLangs[] = {
-    "en", "zh", "de", "es", "ru", "ko", "fr", "ja", "pt", "tr", "pl", "ca", "nl", "ar", "sv", "it", "id",
-    "hi", "fi", "vi", "he", "uk", "el", "ms", "cs", "ro", "da", "hu", "ta", "no", "th", "ur", "hr", "bg",
-    "lt", "la", "mi", "ml", "cy", "sk", "te", "fa", "lv", "bn", "sr", "az", "sl", "kn", "et", "mk", "br",
-    "eu", "is", "hy", "ne", "mn", "bs", "kk", "sq", "sw", "gl", "mr", "pa", "si", "km", "sn", "yo", "so",
-    "af", "oc", "ka", "be", "tg", "sd", "gu", "am", "yi", "lo", "uz", "fo", "ht", "ps", "tk", "nn", "mt",
-    "sa", "lb", "my", "bo", "tl", "mg", "as", "tt", "haw", "ln", "ha", "ba", "jw", "su", "yue"};
-constexpr int kNumLangs = (int)(sizeof(kLangs) / sizeof(kLangs[0]));
-
-int lang_id(const std::string& code) {
-    for (int i = 0; i < kNumLangs; ++i)
-        if (code == kLangs[i]) return i;
-    return -1;
-}
-
-const char* lang_code(int id) { return (id >= 0 && id < kNumLangs) ? kLangs[id] : nullptr; }
-
 bool parse_synthetic_spec(const std::string& spec, ModelDims* dm, uint64_t* seed, std::string* err) {
     const std::string pfx = "synthetic:";
     if (spec.compare(0, pfx.size(), pfx) != 0) return false;
@@ -217,6 +183,12 @@ void Engine::import_weights(const void* dev_src, int64_t bytes) {
     select();
     HIP_CHECK(hipMemcpyAsync(warena_, dev_src, (size_t)wbytes_, hipMemcpyDeviceToDevice, st_));
     HIP_CHECK(hipStreamSynchronize(st_));
+    weights_ready_ = true;
+}
+
+void Engine::commit_weights() {
+    select();
+    HIP_CHECK(hipDeviceSynchronize());  // the writer may have used any stream of this device
     weights_ready_ = true;
 }
 
@@ -828,7 +800,12 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
     const int ctx = dm_.n_text_ctx;
     const int P = rq.row_prefix.empty() ? (int)rq.prefix.size() : (int)rq.row_prefix[0].size();
     if (Tq < 1 || Tq > 4) throw std::runtime_error("prompt must have 1..4 tokens");
-    if (B * Tq > 64) throw std::runtime_error("batch x prompt rows exceed 64");
+    if (B < 1 || B > 64) throw std::runtime_error("batch out of range");
+    // decoder passes carry at most 64 rows: a batch whose prompt rows exceed that prefills the
+    // prompt a chunk of tokens at a time (the same rows, positions and keys) and runs the
+    // logits pass on the last prompt token alone
+    const int cmax = std::max(1, std::min(4, 64 / B));
+    const int Tq_head = B * Tq > 64 ? 1 : Tq;
     if (P > ctx / 2 + 1) throw std::runtime_error("prompt prefix longer than n_text_ctx / 2 + 1");
     for (int t : rq.prefix)
         if (t < 0 || t >= dm_.n_vocab) throw std::runtime_error("prompt token out of the vocabulary");
@@ -878,7 +855,7 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         act.push_back(&g);
         HIP_CHECK(hipStreamWaitEvent(g.st, ev_[6], 0));
         // host sources of this call's token uploads (kept alive in the group until the next call)
-        g.host_tok.assign((size_t)g.B * (1 + 4 * ((P + 3) / 4 + 1)), 0);
+        g.host_tok.assign((size_t)g.B * (P + Tq + 8), 0);
         g.host_used = 0;
         if (rq.n_forced > 0)
             HIP_CHECK(hipMemcpyAsync(g.forced, rq.forced + (size_t)g.b0 * rq.n_forced, (size_t)g.B * rq.n_forced * 4,
@@ -954,22 +931,30 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         // sequence through the decoder layers only (no logits), positions 0..P-1
         const bool rows = !rq.row_prefix.empty();
         const int P = rows ? (int)rq.row_prefix[0].size() : (int)rq.prefix.size();
-        for (int c0 = 0; c0 < P; c0 += 4) {
-            const int n = std::min(4, P - c0);
+        for (int c0 = 0; c0 < P; c0 += cmax) {
+            const int n = std::min(cmax, P - c0);
             upload_tokens(g, [&](int b, int t) { return rows ? rq.row_prefix[b][c0 + t] : rq.prefix[c0 + t]; }, n);
             dec_embed(dt_, g.tok_in, g.B * n, n, dm_.d, tok_emb_, dec_pos_, g.ds, g.dx, g.st);
             enqueue_layers(g, B, n);
             dec_advance(g.ds, n, g.st);
         }
-        upload_tokens(g, [&](int b, int t) { return (t == 1 && lang[b] >= 0) ? lang[b] : rq.prompt[t]; }, Tq);
-        dec_embed(dt_, g.tok_in, g.B * Tq, Tq, dm_.d, tok_emb_, dec_pos_, g.ds, g.dx, g.st);
+        auto prompt_tok = [&](int b, int t) { return (t == 1 && lang[b] >= 0) ? lang[b] : rq.prompt[t]; };
+        for (int c0 = 0; c0 < Tq - Tq_head; c0 += cmax) {  // only when B * Tq > 64
+            const int n = std::min(cmax, Tq - Tq_head - c0);
+            upload_tokens(g, [&](int b, int t) { return prompt_tok(b, c0 + t); }, n);
+            dec_embed(dt_, g.tok_in, g.B * n, n, dm_.d, tok_emb_, dec_pos_, g.ds, g.dx, g.st);
+            enqueue_layers(g, B, n);
+            dec_advance(g.ds, n, g.st);
+        }
+        upload_tokens(g, [&](int b, int t) { return prompt_tok(b, Tq - Tq_head + t); }, Tq_head);
+        dec_embed(dt_, g.tok_in, g.B * Tq_head, Tq_head, dm_.d, tok_emb_, dec_pos_, g.ds, g.dx, g.st);
         if (rq.beam_k > 0) {  // the first step's state: no tokens yet
             beam_host_.assign((size_t)g.B * 4 + 1, 0);
             for (int b = 0; b < g.B; ++b) beam_host_[b * 4 + 3] = 3000;
             HIP_CHECK(hipMemcpyAsync(g.beam_row, beam_host_.data(), (size_t)g.B * 16, hipMemcpyHostToDevice, g.st));
             HIP_CHECK(hipMemcpyAsync(g.beam_step, beam_host_.data() + (size_t)g.B * 4, 4, hipMemcpyHostToDevice, g.st));
         }
-        enqueue_decoder_pass(g, B, Tq, rq, out_cap);  // prompt pass produces token 0
+        enqueue_decoder_pass(g, B, Tq_head, rq, out_cap);  // prompt pass produces token 0
     }
     if (rq.beam_k > 0) {  // beam search continues step by step from the host (beam_next)
         tm_.n_decode_passes = 1;
@@ -997,7 +982,8 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
     } else if (rq.n_steps > 1) {
         std::vector<hipGraphExec_t> ex;
         for (DecGroup* g : act) {
-            const GraphKey key{g->B, out_cap, rq.n_forced, rq.flags, rq.full};
+            // B_total and b0 are baked into the captured cross-K/V addresses
+            const GraphKey key{g->B, B, g->b0, out_cap, rq.n_forced, rq.flags, rq.full};
             auto it = g->graphs.find(key);
             if (it == g->graphs.end()) {
                 hipGraph_t graph;

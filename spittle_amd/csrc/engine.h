@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "kernels.h"
+#include "vocab.h"
 
 namespace spt {
 
@@ -19,13 +20,6 @@ struct ModelDims {
     int n_audio_ctx = 1500, n_text_ctx = 448;
 };
 
-// special token ids (whisper.cpp whisper_vocab + multilingual shift)
-struct Specials {
-    int eot, sot, translate, transcribe, solm, prev, nosp, not_, beg, n_langs;
-};
-Specials specials_for(int n_vocab);
-int lang_id(const std::string& code);  // whisper.cpp g_lang order; -1 if unknown
-const char* lang_code(int id);         // nullptr if out of range
 
 struct DecodeRequest {
     std::vector<int> prompt;    // [sot, (lang, task,) notimestamps]: shared by every sequence
@@ -83,6 +77,11 @@ public:
     // so two engines of one model exchange their weights byte for byte
     void export_weights(void* dev_dst, int64_t bytes);
     void import_weights(const void* dev_src, int64_t bytes);
+    // the arena itself (a collective writes rank 0's bytes straight into it), then
+    // commit_weights() marks an external-weights engine usable
+    void* weight_arena() const { return warena_; }
+    int device() const { return dev_; }
+    void commit_weights();
     int64_t workspace_bytes() const { return abytes_; }
     const Timings& timings() const { return tm_; }
 
@@ -113,12 +112,14 @@ public:
 
 private:
     struct GraphKey {
-        int B, out_cap, n_forced;
+        int B, B_total, b0, out_cap, n_forced;
         uint32_t flags;
         bool full;
         bool operator<(const GraphKey& o) const {
             if (full != o.full) return full < o.full;
             if (B != o.B) return B < o.B;
+            if (B_total != o.B_total) return B_total < o.B_total;
+            if (b0 != o.b0) return b0 < o.b0;
             if (out_cap != o.out_cap) return out_cap < o.out_cap;
             if (n_forced != o.n_forced) return n_forced < o.n_forced;
             return flags < o.flags;

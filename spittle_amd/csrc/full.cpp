@@ -217,7 +217,9 @@ void whisper_full_batch(Engine& e, const Vocab* vocab, const std::vector<const f
     const std::vector<int> nst = (p.suppress_nst && vocab) ? non_speech_tokens(*vocab) : std::vector<int>();
     const int blank = vocab ? vocab->id(" ") : 220;
     const int cap = e.max_batch();
-    const int ndec_hot = std::max(1, std::min(p.best_of, cap));
+    // best_of sampled decoders per window; more than the context's rows run in further
+    // sub-batches (beam search needs its rows together: run_full rejects beam_size > max_batch)
+    const int ndec_hot = std::max(1, p.best_of);
 
     struct Utt {
         int seek = 0, seek_end = 0;
@@ -248,6 +250,7 @@ void whisper_full_batch(Engine& e, const Vocab* vocab, const std::vector<const f
             const float t_cur = temps[it];
             const bool beam = p.beam_size > 1 && t_cur == 0.0f;  // WHISPER_SAMPLING_BEAM_SEARCH
             const int ndec = beam ? std::min(p.beam_size, cap) : t_cur > 0.0f ? ndec_hot : 1;
+            const int dchunk = std::min(ndec, cap);  // decoders of one utterance per engine call
             // prompt_past conditioning: [prev] + the last min(n_max_text_ctx, n_text_ctx / 2) tokens
             std::map<int, std::vector<int>> prefix;
             for (int u : pending) {
@@ -266,10 +269,12 @@ void whisper_full_batch(Engine& e, const Vocab* vocab, const std::vector<const f
             for (auto& kv : by_len) {
                 const std::vector<int>& grp = kv.second;
                 const int P = (int)kv.first;
-                const int per = std::max(1, cap / ndec);
-                for (size_t g0 = 0; g0 < grp.size(); g0 += per) {
+                const int per = std::max(1, cap / dchunk);
+                for (size_t g0 = 0; g0 < grp.size(); g0 += per)
+                for (int d0 = 0; d0 < ndec; d0 += dchunk) {
                     const int nj = (int)std::min<size_t>(per, grp.size() - g0);
-                    const int B = nj * ndec;
+                    const int nd = std::min(dchunk, ndec - d0);  // decoders d0 .. d0 + nd - 1
+                    const int B = nj * nd;
                     DecodeRequest rq;
                     rq.prompt = prompt_init;
                     rq.full = true;
@@ -290,25 +295,25 @@ void whisper_full_batch(Engine& e, const Vocab* vocab, const std::vector<const f
                         const int u = grp[g0 + j];
                         const int64_t off = (int64_t)us[u].seek * kHop;
                         const int avail = (int)std::max<int64_t>(0, std::min<int64_t>(kWin, n[u] - off));
-                        for (int d = 0; d < ndec; ++d) {
-                            const int r = j * ndec + d;
+                        for (int d = 0; d < nd; ++d) {
+                            const int r = j * nd + d;
                             ptr[r] = pcm[u] + std::min<int64_t>(off, n[u]);
                             ns[r] = avail;
                             rq.seek.push_back(us[u].seek);
                             rq.seek_end.push_back(us[u].seek_end);
                             if (P > 0) rq.row_prefix.push_back(prefix[u]);
-                            if (multi) rq.lang_tok.push_back(us[u].lang >= 0 ? us[u].lang : -(j * ndec + 1));
+                            if (multi) rq.lang_tok.push_back(us[u].lang >= 0 ? us[u].lang : -(j * nd + 1));
                         }
                     }
                     if (beam) {
                         rq.beam_k = ndec;
                         std::vector<std::vector<DecOut>> bo;
                         std::vector<int> lang;
-                        run_beam(e, rq, ptr, ns, nj, ndec, rq.seek, rq.seek_end, p, sp, n_max, &bo, &lang);
+                        run_beam(e, rq, ptr, ns, nj, nd, rq.seek, rq.seek_end, p, sp, n_max, &bo, &lang);
                         for (int j = 0; j < nj; ++j) {
                             const int u = grp[g0 + j];
                             if (multi && us[u].lang < 0) {
-                                us[u].lang = lang[j * ndec];
+                                us[u].lang = lang[j * nd];
                                 (*out)[u].lang_tok = us[u].lang;
                             }
                             res[u] = std::move(bo[j]);
@@ -323,12 +328,12 @@ void whisper_full_batch(Engine& e, const Vocab* vocab, const std::vector<const f
                     for (int j = 0; j < nj; ++j) {
                         const int u = grp[g0 + j];
                         if (multi && us[u].lang < 0) {  // detected once, on the utterance's first window
-                            us[u].lang = lang[j * ndec];
+                            us[u].lang = lang[j * nd];
                             (*out)[u].lang_tok = us[u].lang;
                         }
                         std::vector<DecOut>& ds = res[u];
-                        for (int d = 0; d < ndec; ++d) {
-                            const int r = j * ndec + d;
+                        for (int d = 0; d < nd; ++d) {
+                            const int r = j * nd + d;
                             DecOut o;
                             for (int s = 0; s < S; ++s) {
                                 const int tk = tok[(size_t)r * S + s];

@@ -87,7 +87,15 @@ bool GgmlFile::open(const std::string& path, std::string* err) {
         type_block(t.type, &blck, &bytes);
         if (!blck) { *err = "unsupported ggml type " + std::to_string(t.type) + " of " + t.name; return false; }
         if (t.ne[0] % blck) { *err = "row length not a multiple of the block: " + t.name; return false; }
-        t.nbytes = (size_t)(t.numel() / blck) * bytes;
+        // size from an untrusted header: bound the element count by the bytes left in the file
+        // before any product can overflow (4 dims of up to 2^31 each)
+        const uint64_t max_elems = (uint64_t)(r.end - r.p) / (uint64_t)bytes * (uint64_t)blck;
+        uint64_t n_el = 1;
+        for (int i = 0; i < t.n_dims; ++i) {
+            if ((uint64_t)t.ne[i] > max_elems / n_el) { *err = "truncated tensor data (the header claims more than the file holds): " + t.name; return false; }
+            n_el *= (uint64_t)t.ne[i];
+        }
+        t.nbytes = (size_t)(n_el / blck) * bytes;
         t.data = r.take(t.nbytes);
         if (!t.data) { *err = "truncated tensor data: " + t.name; return false; }
         index_[t.name] = tensors_.size();

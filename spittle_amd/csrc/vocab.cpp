@@ -1,11 +1,44 @@
 // vocab.cpp -- see vocab.h.
 #include "vocab.h"
 
+#include <algorithm>
 #include <regex>
 
-#include "engine.h"
-
 namespace spt {
+
+Specials specials_for(int n_vocab) {
+    // whisper.cpp whisper_vocab defaults, shifted for multilingual vocabularies in
+    // whisper_model_load (language count = n_vocab - 51765 - multilingual)
+    Specials s{50256, 50257, 50357, 50358, 50359, 50360, 50361, 50362, 50363, 0};
+    const bool multi = n_vocab >= 51865;
+    const int n_langs = n_vocab - 51765 - (multi ? 1 : 0);
+    if (multi) {
+        s.eot++;
+        s.sot++;
+        const int dt = n_langs - 98;
+        s.translate += dt; s.transcribe += dt; s.solm += dt; s.prev += dt; s.nosp += dt; s.not_ += dt; s.beg += dt;
+        s.n_langs = n_langs;
+    }
+    return s;
+}
+
+static const char* const kLangs[] = {
+    "en", "zh", "de", "es", "ru", "ko", "fr", "ja", "pt", "tr", "pl", "ca", "nl", "ar", "sv", "it", "id",
+    "hi", "fi", "vi", "he", "uk", "el", "ms", "cs", "ro", "da", "hu", "ta", "no", "th", "ur", "hr", "bg",
+    "lt", "la", "mi", "ml", "cy", "sk", "te", "fa", "lv", "bn", "sr", "az", "sl", "kn", "et", "mk", "br",
+    "eu", "is", "hy", "ne", "mn", "bs", "kk", "sq", "sw", "gl", "mr", "pa", "si", "km", "sn", "yo", "so",
+    "af", "oc", "ka", "be", "tg", "sd", "gu", "am", "yi", "lo", "uz", "fo", "ht", "ps", "tk", "nn", "mt",
+    "sa", "lb", "my", "bo", "tl", "mg", "as", "tt", "haw", "ln", "ha", "ba", "jw", "su", "yue"};
+constexpr int kNumLangs = (int)(sizeof(kLangs) / sizeof(kLangs[0]));
+
+int lang_id(const std::string& code) {
+    for (int i = 0; i < kNumLangs; ++i)
+        if (code == kLangs[i]) return i;
+    return -1;
+}
+
+const char* lang_code(int id) { return (id >= 0 && id < kNumLangs) ? kLangs[id] : nullptr; }
+
 
 Vocab::Vocab(const std::vector<std::string>& file_tokens, int n_vocab, const Specials& sp) {
     const int n = std::max<int>(n_vocab, (int)file_tokens.size());

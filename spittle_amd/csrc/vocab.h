@@ -10,7 +10,13 @@
 
 namespace spt {
 
-struct Specials;
+// special token ids (whisper.cpp whisper_vocab + multilingual shift)
+struct Specials {
+    int eot, sot, translate, transcribe, solm, prev, nosp, not_, beg, n_langs;
+};
+Specials specials_for(int n_vocab);
+int lang_id(const std::string& code);  // whisper.cpp g_lang order; -1 if unknown
+const char* lang_code(int id);         // nullptr if out of range
 
 class Vocab {
 public:

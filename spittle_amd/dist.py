@@ -49,13 +49,42 @@ def max_over_ranks(value: float, device=None, group=None) -> float:
     return float(t.item())
 
 
-def broadcast_weights(engine, device=None, group=None, src: int = 0) -> dict:
-    """Replicate `src`'s weight arena into every rank's engine with one broadcast.
+class _DeviceBytes:
+    """A raw device allocation seen through __cuda_array_interface__ (torch.as_tensor aliases it)."""
+
+    def __init__(self, ptr: int, nbytes: int):
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False),
+                                         "strides": None, "version": 3}
+
+
+def arena_tensor(engine, device):
+    """The engine's weight arena as a uint8 tensor that ALIASES it (no copy): a collective on
+    this tensor writes straight into the engine.  `device` is the engine's CUDA device
+    (``"cpu"`` only for host-memory stand-ins in CPU tests)."""
+    import ctypes
+
+    import torch
+    ptr, nbytes = engine.weights_arena()
+    dev = torch.device(device)
+    if dev.type == "cpu":
+        return torch.frombuffer((ctypes.c_uint8 * nbytes).from_address(ptr), dtype=torch.uint8)
+    if dev.type != "cuda":
+        raise ValueError(f"arena_tensor: the arena lives on a GPU, got device {device}")
+    t = torch.as_tensor(_DeviceBytes(ptr, nbytes), device=dev)
+    if t.data_ptr() != ptr or t.numel() != nbytes:
+        raise RuntimeError("arena_tensor: torch did not alias the weight arena")
+    return t
+
+
+def broadcast_weights(engine, device, group=None, src: int = 0) -> dict:
+    """Replicate `src`'s weight arena into every rank's engine with one broadcast, straight
+    into the arenas (no staging buffer, no device copies).
 
     Every rank must have loaded the same model spec and dtype; ranks other than `src` created
-    their engine with ``WhisperModelParams(external_weights=True)``.  The arena travels as one
-    uint8 tensor (RCCL on GPU tensors; gloo also works, via the host).  Returns the size and
-    the wall time of the broadcast on this rank.
+    their engine with ``WhisperModelParams(external_weights=True)`` and are committed
+    (spt_weights_commit) after the broadcast.  On RCCL (backend "nccl") the arena tensors are
+    the collective's buffers; gloo (a one-GPU rehearsal of N ranks) moves the bytes through a
+    host copy.  Returns the size and the wall time of the broadcast on this rank.
     """
     import time
 
@@ -69,17 +98,19 @@ def broadcast_weights(engine, device=None, group=None, src: int = 0) -> dict:
     dist.all_gather_object(sizes, nbytes, group=group)
     if len(set(sizes)) != 1:
         raise RuntimeError(f"broadcast_weights: ranks disagree on the weight arena size: {sizes}")
-    buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
-    if rank == src:
-        engine.export_weights(buf.data_ptr(), nbytes)
-    if buf.is_cuda:
-        torch.cuda.synchronize(buf.device)
+    arena = arena_tensor(engine, device)
+    via_host = arena.is_cuda and dist.get_backend(group) == "gloo"
+    buf = (arena.cpu() if rank == src else torch.empty(nbytes, dtype=torch.uint8)) if via_host else arena
+    if arena.is_cuda:
+        torch.cuda.synchronize(arena.device)
     t0 = time.perf_counter()
     dist.broadcast(buf, src=src, group=group)
-    if buf.is_cuda:
-        torch.cuda.synchronize(buf.device)
+    if arena.is_cuda:
+        torch.cuda.synchronize(arena.device)
     ms = (time.perf_counter() - t0) * 1e3
     if rank != src:
-        engine.import_weights(buf.data_ptr(), nbytes)
-    del buf
-    return {"bytes": nbytes, "ms": ms}
+        if via_host:
+            arena.copy_(buf)
+        engine.commit_weights()
+    del buf, arena
+    return {"bytes": nbytes, "ms": ms, "path": "host (gloo)" if via_host else "in place"}

@@ -234,6 +234,18 @@ class WhisperEngine:
         self._need()
         self._check(self._lib.spt_weights_import(self._ctx, C.c_void_p(dev_ptr), C.c_size_t(nbytes)))
 
+    def weights_arena(self) -> tuple:
+        """(device pointer, bytes) of the weight arena: a collective writes straight into it."""
+        self._need()
+        ptr, n = C.c_void_p(), C.c_size_t()
+        self._check(self._lib.spt_weights_arena(self._ctx, C.byref(ptr), C.byref(n)))
+        return int(ptr.value or 0), int(n.value)
+
+    def commit_weights(self) -> None:
+        """Mark an external-weights engine usable once its arena holds the model's bytes."""
+        self._need()
+        self._check(self._lib.spt_weights_commit(self._ctx))
+
     def info(self) -> dict:
         self._need()
         mi = L.ModelInfo()

@@ -76,24 +76,21 @@ def test_run_sharded_gloo_world2():
 
 class _HostArenaEngine:
     """Stand-in for WhisperEngine's weight-arena calls on CPU memory (the host logic of
-    broadcast_weights; the device copies themselves are covered by test_gpu_parity)."""
+    broadcast_weights; the device path is covered by the -m gpu tests)."""
 
     def __init__(self, nbytes, fill=None):
         import numpy as np
         self.arena = np.zeros(nbytes, np.uint8) if fill is None else fill.copy()
+        self.committed = fill is not None
 
     def info(self):
         return {"weight_bytes": self.arena.size}
 
-    def export_weights(self, ptr, nbytes):
-        import ctypes
-        assert nbytes == self.arena.size
-        ctypes.memmove(ptr, self.arena.ctypes.data, nbytes)
+    def weights_arena(self):
+        return self.arena.ctypes.data, self.arena.size
 
-    def import_weights(self, ptr, nbytes):
-        import ctypes
-        assert nbytes == self.arena.size
-        ctypes.memmove(self.arena.ctypes.data, ptr, nbytes)
+    def commit_weights(self):
+        self.committed = True
 
 
 def _bcast_worker(rank, world, port, q, sizes):
@@ -107,8 +104,8 @@ def _bcast_worker(rank, world, port, q, sizes):
     src = np.random.default_rng(7).integers(0, 256, n, dtype=np.uint8)
     eng = _HostArenaEngine(n, fill=src if rank == 0 else None)
     try:
-        info = broadcast_weights(eng)
-        q.put((rank, "ok", bool((eng.arena == src).all()), info["bytes"]))
+        info = broadcast_weights(eng, device="cpu")
+        q.put((rank, "ok", bool((eng.arena == src).all()) and eng.committed, info["bytes"]))
     except RuntimeError as e:
         q.put((rank, "err", str(e), 0))
     dist.barrier()
