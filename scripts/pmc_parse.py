@@ -14,6 +14,14 @@ SEL = {
     "dec_cross_attn": lambda n: re.search(r"cross_attn_kernel<unsigned short, 1[,>]", n) is not None,
     "dec_logits": lambda n: "gemv_kernel<unsigned short, 4," in n,
     "enc_fc1_gemm": lambda n: "gemm256_kernel<1>" in n,
+    # decoder GEMVs (template <T, MODE, ASRC, RG, ...>; MODE 0 bias, 1 bias+GELU, 2 partial, 3 QKV+cache,
+    # 5 bias+residual; ASRC 0 direct, 16 + n LayerNorm over x + n pending slabs), batch 8 (RG 1)
+    "dec_qkv": lambda n: "gemv_kernel<unsigned short, 3, 18, 1," in n,
+    "dec_self_cross_out": lambda n: "gemv_kernel<unsigned short, 5, 0, 1," in n,
+    "dec_cross_q": lambda n: "gemv_kernel<unsigned short, 0, 16, 1," in n,
+    "dec_fc1": lambda n: "gemv_kernel<unsigned short, 1, 16, 1," in n,
+    "dec_fc2": lambda n: "gemv_kernel<unsigned short, 2, 0, 1," in n,
+    "dec_self_attn": lambda n: "self_attn_kernel<unsigned short, 1," in n,
 }
 vals = {k: defaultdict(list) for k in SEL}
 for counter in ("FETCH_SIZE", "WRITE_SIZE"):

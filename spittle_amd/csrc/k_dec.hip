@@ -108,8 +108,19 @@ constexpr int ATTN_SRC(int s) { return 32 + s; }
 constexpr bool is_attn(int asrc) { return asrc >= 32; }
 constexpr int attn_s(int asrc) { return asrc - 32; }
 
-template <typename T, int MODE, int ASRC, int RG, int NWV, int CT, int MAXJ>
+#ifndef SPT_STAMP
+#define SPT_STAMP 0
+#endif
+// developer timeline (SPT_STAMP=1 builds): thread 0's view of its workgroup's start / end
+#define GV_STAMP(i)                                                                                       \
+    do {                                                                                                  \
+        if (SPT_STAMP && a.stamp && threadIdx.x == 0)                                                     \
+            a.stamp[2 * (blockIdx.x + blockIdx.y * gridDim.x) + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+
+template <typename T, int MODE, int ASRC, int RG, int NWV, int CT, int MAXJ, bool EXACT = false>
 __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
+    GV_STAMP(0);
     constexpr int KS = GV<T>::KS;
     constexpr int CPE = 16 / sizeof(T);  // elements per 16-byte chunk
     constexpr int KSPLIT = NWV / CT;
@@ -133,11 +144,17 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
     const T* wrow = (const T*)a.W + (size_t)min(n0 + fr, a.N - 1) * K + fq * CPE;
 
     frag w[MAXJ][4];
+    // EXACT (every wave's K slice is exactly MAXJ super-steps, checked at launch): the weight
+    // loads are unconditional, so the compiler can wait for the LayerNorm rows and prefetched
+    // operands (issued before them) with a counted vmcnt that leaves the weight stream in flight.
+    // Otherwise a predicated load makes every such wait a vmcnt(0) (r2: the LayerNorm then ran
+    // only after the weights had landed); forcing unconditional loads there instead (waves
+    // re-reading a super-step) measured slower (r2 exp_r2c).
     auto load_chunk = [&](int j0) {
 #pragma unroll
         for (int j = 0; j < MAXJ; ++j) {
             const int ss = ss0 + ks + (j0 + j) * KSPLIT;
-            if (ss < ss1) {
+            if (EXACT || ss < ss1) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) w[j][i] = load_w((const frag*)(wrow + (size_t)ss * KS + i * 4 * CPE));
             }
@@ -159,6 +176,45 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
 #pragma unroll
                     for (int p = 0; p < NP; ++p) x0[p + 1][i] = *(const float4*)(a.pend[p] + ro + k);
                 }
+            }
+        }
+    }
+    // Every operand of the LayerNorm and of the epilogue is fetched here, up front, beside the
+    // LayerNorm rows and before the weight stream: a workgroup then pays one memory round trip
+    // (kernel arguments aside) instead of one per dependent stage (r2 chain timeline: the
+    // epilogue's bias / residual loads and the LayerNorm's gain / shift loads were each a round
+    // trip after the weights had arrived).
+    const int n_ep = n0 + fr;  // the output column this lane finishes
+    const bool ep_lane = ks == 0 && n_ep < a.N;
+    float bias_pre = 0.f;
+    if constexpr (MODE != GV_LOGITS) {
+        if (ep_lane && a.bias && kz == 0) bias_pre = a.bias[n_ep];
+    }
+    float resid_pre[RG][4];
+    if constexpr (MODE == GV_BIAS_RESID) {
+#pragma unroll
+        for (int g = 0; g < RG; ++g)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = g * 16 + 4 * fq + r;
+                resid_pre[g][r] = (ep_lane && row < a.R) ? ((const float*)a.C)[(size_t)row * a.ldc + n_ep] : 0.f;
+            }
+    }
+    int st_pre = 0;  // decoder step state: GV_QKV_CACHE appends at pos0, GV_LOGITS reads step
+    if constexpr (MODE == GV_QKV_CACHE) st_pre = a.st->pos0;
+    if constexpr (MODE == GV_LOGITS) st_pre = a.st->step;
+    uint32_t sup_pre = 0;
+    if constexpr (MODE == GV_LOGITS) {
+        if (n_ep < a.N) sup_pre = a.suppress[n_ep >> 5];
+    }
+    float4 lnw_pre[6], lnb_pre[6];
+    if constexpr (is_ln(ASRC)) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const int k = lane * 4 + 256 * i;
+            if (k < K) {
+                lnw_pre[i] = *(const float4*)(a.ln_w + k);
+                lnb_pre[i] = *(const float4*)(a.ln_b + k);
             }
         }
     }
@@ -209,8 +265,8 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
             for (int i = 0; i < 6; ++i) {
                 const int k = lane * 4 + 256 * i;
                 if (k < K) {
-                    const float4 g = *(const float4*)(a.ln_w + k);
-                    const float4 b = *(const float4*)(a.ln_b + k);
+                    const float4 g = lnw_pre[i];
+                    const float4 b = lnb_pre[i];
                     T* o = img + (size_t)r * lds_ld + k;
                     o[0] = from_f<T>((v[i].x - mean) * rstd * g.x + b.x);
                     o[1] = from_f<T>((v[i].y - mean) * rstd * g.y + b.y);
@@ -263,7 +319,7 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
 #pragma unroll
         for (int j = 0; j < MAXJ; ++j) {
             const int ss = ss0 + ks + (j0 + j) * KSPLIT;
-            if (ss >= ss1) break;
+            if (!EXACT && ss >= ss1) break;
             const int kb = ss * KS + fq * CPE;
 #pragma unroll
             for (int g = 0; g < RG; ++g) {
@@ -295,9 +351,13 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
             }
         }
     };
-    for (int j0 = 0; ss0 + ks + j0 * KSPLIT < ss1; j0 += MAXJ) {
-        if (j0 > 0) load_chunk(j0);
-        compute_chunk(j0);
+    if constexpr (EXACT) {
+        compute_chunk(0);
+    } else {
+        for (int j0 = 0; ss0 + ks + j0 * KSPLIT < ss1; j0 += MAXJ) {
+            if (j0 > 0) load_chunk(j0);
+            compute_chunk(j0);
+        }
     }
 
     // cross-wave K reduction (waves sharing a column tile)
@@ -319,11 +379,11 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
     const int n = n0 + fr;
     if constexpr (MODE == GV_LOGITS) {
         // logits + this tile's suppressed top-2 per row (finished by dec_finalize)
-        const int step = a.st->step;
+        const int step = st_pre;
         const bool nvalid = n < a.N;
         bool sup = !nvalid;
         if (nvalid) {
-            sup = (a.suppress[n >> 5] >> (n & 31)) & 1u;
+            sup = (sup_pre >> (n & 31)) & 1u;
             if (step == 0 && (n == a.blank0 || n == a.blank1)) sup = true;
         }
 #pragma unroll
@@ -341,10 +401,11 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
                 if (fr == 0 && row < a.R && tile < a.n_tiles) ((TopP*)a.part)[(size_t)row * a.n_tiles + tile] = t;
             }
         }
+        GV_STAMP(1);
         return;
     }
     if (n >= a.N) return;
-    const float bv = (a.bias && kz == 0) ? a.bias[n] : 0.0f;
+    const float bv = bias_pre;
 #pragma unroll
     for (int g = 0; g < RG; ++g) {
 #pragma unroll
@@ -359,7 +420,7 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
             } else if constexpr (MODE == GV_PARTIAL) {
                 ((float*)a.C + (size_t)kz * a.c_split)[(size_t)row * a.ldc + n] = y;
             } else if constexpr (MODE == GV_BIAS_RESID) {
-                ((float*)a.C)[(size_t)row * a.ldc + n] += y;
+                ((float*)a.C)[(size_t)row * a.ldc + n] = resid_pre[g][r] + y;
             } else if constexpr (MODE == GV_QKV_CACHE) {
                 const int d = a.cache_H * 64;
                 if (n < d) {
@@ -369,27 +430,30 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
                     const int rem = n - (part + 1) * d;
                     const int hh = rem >> 6, e = rem & 63;
                     const int bb = row / a.Tq, t = row - bb * a.Tq;
-                    const int pos = a.st->pos0 + t;
+                    const int pos = st_pre + t;
                     const size_t off = ((((size_t)part * a.cache_B + bb) * a.cache_H + hh) * a.cache_ctx + pos) * 64 + e;
                     ((T*)a.cache)[off] = from_f<T>(y);
                 }
             }
         }
     }
+    GV_STAMP(1);
 }
 
-template <typename T, int MODE, int ASRC, int RG, int NWV, int CT, int MAXJ>
+template <typename T, int MODE, int ASRC, int RG, int NWV, int CT, int MAXJ, bool EXACT = false>
 void gemv_attr() {
     const int red = NWV * RG * 64 * (int)sizeof(f32x4);
-    HIP_CHECK(hipFuncSetAttribute((const void*)gemv_kernel<T, MODE, ASRC, RG, NWV, CT, MAXJ>,
+    HIP_CHECK(hipFuncSetAttribute((const void*)gemv_kernel<T, MODE, ASRC, RG, NWV, CT, MAXJ, EXACT>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, GV_LDS_BYTES + red));
 }
 
-template <typename T, int MODE, int ASRC, int RG, int NWV, int CT, int MAXJ>
+template <typename T, int MODE, int ASRC, int RG, int NWV, int CT, int MAXJ, bool EXACT = false>
 void gemv_launch_cfg(const GemvArgs& a, hipStream_t st) {
+    if (EXACT && cdiv(a.K / GV<T>::KS, a.ksplit) != MAXJ * (NWV / CT))
+        throw std::runtime_error("gemv: exact configuration does not match the K slice");
     const int red = NWV * RG * 64 * (int)sizeof(f32x4);
     const int lds = (ASRC != A_DIRECT ? gv_img_bytes(a.R, a.K, sizeof(T)) : 0) + (NWV / CT > 1 ? red : 0);
-    hipLaunchKernelGGL((gemv_kernel<T, MODE, ASRC, RG, NWV, CT, MAXJ>), dim3(cdiv(a.N, 16 * CT), a.ksplit),
+    hipLaunchKernelGGL((gemv_kernel<T, MODE, ASRC, RG, NWV, CT, MAXJ, EXACT>), dim3(cdiv(a.N, 16 * CT), a.ksplit),
                        dim3(64 * NWV), lds, st, a);
     SPT_LAUNCH_CHECK();
 }
@@ -433,6 +497,12 @@ void gemv_attr_all() {
         SPT_ATTR(4, 1, 2)
         SPT_ATTR(8, 1, 2)
         SPT_ATTR(8, 2, 3)
+        gemv_attr<T, MODE, ASRC, 1, 10, 1, 1, true>();
+        gemv_attr<T, MODE, ASRC, 2, 10, 1, 1, true>();
+        gemv_attr<T, MODE, ASRC, 4, 10, 1, 1, true>();
+        gemv_attr<T, MODE, ASRC, 1, 10, 2, 2, true>();
+        gemv_attr<T, MODE, ASRC, 2, 10, 2, 2, true>();
+        gemv_attr<T, MODE, ASRC, 4, 10, 2, 2, true>();
     }
 #undef SPT_ATTR
 }
@@ -453,6 +523,14 @@ void gemv_launch_rg(const GemvArgs& a, hipStream_t st) {
         // so half as many workgroups re-read the residual rows for their LayerNorm image (r1
         // exp23: fc1 9.4 -> 8.6 us, RTFx +1.2 %; the QKV and cross-Q projections lose with it)
         if constexpr (ASRC != A_DIRECT) {
+            // K = 10 super-steps (large-v3's d = 1280 in bf16): 10 waves, each an exact slice, so
+            // the LayerNorm does not wait for the weight stream (GV_EXACT_LN=0 restores r1's shapes)
+            static const bool exact_ln = !getenv("GV_EXACT_LN") || atoi(getenv("GV_EXACT_LN")) != 0;
+            if (exact_ln && nss == 10) {
+                if (a.N >= 4096) gemv_launch_cfg<T, MODE, ASRC, RG, 10, 2, 2, true>(a, st);
+                else gemv_launch_cfg<T, MODE, ASRC, RG, 10, 1, 1, true>(a, st);
+                return;
+            }
             if (a.N >= 4096 && nss <= 24) {
                 gemv_launch_cfg<T, MODE, ASRC, RG, 8, 2, 3>(a, st);
                 return;

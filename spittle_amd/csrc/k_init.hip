@@ -122,6 +122,23 @@ void cache_flush(const void* p, int64_t bytes, unsigned* sink, hipStream_t st) {
     hipLaunchKernelGGL(touch_kernel, dim3(2048), dim3(256), 0, st, (const uint4*)p, bytes >> 4, sink);
 }
 
+// developer bandwidth probe: grid-stride 16 B per lane, 4 loads in flight per lane
+__global__ void stream_kernel(const uint4* __restrict__ p, int64_t n16, unsigned* sink) {
+    uint32_t acc = 0;
+    const int64_t s = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * s < n16; i += 4 * s) {
+        const uint4 a = p[i], b = p[i + s], c = p[i + 2 * s], d = p[i + 3 * s];
+        acc ^= a.x ^ b.y ^ c.z ^ d.w;
+    }
+    for (; i < n16; i += s) acc ^= p[i].x;
+    if (acc == 0x9e3779b9u && threadIdx.x == 0x3ff) *sink = acc;
+}
+
+void stream_read(const void* p, int64_t bytes, unsigned* sink, int grid, int tpb, hipStream_t st) {
+    hipLaunchKernelGGL(stream_kernel, dim3(grid), dim3(tpb), 0, st, (const uint4*)p, bytes >> 4, sink);
+}
+
 // ---------------------------------------------------------------- ggml weight dequantisation
 // Model loading (ggml_file.h): the raw ggml blocks are copied to the device as they lie in the
 // file and expanded here into the engine's storage type, one thread per block (per element for

@@ -37,6 +37,7 @@ void fill_f32(float* dst, int64_t n, float v, hipStream_t st);
 // ggml type id (ggml_quant.h GQ_*), n a multiple of the type's block
 void ggml_dequant(int type, const void* src, int64_t n, int out_dtype, void* dst, hipStream_t st);
 void cache_flush(const void* p, int64_t bytes, unsigned* sink, hipStream_t st);
+void stream_read(const void* p, int64_t bytes, unsigned* sink, int grid, int tpb, hipStream_t st);  // ubench probe
 // weight checksum helper for tests: sum of |w| and sum of w (f64) of a device tensor
 void tensor_checksum(int dtype, const void* src, int64_t n, double* out2_dev, hipStream_t st);
 
@@ -93,6 +94,9 @@ struct GemvArgs {
     // GV_LOGITS: suppression + per-16-column-tile top-2 partials [R][n_tiles] (16 B each)
     const uint32_t* suppress; int blank0, blank1;
     void* part; int n_tiles;
+    // SPT_STAMP builds only (developer timeline): s_memrealtime at each workgroup's start / end,
+    // [2 * workgroup + {0, 1}]
+    unsigned long long* stamp;
 };
 constexpr int kMaxPend = 4;
 void gemv(int dtype, int mode, int asrc, const GemvArgs& a, hipStream_t st);

@@ -72,6 +72,123 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
+    if (what == "chain") {
+        // a captured graph of NL dependent launches of one decoder GEMV shape, every launch on its
+        // own weights (cache-cold: a 512 MB read precedes each replay), as in the decode loop.
+        // kind: 0 null kernel; 1 self/cross-out (resid, A_DIRECT, N=K=1280); 2 cross-Q (LN, N=K=1280);
+        // 3 QKV (LN + 2 pending slabs, N=3840); 4 fc1 (LN, GELU, N=5120); 5 fc2 (K=5120, 2 slabs)
+        // SPT_STAMP builds print the workgroup timeline: per launch the start of its first workgroup
+        // after the previous launch's last end (gap), start spread, first / last end.
+        const int kind = ai(2, 1), NL = ai(3, 48), G = ai(4, 80), dt = DT_BF16, d = 1280, B = 8;
+        gemv_prepare(dt);
+        const int N = kind == 3 ? 3 * d : kind == 4 ? 4 * d : d, K = kind == 5 ? 4 * d : d;
+        std::vector<void*> Ws(NL);
+        for (int l = 0; l < NL; ++l) Ws[l] = drand((size_t)N * K, dt, 100 + l, -5);
+        float* bias = frand(N, 2, -5);
+        float* lnw = frand(K, 3, -3);
+        float* lnb = frand(K, 4, -4);
+        float* x = frand((size_t)B * K, 5, 0);
+        void* A = drand((size_t)B * K, dt, 6, 0);
+        float* pend = frand((size_t)4 * B * d, 7, -3);
+        float* x2 = (float*)dalloc((size_t)B * d * 4);
+        void* C = dalloc((size_t)4 * B * N * 4 + 64);
+        void* cache = dalloc((size_t)2 * B * 20 * 448 * 64 * 2);
+        void* flush = dalloc((size_t)512 << 20);
+        unsigned* scratch = (unsigned*)dalloc(64);
+        const int maxwg = 1024;
+        unsigned long long* stamps = (unsigned long long*)dalloc((size_t)NL * maxwg * 2 * 8);
+        int* np = (int*)dalloc(4);
+        auto launch = [&](int l) {
+            unsigned long long* sp = stamps + (size_t)l * maxwg * 2;
+            if (kind == 0) {
+                hipLaunchKernelGGL(null_kernel, dim3(G), dim3(512), 0, st, np);
+                return;
+            }
+            GemvArgs a{};
+            a.R = B; a.K = K; a.N = N; a.W = Ws[l]; a.bias = bias; a.stamp = sp;
+            for (int p = 0; p < kMaxPend; ++p) a.pend[p] = pend + (size_t)p * B * d;
+            if (kind == 1) {
+                a.A = A; a.lda = K; a.C = x; a.ldc = d;
+                gemv(dt, GV_BIAS_RESID, A_DIRECT, a, st);
+            } else if (kind == 5) {
+                a.A = A; a.lda = K; a.C = pend; a.ldc = d; a.c_split = (int64_t)B * d; a.ksplit = 2;
+                a.A = C; a.lda = K;  // any bf16 rows of width K (contents irrelevant)
+                gemv(dt, GV_PARTIAL, A_DIRECT, a, st);
+            } else {
+                a.A = x; a.lda = K; a.ln_w = lnw; a.ln_b = lnb;
+                a.n_pend = kind == 3 ? 2 : 0;
+                a.x_out = kind == 3 ? x2 : nullptr;
+                a.C = C; a.ldc = kind == 3 ? d : N;
+                if (kind == 3) {
+                    a.cache = cache; a.cache_B = B; a.cache_H = 20; a.cache_ctx = 448; a.Tq = 1; a.st = ds;
+                    gemv(dt, GV_QKV_CACHE, A_LN, a, st);
+                } else {
+                    gemv(dt, kind == 4 ? GV_BIAS_GELU : GV_BIAS, A_LN, a, st);
+                }
+            }
+        };
+        HIP_CHECK(hipDeviceSynchronize());
+        hipGraph_t g;
+        HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+        for (int l = 0; l < NL; ++l) launch(l);
+        HIP_CHECK(hipStreamEndCapture(st, &g));
+        hipGraphExec_t ge;
+        HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+        hipEvent_t e0, e1;
+        HIP_CHECK(hipEventCreate(&e0));
+        HIP_CHECK(hipEventCreate(&e1));
+        double tot = 0;
+        const int reps = 6;
+        for (int r = 0; r < reps; ++r) {
+            cache_flush(flush, (int64_t)512 << 20, scratch, st);
+            HIP_CHECK(hipEventRecord(e0, st));
+            HIP_CHECK(hipGraphLaunch(ge, st));
+            HIP_CHECK(hipEventRecord(e1, st));
+            HIP_CHECK(hipEventSynchronize(e1));
+            float ms;
+            HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+            if (r > 0) tot += ms;
+        }
+        const double us = tot * 1000.0 / ((reps - 1) * NL);
+        printf("chain kind=%d N=%d K=%d launches=%d : %.2f us per launch  %.0f GB/s\n", kind, N, K, NL, us,
+               kind ? (double)N * K * 2 / us / 1e3 : 0.0);
+        if (kind > 0) {
+            std::vector<unsigned long long> h((size_t)NL * maxwg * 2);
+            HIP_CHECK(hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost));
+            const int nwg = kind == 5 ? 2 * (N / 16) : (kind == 4 ? N / 32 : N / 16);
+            double sg = 0, ss = 0, sf = 0, sl = 0;
+            unsigned long long prev_end = 0;
+            int cnt = 0;
+            for (int l = 0; l < NL; ++l) {
+                unsigned long long s0 = ~0ull, s1 = 0, e0_ = ~0ull, e1_ = 0;
+                for (int w = 0; w < nwg; ++w) {
+                    const unsigned long long a0 = h[((size_t)l * maxwg + w) * 2], a1 = h[((size_t)l * maxwg + w) * 2 + 1];
+                    s0 = std::min(s0, a0); s1 = std::max(s1, a0); e0_ = std::min(e0_, a1); e1_ = std::max(e1_, a1);
+                }
+                if (l > 0 && s0 >= prev_end) {
+                    sg += (s0 - prev_end) * 0.01; ss += (s1 - s0) * 0.01; sf += (e0_ - s0) * 0.01; sl += (e1_ - s0) * 0.01;
+                    ++cnt;
+                }
+                prev_end = e1_;
+            }
+            if (cnt)
+                printf("  timeline (us, mean over %d launches): gap prev-last-end -> first-start %.2f | start spread %.2f | "
+                       "first end %.2f | last end %.2f\n", cnt, sg / cnt, ss / cnt, sf / cnt, sl / cnt);
+        }
+        return 0;
+    }
+    if (what == "stream") {  // bandwidth ceiling of a plain coalesced read of NL x 61.4 MB (one per launch)
+        const int G = ai(2, 1024), TPB = ai(3, 256), NL = 8;
+        const size_t bytes = (size_t)61440000;
+        void* buf = dalloc(bytes * NL);
+        unsigned* sink = (unsigned*)dalloc(64);
+        HIP_CHECK(hipDeviceSynchronize());
+        const double us = time_us(st, 10, [&] {
+            for (int l = 0; l < NL; ++l) stream_read((const char*)buf + bytes * l, (int64_t)bytes, sink, G, TPB, st);
+        }) / NL;
+        printf("stream grid=%d x %d : %.2f us per 61.4 MB  %.0f GB/s\n", G, TPB, us, bytes / us / 1e3);
+        return 0;
+    }
     if (what == "gemv") {
         const int N = ai(2, 1280), K = ai(3, 1280), R = ai(4, 8), mode = ai(5, 2), ln = ai(6, 0), dt = ai(7, DT_BF16),
                   ksplit = ai(8, 1), npend = ai(9, 0);
@@ -122,11 +239,12 @@ int main(int argc, char** argv) {
         const size_t layer = (size_t)2 * B * H * T * 64;
         void* kv = drand(layer * NL, dt, 2, 0);
         void* out = dalloc((size_t)B * d * esz);
-        float* part = (float*)dalloc((size_t)B * H * 4 * 66 * 4);
+        float* part = (float*)dalloc((size_t)B * H * 32 * 66 * 4);
         HIP_CHECK(hipDeviceSynchronize());
         const double us = time_us(st, 10, [&] {
-            for (int l = 0; l < NL; ++l)
+            for (int l = 0; l < NL; ++l) {
                 dec_cross_attn(dt, q, (const char*)kv + layer * l * esz, B, B, H, T, 1, out, st, S, part);
+            }
         }) / NL;
         printf("cross-attn B=%d T=%d splits=%d dt=%d (8 layers back to back) : %.2f us  %.0f GB/s\n", B, T, S, dt, us,
                2.0 * B * H * T * 64 * esz / us / 1e3);

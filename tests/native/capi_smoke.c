@@ -1,0 +1,102 @@
+/* capi_smoke.c -- the exact call sequence the Rust binding (rust/spittle-hip) performs, in C,
+ * through include/spittle_hip.h and libspittle_hip.so:
+ *   load_model          spt_default_model_params + spt_ctx_create   (transcription.rs:261-276)
+ *   transcribe_samples  spt_default_infer_params + language/initial_prompt + spt_transcribe
+ *                       -> read text / segments -> spt_result_free    (transcription.rs:494-503)
+ *   unload_model        spt_ctx_destroy                               (transcription.rs:175-208)
+ * then the same again (the idle watcher unloads, the next dictation reloads), and the error
+ * paths the binding maps to Err(..).  Exit 0 = every step behaved. */
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "spittle_hip.h"
+
+#define CHECK(c, msg)                                                       \
+    do {                                                                    \
+        if (!(c)) {                                                         \
+            fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, msg);   \
+            return 1;                                                       \
+        }                                                                   \
+    } while (0)
+
+static int one_session(const char* spec, const float* pcm, size_t n) {
+    spt_model_params mp;
+    spt_default_model_params(&mp);
+    mp.dtype = SPT_DTYPE_F32;
+    mp.max_batch = 5; /* whisper_full's best_of decoders fit one call */
+    spt_ctx* ctx = NULL;
+    char err[512] = {0};
+    spt_status st = spt_ctx_create(spec, &mp, &ctx, err, sizeof err);
+    if (st != SPT_OK) fprintf(stderr, "create: %s\n", err);
+    CHECK(st == SPT_OK && ctx, "spt_ctx_create");
+
+    spt_model_info info;
+    CHECK(spt_ctx_info(ctx, &info) == SPT_OK && info.n_audio_ctx == 1500, "spt_ctx_info");
+
+    /* the app's params: whisper_full defaults + language + (for ggml models) initial_prompt */
+    spt_infer_params ip;
+    spt_default_infer_params(&ip);
+    ip.language = "en";
+    ip.max_new_tokens = 16;
+    spt_result* r = NULL;
+    st = spt_transcribe(ctx, pcm, n, &ip, &r);
+    if (st != SPT_OK) fprintf(stderr, "transcribe: %s\n", spt_last_error(ctx));
+    CHECK(st == SPT_OK && r && r->text, "spt_transcribe (whisper_full defaults)");
+    CHECK(r->n_windows >= 1 && r->n_tokens >= 0, "result fields");
+    for (int i = 0; i < r->n_segments; ++i)
+        CHECK(r->segments[i].text && r->segments[i].t1 >= r->segments[i].t0, "segment");
+    printf("whisper_full: %d tokens, %d segments, text \"%.60s\"\n", r->n_tokens, r->n_segments, r->text);
+    spt_result_free(r);
+
+    /* an initial_prompt needs a vocabulary: a synthetic model reports it, it does not crash */
+    ip.initial_prompt = "Technical dictation. Common terms: Kubernetes";
+    r = NULL;
+    st = spt_transcribe(ctx, pcm, n, &ip, &r);
+    CHECK(st == SPT_ERR_UNSUPPORTED && r == NULL && strlen(spt_last_error(ctx)) > 0, "initial_prompt without vocab");
+    ip.initial_prompt = NULL;
+
+    /* empty audio: "" without device work */
+    r = NULL;
+    CHECK(spt_transcribe(ctx, pcm, 0, &ip, &r) == SPT_OK && r && r->text[0] == 0, "empty audio");
+    spt_result_free(r);
+
+    /* the benchmark protocol (device-resident greedy, no timestamps) */
+    ip.flags = SPT_SUPPRESS_BLANK | SPT_NO_TIMESTAMPS | SPT_IGNORE_EOT;
+    ip.temperature_inc = 0.0f;
+    ip.max_new_tokens = 8;
+    r = NULL;
+    CHECK(spt_transcribe(ctx, pcm, n, &ip, &r) == SPT_OK && r->n_tokens == 8, "fast path");
+    spt_result_free(r);
+
+    /* bad arguments are errors, not crashes */
+    CHECK(spt_transcribe(ctx, NULL, 10, &ip, &r) == SPT_ERR_INVALID_ARG, "null pcm");
+    ip.language = "xx";
+    CHECK(spt_transcribe(ctx, pcm, n, &ip, &r) == SPT_ERR_INVALID_ARG, "unknown language");
+
+    spt_timings tm;
+    CHECK(spt_get_timings(ctx, &tm) == SPT_OK, "timings");
+    spt_ctx_destroy(ctx);
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    const char* spec = argc > 1 ? argv[1] : "synthetic:tiny";
+    printf("%s\n", spt_version());
+    spt_ctx* ctx = NULL;
+    char err[256];
+    CHECK(spt_ctx_create("/nonexistent/ggml-base.bin", NULL, &ctx, err, sizeof err) == SPT_ERR_LOAD && !ctx,
+          "missing model file");
+    if (argc > 2 && strcmp(argv[2], "--link-only") == 0) return 0;
+    const size_t n = 16000 * 6;
+    float* pcm = (float*)malloc(n * sizeof(float));
+    for (size_t i = 0; i < n; ++i)
+        pcm[i] = 0.3f * sinf(2.0f * 3.14159265f * 440.0f * (float)i / 16000.0f) +
+                 0.05f * sinf(2.0f * 3.14159265f * 1234.5f * (float)i / 16000.0f);
+    int rc = one_session(spec, pcm, n);
+    if (!rc) rc = one_session(spec, pcm, n); /* unload, then load again */
+    free(pcm);
+    if (!rc) printf("capi_smoke ok\n");
+    return rc;
+}
