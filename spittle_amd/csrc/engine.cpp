@@ -547,7 +547,7 @@ void Engine::alloc_workspace() {
         ao_ = A(B * T * d);
         ff_ = A(B * T * 4 * d);
         enc_out_ = A(B * T * d);
-        ckv_ = A(L * 2 * B * T * d);
+        ckv_ = A(L * kv_layer_elems((int)B, dm_.n_head, (int)T));
         suppress_ = (uint32_t*)c.take((V / 32 + 1) * 4);
         suppress_lang_ = (uint32_t*)c.take((V / 32 + 1) * 4);
         scratch_ = (double*)c.take(64);
@@ -671,7 +671,7 @@ void Engine::enqueue_decoder_pass(DecGroup& g, int B_total, int Tq, const Decode
 // the residual buffer holding the result (plus g.pend's pending slabs, n = fc2's split).
 float* Engine::enqueue_layers(DecGroup& g, int B_total, int Tq) {
     const int d = dm_.d, H = dm_.n_head, ctx = dm_.n_text_ctx, T = dm_.n_audio_ctx, B = g.B, R = B * Tq;
-    const int64_t self_layer = (int64_t)2 * B * H * ctx * 64, cross_layer = (int64_t)2 * B_total * H * T * 64;
+    const int64_t self_layer = (int64_t)2 * B * H * ctx * 64, cross_layer = kv_layer_elems(B_total, H, T);
     const int ks = dt_ == DT_BF16 ? 128 : 64;
     hipStream_t st = g.st;
     float* xc = g.dx;   // current residual rows (dec_embed / dec_finalize wrote this pass's input here)
@@ -696,8 +696,8 @@ float* Engine::enqueue_layers(DecGroup& g, int B_total, int Tq) {
     for (int l = 0; l < dm_.n_dec; ++l) {
         const DecL& e = dec_[l];
         void* skv_l = (char*)g.skv + self_layer * l * esz_;
-        // this group's sequences inside the [2][B_total][H][T][64] cross K/V of layer l
-        const void* ckv_l = (const char*)ckv_ + (cross_layer * l + (int64_t)g.b0 * H * T * 64) * esz_;
+        // this group's sequences inside the cross K/V of layer l (kv_offset layout, B_total sequences)
+        const void* ckv_l = (const char*)ckv_ + (cross_layer * l + (int64_t)g.b0 * H * 4096) * esz_;
         // LN1 + QKV projection + self K/V append
         GemvArgs a{};
         ln_input(a); a.lda = d; a.ln_w = e.ln1_w; a.ln_b = e.ln1_b; a.R = R;
@@ -1214,7 +1214,7 @@ double Engine::probe(int kind, int iters, double* work, int* is_flops) {
         case 0:  // cross-attention of layers 0..nl-1 (one launch each) over this group's cross K/V
             launch = [&] {
                 for (int l = 0; l < nl; ++l)
-                    dec_cross_attn(dt_, g.dq, (const char*)ckv_ + (int64_t)2 * B * H * T * 64 * l * esz_, Bg, B, H,
+                    dec_cross_attn(dt_, g.dq, (const char*)ckv_ + kv_layer_elems(B, H, T) * l * esz_, Bg, B, H,
                                    T, 1, g.dao, st_, xsplit_, g.xpart);
             };
             *work = 2.0 * Bg * H * T * 64 * esz_;

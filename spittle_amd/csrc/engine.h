@@ -214,7 +214,7 @@ private:
     void* y1p_ = nullptr;
     float* x_ = nullptr;
     void *xn_ = nullptr, *qkv_ = nullptr, *ao_ = nullptr, *ff_ = nullptr, *enc_out_ = nullptr;
-    void* ckv_ = nullptr;   // cross K/V [L][2][B][H][1500][64]
+    void* ckv_ = nullptr;   // cross K/V, per layer [47][B][H][2][32][64] (kernels.h kv_offset)
     uint32_t* suppress_ = nullptr;
     uint32_t* suppress_lang_ = nullptr;  // all but the language tokens (language detection)
     bool suppress_lang_ready_ = false;

@@ -25,7 +25,25 @@
 
 #include <algorithm>
 
+#ifndef SPT_STAMP
+#define SPT_STAMP 0
+#endif
+
 namespace spt {
+
+#if SPT_STAMP
+// developer timeline of the decode-step cross-attention (SPT_STAMP=1 builds): per workgroup
+// {entry, streaming done, exit} in s_memrealtime ticks
+__device__ unsigned long long* g_xattn_stamp;
+void set_xattn_stamp(void* p) { HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_xattn_stamp), &p, sizeof(p))); }
+#define XA_STAMP(i)                                                                          \
+    do {                                                                                     \
+        if (g_xattn_stamp && threadIdx.x == 0)                                               \
+            g_xattn_stamp[3 * blockIdx.x + (i)] = __builtin_amdgcn_s_memrealtime();          \
+    } while (0)
+#else
+#define XA_STAMP(i) do {} while (0)
+#endif
 
 namespace {
 
@@ -108,9 +126,6 @@ constexpr int ATTN_SRC(int s) { return 32 + s; }
 constexpr bool is_attn(int asrc) { return asrc >= 32; }
 constexpr int attn_s(int asrc) { return asrc - 32; }
 
-#ifndef SPT_STAMP
-#define SPT_STAMP 0
-#endif
 // developer timeline (SPT_STAMP=1 builds): thread 0's view of its workgroup's start / end
 #define GV_STAMP(i)                                                                                       \
     do {                                                                                                  \
@@ -582,12 +597,14 @@ struct AttnWave {
     float m[NQ], l[NQ], o[NQ][8];
     const T *Kb, *Vb;
     int n_keys, slot;
+    int64_t bstride = 0;  // 0: key rows contiguous ([T][64]); else 32-key blocks this far apart
 
-    __device__ __forceinline__ void init(const T* K, const T* V, int nk, int lane) {
+    __device__ __forceinline__ void init(const T* K, const T* V, int nk, int lane, int64_t blk_stride = 0) {
         slot = lane >> 3;
         Kb = K;
         Vb = V;
         n_keys = nk;
+        bstride = blk_stride;
 #pragma unroll
         for (int t = 0; t < NQ; ++t) {
             m[t] = -INFINITY;
@@ -600,8 +617,9 @@ struct AttnWave {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             const int key = min(blk * KB + 8 * i + slot, n_keys - 1);
-            kc[i].load(Kb + (size_t)key * 64);
-            vc[i].load(Vb + (size_t)key * 64);
+            const size_t off = bstride ? (size_t)(key >> 5) * bstride + (size_t)(key & 31) * 64 : (size_t)key * 64;
+            kc[i].load(Kb + off);
+            vc[i].load(Vb + off);
         }
     }
     __device__ __forceinline__ void process(const KVChunk<T> (&kc)[NI], const KVChunk<T> (&vc)[NI], int kbase,
@@ -752,13 +770,14 @@ __global__ __launch_bounds__(64 * NW) void cross_attn_kernel(const T* __restrict
                                                              int B_layout, int H, int T_enc, int Tq,
                                                              T* __restrict__ out, float* __restrict__ part) {
     typedef AttnWave<T, NQ, NIX, NW> W;
+    XA_STAMP(0);
     __shared__ float s_m[NW][NQ], s_l[NW][NQ];
     __shared__ float s_o[NW][NQ][64];
     const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane & 7;
-    const size_t kvo = ((size_t)b * H + h) * (size_t)T_enc * 64 + 8 * g;
-    W aw;
-    aw.init(kv + kvo, kv + (size_t)B_layout * H * T_enc * 64 + kvo, T_enc, lane);
+    W aw;  // kv_offset layout: 32-key blocks [T/32][B][H][2][32][64]
+    const size_t kvo = ((size_t)b * H + h) * 4096 + 8 * g;
+    aw.init(kv + kvo, kv + kvo + 2048, T_enc, lane, (int64_t)B_layout * H * 4096);
     float qv[NQ][8];
     int lim[NQ];
 #pragma unroll
@@ -774,8 +793,10 @@ __global__ __launch_bounds__(64 * NW) void cross_attn_kernel(const T* __restrict
     const int S = SPLIT ? (int)gridDim.y : 1, sp = SPLIT ? (int)blockIdx.y : 0;
     const int per = cdiv(nblk_all, S), blk0 = sp * per, nblk = min(nblk_all, blk0 + per);
     aw.run(blk0 + wid, nblk, false, qv, lim, Tq);
+    if (wid == 0) XA_STAMP(1);
     aw.to_lds(s_m, s_l, s_o, wid, lane);
     __syncthreads();
+    XA_STAMP(2);
     if (tid < 64 * Tq) {
         const int t = tid >> 6, e = tid & 63;
         float M, L, O;

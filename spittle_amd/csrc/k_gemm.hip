@@ -44,15 +44,17 @@ __device__ __forceinline__ void glds16(const void* g, SPT_LDS void* l) {
 
 // fused epilogue of one output element (row, column): bias, GELU, positional add, residual
 // add or the head-split store of the cross-attention K/V cache
-struct EpiCol { int col; float bv; int64_t kv_off; };
+struct EpiCol { int col; float bv; int l, kvi, h, el; };
 template <int EPI>
 __device__ __forceinline__ EpiCol epi_col(const GemmArgs& g, int col) {
-    EpiCol e{col, g.bias ? g.bias[col] : 0.0f, 0};
+    EpiCol e{col, g.bias ? g.bias[col] : 0.0f, 0, 0, 0, 0};
     if constexpr (EPI == EPI_KVSPLIT) {
         const int d = g.kv_H * 64;
-        const int l = col / (2 * d), rem = col - l * 2 * d;
-        const int kvi = rem / d, h = (rem - kvi * d) >> 6, el = rem & 63;
-        e.kv_off = ((((int64_t)(l * 2 + kvi) * g.kv_B) * g.kv_H + h) * g.kv_T) * 64 + el;  // + (bb*H*T + t)*64
+        e.l = col / (2 * d);
+        const int rem = col - e.l * 2 * d;
+        e.kvi = rem / d;
+        e.h = (rem - e.kvi * d) >> 6;
+        e.el = rem & 63;
     }
     return e;
 }
@@ -69,7 +71,7 @@ __device__ __forceinline__ void epi_store(const GemmArgs& g, int bz, int row, co
         ((float*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col] += v;
     } else if constexpr (EPI == EPI_KVSPLIT) {
         const int bb = row / g.kv_T, t = row - bb * g.kv_T;
-        ((T*)g.C)[e.kv_off + ((int64_t)bb * g.kv_H * g.kv_T + t) * 64] = from_f<T>(v);
+        ((T*)g.C)[kv_offset(e.l, e.kvi, bb, e.h, t, e.el, g.kv_B, g.kv_H, g.kv_T)] = from_f<T>(v);
     }
 }
 
@@ -394,8 +396,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
                 const int l = col / (2 * d), rem = col - l * 2 * d;
                 const int kvi = rem / d, hh = (rem - kvi * d) >> 6, el = rem & 63;
                 const int bb = row / g.kv_T, t = row - bb * g.kv_T;
-                const int64_t off = ((((int64_t)(l * 2 + kvi) * g.kv_B + bb) * g.kv_H + hh) * g.kv_T + t) * 64 + el;
-                *(uint4*)((bf16*)g.C + off) = v;
+                *(uint4*)((bf16*)g.C + kv_offset(l, kvi, bb, hh, t, el, g.kv_B, g.kv_H, g.kv_T)) = v;
             } else {
                 float* cp = (float*)g.C + (size_t)bz * g.sC + (size_t)row * g.ldc + col;
                 float4 o = *(const float4*)&v;

@@ -12,6 +12,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <functional>
 #include <string>
 #include <vector>
@@ -236,16 +237,45 @@ int main(int argc, char** argv) {
         const int B = ai(2, 8), T = ai(3, 1500), S = ai(4, 1), dt = ai(5, DT_BF16), NL = 8, d = 1280, H = 20;
         const int esz = dt == DT_BF16 ? 2 : 4;
         void* q = drand((size_t)B * d, dt, 1, 0);
-        const size_t layer = (size_t)2 * B * H * T * 64;
+        const size_t layer = (size_t)2 * B * H * ((T + 31) / 32 * 32) * 64;
         void* kv = drand(layer * NL, dt, 2, 0);
         void* out = dalloc((size_t)B * d * esz);
         float* part = (float*)dalloc((size_t)B * H * 32 * 66 * 4);
         HIP_CHECK(hipDeviceSynchronize());
         const double us = time_us(st, 10, [&] {
-            for (int l = 0; l < NL; ++l) {
-                dec_cross_attn(dt, q, (const char*)kv + layer * l * esz, B, B, H, T, 1, out, st, S, part);
-            }
+            // S = 9: the blocked [T/32][B][H][2][32][64] layout, one workgroup per (b, h)
+            for (int l = 0; l < NL; ++l) dec_cross_attn(dt, q, (const char*)kv + layer * l * esz, B, B, H, T, 1, out, st, S, part);
         }) / NL;
+#if SPT_STAMP
+        {   // workgroup timeline of one more (cache-cold) launch
+            unsigned long long* sp = (unsigned long long*)dalloc((size_t)B * H * 3 * 8);
+            void* flush = dalloc((size_t)512 << 20);
+            unsigned* sink = (unsigned*)dalloc(64);
+            cache_flush(flush, (int64_t)512 << 20, sink, st);
+            set_xattn_stamp(sp);
+            dec_cross_attn(dt, q, kv, B, B, H, T, 1, out, st, S, part);
+            HIP_CHECK(hipStreamSynchronize(st));
+            set_xattn_stamp(nullptr);
+            std::vector<unsigned long long> h((size_t)B * H * 3);
+            HIP_CHECK(hipMemcpy(h.data(), sp, h.size() * 8, hipMemcpyDeviceToHost));
+            unsigned long long t0 = ~0ull;
+            for (int i = 0; i < B * H; ++i) t0 = std::min(t0, h[3 * i]);
+            std::vector<double> st_, str_, end_;
+            for (int i = 0; i < B * H; ++i) {
+                st_.push_back((h[3 * i] - t0) * 0.01);
+                str_.push_back((h[3 * i + 1] - t0) * 0.01);
+                end_.push_back((h[3 * i + 2] - t0) * 0.01);
+            }
+            auto q5 = [](std::vector<double> v) {
+                std::sort(v.begin(), v.end());
+                char b[128];
+                snprintf(b, sizeof b, "min %.2f med %.2f max %.2f", v.front(), v[v.size() / 2], v.back());
+                return std::string(b);
+            };
+            printf("  timeline us from first start: start %s | wave0 streamed %s | merged %s\n", q5(st_).c_str(),
+                   q5(str_).c_str(), q5(end_).c_str());
+        }
+#endif
         printf("cross-attn B=%d T=%d splits=%d dt=%d (8 layers back to back) : %.2f us  %.0f GB/s\n", B, T, S, dt, us,
                2.0 * B * H * T * 64 * esz / us / 1e3);
         return 0;
