@@ -22,6 +22,7 @@ namespace spt {
 namespace {
 
 constexpr float kScaleLog2 = 0.125f * 1.4426950408889634f;  // (1/sqrt(64)) * log2(e)
+constexpr float kLazy = 8.0f;  // bf16 kernel: re-base the softmax only past a 2^8 growth
 
 __device__ __forceinline__ void glds16(const void* g, SPT_LDS void* l) {
     __builtin_amdgcn_global_load_lds((const void*)g, l, 16, 0, 0);
@@ -105,11 +106,23 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16* __restric
 #pragma unroll
         for (int r = 0; r < 16; ++r) mloc = max3f(mloc, s[0][r], s[1][r]);
         mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-        const float m_new = fmaxf(m_run, mloc);
-        // v_exp_f32 directly: exp2f's denormal-range fix-up (cmp / cndmask / ldexp per score)
-        // only matters for probabilities below 2^-126 of the running maximum
-        const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * kScaleLog2);
-        const float mc = m_new * kScaleLog2;
+        // Lazy rescaling: the reference maximum m_run moves only when some query's new scores
+        // exceed it by more than 2^kLazy (then every lane re-bases, alpha <= 1); otherwise the
+        // probabilities are taken against the stale maximum (p <= 2^kLazy: no overflow in f32
+        // or bf16) and the accumulator rescale -- 32 multiplies and an exp per tile, a third of
+        // the softmax's vector work -- is skipped.  l and o always share the same reference,
+        // so the result is the same softmax up to rounding.
+        float alpha = 1.0f;
+        if (__any((mloc - m_run) * kScaleLog2 > kLazy)) {
+            const float m_new = fmaxf(m_run, mloc);
+            // v_exp_f32 directly: exp2f's denormal-range fix-up (cmp / cndmask / ldexp per
+            // score) only matters for probabilities below 2^-126 of the running maximum
+            alpha = __builtin_amdgcn_exp2f((m_run - m_new) * kScaleLog2);
+            m_run = m_new;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
+        }
+        const float mc = m_run * kScaleLog2;
         // scores in pairs: packed f32 FMA / add (v_pk_fma_f32, v_pk_add_f32) and one
         // v_cvt_pk_bf16_f32 per pair straight into the P^T fragment dwords
         const f32x2 sc2 = {kScaleLog2, kScaleLog2}, mc2 = {-mc, -mc};
@@ -132,9 +145,6 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16* __restric
 #pragma unroll
             for (int sp = 0; sp < 2; ++sp) pf[kt2][sp] = pu[kt2][sp].v;
         l_run = l_run * alpha + lsum;
-        m_run = m_new;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
         // O^T += V^T . P^T
         const int g = lane >> 4, i16 = lane & 15;
 #pragma unroll
