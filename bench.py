@@ -232,6 +232,16 @@ def app_latency(eng, dur_s=(5, 10, 30)) -> dict:
         ms = (time.perf_counter() - t0) * 1e3
         out[f"{s}s"] = {"ms": round(ms, 2), "windows": r.n_windows, "fallbacks": r.n_fallbacks,
                         "tokens": len(r.tokens), "segments": len(r.segments)}
+    # beam search (whisper.cpp's WHISPER_SAMPLING_BEAM_SEARCH, beam_size 5; one captured graph per
+    # step, the candidate bookkeeping on the host), 10 s, no fallback
+    pb = WhisperInferenceParams(language="en", beam_size=5, temperature_inc=0.0)
+    x = synth_audio(2010)[:16000 * 10]
+    eng.transcribe_samples(x, pb)  # warm: the step graph is captured on first use
+    t0 = time.perf_counter()
+    r = eng.transcribe_samples(x, pb)
+    ms = (time.perf_counter() - t0) * 1e3
+    out["10s_beam5"] = {"ms": round(ms, 2), "windows": r.n_windows, "tokens": len(r.tokens),
+                        "ms_per_token": round(ms / max(1, len(r.tokens)), 3)}
     return out
 
 

@@ -1136,12 +1136,35 @@ void Engine::beam_next(const int* src, const int* tokens, const int* rowstate, i
     HIP_CHECK(hipMemcpyAsync(g.tok_in, h + B, B * 4, hipMemcpyHostToDevice, g.st));
     HIP_CHECK(hipMemcpyAsync(g.beam_row, h + 2 * B, (size_t)B * 16, hipMemcpyHostToDevice, g.st));
     HIP_CHECK(hipMemcpyAsync(g.beam_step, h + 6 * B, 4, hipMemcpyHostToDevice, g.st));
-    // reorder the self-K/V rows (positions < pos0) through the scratch, then feed the tokens
-    dec_kv_gather(dt_, g.skv, kvtmp_, g.beam_src, dm_.n_dec, B, dm_.n_head, dm_.n_text_ctx, g.ds, g.st);
-    dec_kv_gather(dt_, kvtmp_, g.skv, g.beam_ident, dm_.n_dec, B, dm_.n_head, dm_.n_text_ctx, g.ds, g.st);
-    dec_embed(dt_, g.tok_in, B, 1, dm_.d, tok_emb_, dec_pos_, g.ds, g.dx, g.st);
-    float* x = enqueue_layers(g, B, 1);
-    enqueue_head(g, 1, beam_rq_, beam_rq_.n_steps, x, suppress_, (beam_rq_.flags & 1u) != 0);
+    // one captured graph per (rows, candidates, flags, length): reorder the self-K/V rows
+    // (positions < pos0) through the scratch, feed the tokens, the decoder pass and the
+    // candidates kernel.  The uploads above stay outside: the graph reads them in place.
+    auto beam_pass = [&] {
+        dec_kv_gather(dt_, g.skv, kvtmp_, g.beam_src, dm_.n_dec, B, dm_.n_head, dm_.n_text_ctx, g.ds, g.st);
+        dec_kv_gather(dt_, kvtmp_, g.skv, g.beam_ident, dm_.n_dec, B, dm_.n_head, dm_.n_text_ctx, g.ds, g.st);
+        dec_embed(dt_, g.tok_in, B, 1, dm_.d, tok_emb_, dec_pos_, g.ds, g.dx, g.st);
+        float* x = enqueue_layers(g, B, 1);
+        enqueue_head(g, 1, beam_rq_, beam_rq_.n_steps, x, suppress_, (beam_rq_.flags & 1u) != 0);
+    };
+    static const bool no_graph = getenv("SPT_NO_GRAPH") != nullptr;
+    if (no_graph) {
+        beam_pass();
+    } else {
+        // n_forced = -beam_k marks a beam-step graph (a real n_forced is >= 0)
+        const GraphKey key{B, B, 0, beam_rq_.n_steps, -beam_rq_.beam_k, beam_rq_.flags, beam_rq_.full};
+        auto it = g.graphs.find(key);
+        if (it == g.graphs.end()) {
+            hipGraph_t graph;
+            HIP_CHECK(hipStreamBeginCapture(g.st, hipStreamCaptureModeThreadLocal));
+            beam_pass();
+            HIP_CHECK(hipStreamEndCapture(g.st, &graph));
+            hipGraphExec_t exec;
+            HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+            HIP_CHECK(hipGraphDestroy(graph));
+            it = g.graphs.emplace(key, exec).first;
+        }
+        HIP_CHECK(hipGraphLaunch(it->second, g.st));
+    }
     read_cands(B, out);
 }
 
