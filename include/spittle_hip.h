@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 5
+#define SPT_ABI_VERSION 6
 
 typedef enum {
     SPT_OK = 0,
@@ -45,7 +45,7 @@ typedef enum {
     SPT_ERR_INTERNAL = 6
 } spt_status;
 
-typedef enum { SPT_DTYPE_F32 = 0, SPT_DTYPE_BF16 = 1 } spt_dtype;
+typedef enum { SPT_DTYPE_F32 = 0, SPT_DTYPE_BF16 = 1, SPT_DTYPE_F16 = 2 /* Parakeet only */ } spt_dtype;
 
 /* decode flags (spt_infer_params.flags) */
 #define SPT_SUPPRESS_BLANK  1u  /* whisper_full_params.suppress_blank (default on) */
@@ -236,6 +236,110 @@ spt_status spt_debug_ggml_tokenize(const char* model_path, const char* text, int
                                    int32_t* n_out);
 /* host-only: the host reference dequantisation of n elements of one ggml type to f32 */
 spt_status spt_debug_ggml_dequant(int32_t ggml_type, const void* src, int64_t n, float* dst);
+
+/* ================================================================================================
+ * ABI 6: Parakeet-V3 (NeMo FastConformer-TDT), the app's other local engine.
+ *
+ * In the reference TranscriptionManager owns a transcribe_rs ParakeetEngine through
+ * LoadedEngine::Parakeet and calls (src-tauri/src/managers/transcription.rs):
+ *
+ *   ParakeetEngine::new() + load_model_with_params(&path, ParakeetModelParams::int8())
+ *                                                   :278-297  -> spt_parakeet_create (+ set_tensor)
+ *   transcribe_samples(audio, Some(ParakeetInferenceParams { timestamp_granularity: Segment, .. }))
+ *                                                   :505-513  -> spt_parakeet_transcribe
+ *   unload_model() / Drop                            :175-208  -> spt_parakeet_destroy
+ *
+ * and reads TranscriptionResult.text (:537-546).  The encoder runs in fp16 (SPT_DTYPE_F16, the
+ * BASELINE config) or f32; the prediction network and joint always in f32.  Weights come from a
+ * synthetic spec or tensor by tensor through spt_parakeet_set_tensor (the id table of
+ * oracle/po_model.c, NeMo layouts; spittle_amd.parakeet.load_nemo maps a .nemo checkpoint).
+ * ============================================================================================== */
+typedef struct spt_pk_ctx spt_pk_ctx;
+
+typedef struct {
+    int32_t dtype;        /* SPT_DTYPE_F16 (default) or SPT_DTYPE_F32 (bf16 also accepted) */
+    int32_t device;
+    int32_t max_batch;    /* utterances (chunks) per device pass, <= 64 */
+    float max_seconds;    /* longest chunk one pass takes; longer utterances are cut into chunks of
+                             this length (a multiple of 80 ms) and their results concatenated */
+    uint64_t seed;        /* synthetic weights */
+    uint32_t flags;       /* SPT_PK_WEIGHTS_EMPTY: zero weights, to be filled by set_tensor */
+    int32_t reserved0;
+} spt_pk_model_params;
+
+#define SPT_PK_WEIGHTS_EMPTY 1u
+
+typedef enum { SPT_PK_TS_TOKEN = 0, SPT_PK_TS_WORD = 1, SPT_PK_TS_SEGMENT = 2 } spt_pk_granularity;
+
+typedef struct {
+    int32_t max_symbols;            /* TDT greedy: tokens per encoder frame (NeMo default 10; <= 16) */
+    int32_t timestamp_granularity;  /* an spt_pk_granularity; the app asks for SPT_PK_TS_SEGMENT */
+} spt_pk_infer_params;
+
+typedef struct {
+    double start, end;     /* seconds */
+    char* text;
+    int32_t i0, n_tokens;  /* the unit's tokens in spt_pk_result.tokens */
+} spt_pk_segment;
+
+typedef struct {
+    char* text;            /* the pieces joined ("▁" -> space) and trimmed; "[id]" without a vocabulary */
+    int32_t* tokens;
+    int32_t* frames;       /* encoder frame (80 ms) of each token, utterance-relative */
+    float* logit;          /* the token's joint logit */
+    float* runner_up;      /* the best other token's (blank included) */
+    int32_t n_tokens;
+    int32_t n_segments;
+    spt_pk_segment* segments;  /* timestamp units of the requested granularity */
+    int32_t n_chunks;
+    int32_t reserved0;
+} spt_pk_result;
+
+typedef struct {
+    int32_t n_mels, d, n_layers, n_heads, ff, sub_ch, conv_k, pred, n_vocab, n_dur;
+    int32_t dtype, max_batch, max_samples, reserved0;
+    int64_t weight_bytes, workspace_bytes;
+} spt_pk_model_info;
+
+typedef struct {
+    double mel_ms, encoder_ms, decode_ms, total_ms, h2d_ms;
+    int32_t n_steps;       /* TDT joint evaluations (graph-replayed decode steps) */
+    int32_t batch;
+    int32_t enc_frames;    /* padded encoder frames of the pass */
+    int32_t reserved0;
+} spt_pk_timings;
+
+void spt_parakeet_default_model_params(spt_pk_model_params* p);
+void spt_parakeet_default_infer_params(spt_pk_infer_params* p);
+/* spec: "synthetic:parakeet-tdt-0.6b-v3[:layers=N][:seed=S]" or "synthetic:parakeet-test-small[...]" */
+spt_status spt_parakeet_create(const char* model_spec, const spt_pk_model_params* params, spt_pk_ctx** out,
+                               char* err, size_t errlen);
+void spt_parakeet_destroy(spt_pk_ctx* ctx);
+const char* spt_parakeet_last_error(const spt_pk_ctx* ctx);
+spt_status spt_parakeet_info(const spt_pk_ctx* ctx, spt_pk_model_info* info);
+/* element count of tensor id (SPT_ERR_INVALID_ARG if unknown) and its upload (f32, NeMo layout) */
+spt_status spt_parakeet_tensor_numel(const spt_pk_ctx* ctx, int32_t tensor_id, int64_t* n);
+spt_status spt_parakeet_set_tensor(spt_pk_ctx* ctx, int32_t tensor_id, const float* data, int64_t n);
+/* SentencePiece pieces by id (UTF-8, "▁" marks a word start); copied */
+spt_status spt_parakeet_set_vocab(spt_pk_ctx* ctx, const char* const* pieces, int32_t n);
+spt_status spt_parakeet_transcribe(spt_pk_ctx* ctx, const float* pcm16k, size_t n_samples,
+                                   const spt_pk_infer_params* params, spt_pk_result** out);
+spt_status spt_parakeet_transcribe_batch(spt_pk_ctx* ctx, const float* const* pcm, const size_t* n_samples,
+                                         size_t batch, const spt_pk_infer_params* params, spt_pk_result** out);
+/* batch <= max_batch chunks already in device memory (pcm_dev[b * stride + i], n <= max samples) */
+spt_status spt_parakeet_transcribe_batch_device(spt_pk_ctx* ctx, const float* pcm_dev, size_t stride,
+                                                const size_t* n_samples, size_t batch,
+                                                const spt_pk_infer_params* params, spt_pk_result** out);
+void spt_parakeet_result_free(spt_pk_result* r);
+spt_status spt_parakeet_get_timings(const spt_pk_ctx* ctx, spt_pk_timings* t);
+/* test hooks: normalised log-mel [n_mels][n / 160 + 1]; encoder output [T3][d] of a mel
+ * [n_mels][T]; sum|w| and sum w of a tensor as stored (transposed tensors: SPT_ERR_UNSUPPORTED) */
+spt_status spt_parakeet_debug_mel(spt_pk_ctx* ctx, const float* pcm16k, size_t n_samples, float* out);
+spt_status spt_parakeet_debug_encode(spt_pk_ctx* ctx, const float* mel, int32_t T, float* out);
+/* TDT greedy decoding of a given encoder output [T3][d] (f32): the decoder alone */
+spt_status spt_parakeet_debug_decode(spt_pk_ctx* ctx, const float* enc, int32_t T3, int32_t max_symbols,
+                                     spt_pk_result** out);
+spt_status spt_parakeet_debug_weight_checksum(spt_pk_ctx* ctx, int32_t tensor_id, double* out2);
 
 #ifdef __cplusplus
 }

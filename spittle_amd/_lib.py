@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(HERE, "libspittle_hip.so")
 # status codes
 SPT_OK, SPT_ERR_INVALID_ARG, SPT_ERR_LOAD, SPT_ERR_DEVICE, SPT_ERR_OOM, SPT_ERR_UNSUPPORTED, SPT_ERR_INTERNAL = range(7)
 STATUS_NAMES = {0: "OK", 1: "INVALID_ARG", 2: "LOAD", 3: "DEVICE", 4: "OOM", 5: "UNSUPPORTED", 6: "INTERNAL"}
-SPT_DTYPE_F32, SPT_DTYPE_BF16 = 0, 1
+SPT_DTYPE_F32, SPT_DTYPE_BF16, SPT_DTYPE_F16 = 0, 1, 2
 SPT_SUPPRESS_BLANK, SPT_NO_TIMESTAMPS, SPT_IGNORE_EOT, SPT_SUPPRESS_NST = 1, 2, 4, 8
 
 # every symbol include/spittle_hip.h declares
@@ -26,7 +26,16 @@ EXPORTS = [
     "spt_tokenize", "spt_token_to_str", "spt_debug_ggml_tokenize", "spt_debug_ggml_dequant",
     "spt_weights_export", "spt_weights_import", "spt_weights_arena", "spt_weights_commit",
     "spt_ctx_create_replicas", "spt_transcribe_batch_replicas",
+    # ABI 6: Parakeet-V3
+    "spt_parakeet_default_model_params", "spt_parakeet_default_infer_params", "spt_parakeet_create",
+    "spt_parakeet_destroy", "spt_parakeet_last_error", "spt_parakeet_info", "spt_parakeet_tensor_numel",
+    "spt_parakeet_set_tensor", "spt_parakeet_set_vocab", "spt_parakeet_transcribe", "spt_parakeet_transcribe_batch",
+    "spt_parakeet_transcribe_batch_device", "spt_parakeet_result_free", "spt_parakeet_get_timings",
+    "spt_parakeet_debug_mel", "spt_parakeet_debug_encode", "spt_parakeet_debug_decode",
+    "spt_parakeet_debug_weight_checksum",
 ]
+SPT_PK_WEIGHTS_EMPTY = 1
+SPT_PK_TS_TOKEN, SPT_PK_TS_WORD, SPT_PK_TS_SEGMENT = 0, 1, 2
 SPT_MODEL_WEIGHTS_EXTERNAL = 1
 PROBES = {"dec_cross_attn": 0, "dec_self_attn": 1, "dec_logits": 2, "dec_fc1": 3, "enc_fc1_gemm": 4,
           "enc_attn": 5}
@@ -68,6 +77,38 @@ class ModelInfo(C.Structure):
 class Timings(C.Structure):
     _fields_ = [(n, C.c_double) for n in ("mel_ms", "encoder_ms", "cross_kv_ms", "decode_ms", "total_ms",
                                            "h2d_ms")] + [("n_decode_passes", C.c_int32), ("batch", C.c_int32)]
+
+
+class PkModelParams(C.Structure):
+    _fields_ = [("dtype", C.c_int32), ("device", C.c_int32), ("max_batch", C.c_int32), ("max_seconds", C.c_float),
+                ("seed", C.c_uint64), ("flags", C.c_uint32), ("reserved0", C.c_int32)]
+
+
+class PkInferParams(C.Structure):
+    _fields_ = [("max_symbols", C.c_int32), ("timestamp_granularity", C.c_int32)]
+
+
+class PkSegment(C.Structure):
+    _fields_ = [("start", C.c_double), ("end", C.c_double), ("text", C.c_char_p), ("i0", C.c_int32),
+                ("n_tokens", C.c_int32)]
+
+
+class PkResult(C.Structure):
+    _fields_ = [("text", C.c_char_p), ("tokens", C.POINTER(C.c_int32)), ("frames", C.POINTER(C.c_int32)),
+                ("logit", C.POINTER(C.c_float)), ("runner_up", C.POINTER(C.c_float)), ("n_tokens", C.c_int32),
+                ("n_segments", C.c_int32), ("segments", C.POINTER(PkSegment)), ("n_chunks", C.c_int32),
+                ("reserved0", C.c_int32)]
+
+
+class PkModelInfo(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("n_mels", "d", "n_layers", "n_heads", "ff", "sub_ch", "conv_k", "pred",
+                                          "n_vocab", "n_dur", "dtype", "max_batch", "max_samples", "reserved0")] + \
+               [("weight_bytes", C.c_int64), ("workspace_bytes", C.c_int64)]
+
+
+class PkTimings(C.Structure):
+    _fields_ = [(n, C.c_double) for n in ("mel_ms", "encoder_ms", "decode_ms", "total_ms", "h2d_ms")] + \
+               [(n, C.c_int32) for n in ("n_steps", "batch", "enc_frames", "reserved0")]
 
 
 _lib = None
@@ -122,6 +163,34 @@ def load():
                                           C.POINTER(vp), C.POINTER(C.c_double), C.c_char_p, C.c_size_t]
     L.spt_transcribe_batch_replicas.argtypes = [C.POINTER(vp), C.c_int32, C.POINTER(fp), C.POINTER(C.c_size_t),
                                                 C.c_size_t, C.POINTER(InferParams), C.POINTER(C.POINTER(Result))]
+    # ABI 6: Parakeet-V3
+    PR = C.POINTER(C.POINTER(PkResult))
+    L.spt_parakeet_default_model_params.argtypes = [C.POINTER(PkModelParams)]
+    L.spt_parakeet_default_infer_params.argtypes = [C.POINTER(PkInferParams)]
+    L.spt_parakeet_create.argtypes = [C.c_char_p, C.POINTER(PkModelParams), C.POINTER(vp), C.c_char_p, C.c_size_t]
+    L.spt_parakeet_destroy.argtypes = [vp]
+    L.spt_parakeet_last_error.argtypes = [vp]
+    L.spt_parakeet_last_error.restype = C.c_char_p
+    L.spt_parakeet_info.argtypes = [vp, C.POINTER(PkModelInfo)]
+    L.spt_parakeet_tensor_numel.argtypes = [vp, C.c_int32, C.POINTER(C.c_int64)]
+    L.spt_parakeet_set_tensor.argtypes = [vp, C.c_int32, fp, C.c_int64]
+    L.spt_parakeet_set_vocab.argtypes = [vp, C.POINTER(C.c_char_p), C.c_int32]
+    L.spt_parakeet_transcribe.argtypes = [vp, fp, C.c_size_t, C.POINTER(PkInferParams), PR]
+    L.spt_parakeet_transcribe_batch.argtypes = [vp, C.POINTER(fp), C.POINTER(C.c_size_t), C.c_size_t,
+                                                C.POINTER(PkInferParams), PR]
+    L.spt_parakeet_transcribe_batch_device.argtypes = [vp, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t), C.c_size_t,
+                                                       C.POINTER(PkInferParams), PR]
+    L.spt_parakeet_result_free.argtypes = [C.POINTER(PkResult)]
+    L.spt_parakeet_get_timings.argtypes = [vp, C.POINTER(PkTimings)]
+    L.spt_parakeet_debug_mel.argtypes = [vp, fp, C.c_size_t, fp]
+    L.spt_parakeet_debug_encode.argtypes = [vp, fp, C.c_int32, fp]
+    L.spt_parakeet_debug_decode.argtypes = [vp, fp, C.c_int32, C.c_int32, PR]
+    L.spt_parakeet_debug_weight_checksum.argtypes = [vp, C.c_int32, C.POINTER(C.c_double)]
+    for fn in EXPORTS:
+        if fn.startswith("spt_parakeet_") and fn not in ("spt_parakeet_default_model_params",
+                                                          "spt_parakeet_default_infer_params", "spt_parakeet_destroy",
+                                                          "spt_parakeet_last_error", "spt_parakeet_result_free"):
+            getattr(L, fn).restype = C.c_int
     for fn in ("spt_weights_arena", "spt_weights_commit", "spt_ctx_create_replicas", "spt_transcribe_batch_replicas",
                "spt_weights_export", "spt_weights_import", "spt_ctx_info", "spt_transcribe", "spt_transcribe_batch", "spt_transcribe_batch_device",
                "spt_get_timings", "spt_debug_mel", "spt_debug_encode", "spt_debug_weight_checksum",

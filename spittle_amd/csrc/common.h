@@ -8,6 +8,8 @@
 namespace spt {
 
 typedef uint16_t bf16;  // raw bf16 storage
+typedef _Float16 f16;   // IEEE half (Parakeet's fp16 encoder)
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 typedef __attribute__((ext_vector_type(8))) short bf16x8;
 typedef __attribute__((ext_vector_type(4))) short bf16x4v;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
@@ -57,13 +59,16 @@ __device__ inline uint32_t pack_bf2(float a, float b) {
 template <typename T> struct TypeTag;
 template <> struct TypeTag<float> { static constexpr int id = 0; };
 template <> struct TypeTag<bf16> { static constexpr int id = 1; };
+template <> struct TypeTag<f16> { static constexpr int id = 2; };
 
 template <typename T> __device__ inline float to_f(T v);
 template <> __device__ inline float to_f<float>(float v) { return v; }
 template <> __device__ inline float to_f<bf16>(bf16 v) { return bf2f(v); }
+template <> __device__ inline float to_f<f16>(f16 v) { return (float)v; }
 template <typename T> __device__ inline T from_f(float v);
 template <> __device__ inline float from_f<float>(float v) { return v; }
 template <> __device__ inline bf16 from_f<bf16>(float v) { return f2bf(v); }
+template <> __device__ inline f16 from_f<f16>(float v) { return (f16)v; }  // RNE
 
 // GELU, tanh form (ggml / whisper.cpp): 0.5 x (1 + tanh(u)), u = sqrt(2/pi) (x + 0.044715 x^3),
 // evaluated as x * sigmoid(2u) = x / (1 + 2^(-2u log2 e)): one v_exp_f32 + one v_rcp_f32
@@ -72,6 +77,14 @@ __device__ inline float gelu_tanh(float x) {
     const float c2 = -2.0f * 0.7978845608028654f * 1.4426950408889634f;
     const float e = __builtin_amdgcn_exp2f(c2 * (x + 0.044715f * x * x * x));
     return x * __builtin_amdgcn_rcpf(1.0f + e);
+}
+
+// Swish / SiLU x * sigmoid(x) (NeMo's Swish activation): one v_exp_f32 + one v_rcp_f32
+__device__ inline float swish(float x) {
+    return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
+}
+__device__ inline float sigmoidf_(float x) {
+    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
 }
 
 __device__ inline float wave_sum(float v) {

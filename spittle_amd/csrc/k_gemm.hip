@@ -63,12 +63,18 @@ __device__ __forceinline__ void epi_store(const GemmArgs& g, int bz, int row, co
     const float v = acc + e.bv;
     if constexpr (EPI == EPI_BIAS) {
         ((T*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col] = from_f<T>(v);
+    } else if constexpr (EPI == EPI_BIAS_SWISH) {
+        ((T*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col] = from_f<T>(swish(v));
+    } else if constexpr (EPI == EPI_BIAS_RELU) {
+        ((T*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col] = from_f<T>(fmaxf(v, 0.0f));
+    } else if constexpr (EPI == EPI_BIAS_F32) {
+        ((float*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col] = g.alpha * v;
     } else if constexpr (EPI == EPI_BIAS_GELU) {
         ((T*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col] = from_f<T>(gelu_tanh(v));
     } else if constexpr (EPI == EPI_BIAS_GELU_POS) {
         ((float*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col] = gelu_tanh(v) + g.pos[(size_t)row * g.N + e.col];
     } else if constexpr (EPI == EPI_BIAS_RESID) {
-        ((float*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col] += v;
+        ((float*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col] += g.alpha * v;
     } else if constexpr (EPI == EPI_KVSPLIT) {
         const int bb = row / g.kv_T, t = row - bb * g.kv_T;
         ((T*)g.C)[kv_offset(e.l, e.kvi, bb, e.h, t, e.el, g.kv_B, g.kv_H, g.kv_T)] = from_f<T>(v);
@@ -146,8 +152,13 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], wf[j], acc[i][j], 0, 0, 0);
+                    for (int j = 0; j < 4; ++j) {
+                        if constexpr (TypeTag<T>::id == 2)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, af[i]),
+                                                                               __builtin_bit_cast(f16x8, wf[j]), acc[i][j], 0, 0, 0);
+                        else
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], wf[j], acc[i][j], 0, 0, 0);
+                    }
             }
         } else {
             f32x4 af[4][2], wf[4][2];
@@ -215,7 +226,7 @@ constexpr int G2_BUF = 2 * 256 * G2_ROW;               // one buffer: A + W
 constexpr int G2_LDS = 2 * G2_BUF;                     // 128 KiB
 constexpr int G2_LDS_ALL = 8 * 128 * (128 + 16) > G2_LDS ? 8 * 128 * (128 + 16) : G2_LDS;  // + epilogue staging
 
-template <int EPI>
+template <int EPI, bool F16>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -303,8 +314,13 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
-                    acc[rh * 4 + i][ch * 2 + j] =
-                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bw[ch][j][s], acc[rh * 4 + i][ch * 2 + j], 0, 0, 0);
+                    if constexpr (F16)
+                        acc[rh * 4 + i][ch * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                            __builtin_bit_cast(f16x8, af[i][s]), __builtin_bit_cast(f16x8, bw[ch][j][s]),
+                            acc[rh * 4 + i][ch * 2 + j], 0, 0, 0);
+                    else
+                        acc[rh * 4 + i][ch * 2 + j] =
+                            __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bw[ch][j][s], acc[rh * 4 + i][ch * 2 + j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
     };
 #define G2_BARRIER() asm volatile("s_barrier" ::: "memory")
@@ -353,7 +369,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     // would be 2- or 4-byte stores at a row stride).  bf16 outputs: one pass of 128 rows,
     // row stride 144 B; f32 outputs: two passes of 64 rows, row stride 272 B (the 16-byte pad
     // spreads the four row groups a store instruction writes over distinct banks).
-    constexpr bool F32OUT = EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU_POS;
+    constexpr bool F32OUT = EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU_POS || EPI == EPI_BIAS_F32;
     constexpr int ESZ = F32OUT ? 4 : 2;
     constexpr int RS = 64 * ESZ + 16;          // LDS row stride (bytes)
     constexpr int PR = F32OUT ? 64 : 128;      // rows per pass
@@ -375,7 +391,11 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
                     const int rl = 16 * ii + 4 * fq + r, cl = 16 * j + fr;
                     float v = acc[i][j][r] + bv[j];
                     if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_POS) v = gelu_tanh(v);
+                    if constexpr (EPI == EPI_BIAS_SWISH) v = swish(v);
+                    if constexpr (EPI == EPI_BIAS_RELU) v = fmaxf(v, 0.0f);
+                    if constexpr (EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_F32) v *= g.alpha;
                     if constexpr (F32OUT) *(float*)(wreg + rl * RS + cl * 4) = v;
+                    else if constexpr (F16) *(f16*)(wreg + rl * RS + cl * 2) = (f16)v;
                     else *(bf16*)(wreg + rl * RS + cl * 2) = f2bf(v);
                 }
         }
@@ -389,7 +409,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
             const uint4 v = *(const uint4*)(wreg + rl * RS + ch * 16);
             if (row >= g.M) continue;
             const int col = n0 + wc * 64 + ch * (16 / ESZ);
-            if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+            if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_SWISH || EPI == EPI_BIAS_RELU) {
                 *(uint4*)((bf16*)g.C + (size_t)bz * g.sC + (size_t)row * g.ldc + col) = v;
             } else if constexpr (EPI == EPI_KVSPLIT) {
                 const int d = g.kv_H * 64;
@@ -402,6 +422,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
                 float4 o = *(const float4*)&v;
                 float4 y;
                 if constexpr (EPI == EPI_BIAS_RESID) y = *(const float4*)cp;
+                else if constexpr (EPI == EPI_BIAS_F32) y = make_float4(0.f, 0.f, 0.f, 0.f);
                 else y = *(const float4*)(g.pos + (size_t)row * g.N + col);
                 o.x += y.x; o.y += y.y; o.z += y.z; o.w += y.w;
                 *(float4*)cp = o;
@@ -411,15 +432,16 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     }
 }
 
-template <int EPI>
+template <int EPI, bool F16>
 void launch_256(const GemmArgs& g, int batch, hipStream_t st) {
     static bool attr = false;  // > 64 KiB dynamic LDS: set once per kernel
     if (!attr) {
-        HIP_CHECK(hipFuncSetAttribute((const void*)gemm256_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS_ALL));
+        HIP_CHECK(hipFuncSetAttribute((const void*)gemm256_kernel<EPI, F16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      G2_LDS_ALL));
         attr = true;
     }
     dim3 grid(cdiv(g.M, G2_BM) * (g.N / G2_BN), 1, batch);
-    hipLaunchKernelGGL((gemm256_kernel<EPI>), grid, dim3(512), G2_LDS_ALL, st, g);
+    hipLaunchKernelGGL((gemm256_kernel<EPI, F16>), grid, dim3(512), G2_LDS_ALL, st, g);
     SPT_LAUNCH_CHECK();
 }
 
@@ -434,41 +456,44 @@ void launch_t(const GemmArgs& g, int batch, hipStream_t st) {
 void gemm_nt(int dtype, int epi, const GemmArgs& g, int batch, hipStream_t st) { gemm_nt_variant(dtype, epi, g, batch, 0, st); }
 
 void gemm_nt_variant(int dtype, int epi, const GemmArgs& g, int batch, int variant, hipStream_t st) {
-    if (g.N % BN != 0 || (g.K * (dtype == DT_BF16 ? 2 : 4)) % SLAB != 0 || g.M <= 0)
+    const int esz = dtype == DT_F32 ? 4 : 2;
+    if (g.N % BN != 0 || (g.K * esz) % SLAB != 0 || g.M <= 0)
         throw std::runtime_error("gemm_nt: unsupported shape M=" + std::to_string(g.M) + " N=" +
                                  std::to_string(g.N) + " K=" + std::to_string(g.K));
-#define SPT_GEMM_CASE(T, E) \
-    case E: launch_t<T, E>(g, batch, st); return;
+#define SPT_GEMM_CASES(T)                                                          \
+    switch (epi) {                                                                 \
+        case EPI_BIAS: launch_t<T, EPI_BIAS>(g, batch, st); return;                \
+        case EPI_BIAS_GELU: launch_t<T, EPI_BIAS_GELU>(g, batch, st); return;      \
+        case EPI_BIAS_GELU_POS: launch_t<T, EPI_BIAS_GELU_POS>(g, batch, st); return; \
+        case EPI_BIAS_RESID: launch_t<T, EPI_BIAS_RESID>(g, batch, st); return;    \
+        case EPI_KVSPLIT: launch_t<T, EPI_KVSPLIT>(g, batch, st); return;          \
+        case EPI_BIAS_SWISH: launch_t<T, EPI_BIAS_SWISH>(g, batch, st); return;    \
+        case EPI_BIAS_RELU: launch_t<T, EPI_BIAS_RELU>(g, batch, st); return;      \
+        case EPI_BIAS_F32: launch_t<T, EPI_BIAS_F32>(g, batch, st); return;        \
+    }
+#define SPT_GEMM256_CASES(F)                                                       \
+    switch (epi) {                                                                 \
+        case EPI_BIAS: launch_256<EPI_BIAS, F>(g, batch, st); return;              \
+        case EPI_BIAS_GELU: launch_256<EPI_BIAS_GELU, F>(g, batch, st); return;    \
+        case EPI_BIAS_GELU_POS: launch_256<EPI_BIAS_GELU_POS, F>(g, batch, st); return; \
+        case EPI_BIAS_RESID: launch_256<EPI_BIAS_RESID, F>(g, batch, st); return;  \
+        case EPI_KVSPLIT: launch_256<EPI_KVSPLIT, F>(g, batch, st); return;        \
+        case EPI_BIAS_SWISH: launch_256<EPI_BIAS_SWISH, F>(g, batch, st); return;  \
+        case EPI_BIAS_RELU: launch_256<EPI_BIAS_RELU, F>(g, batch, st); return;    \
+        case EPI_BIAS_F32: launch_256<EPI_BIAS_F32, F>(g, batch, st); return;      \
+    }
     static const bool force128 = getenv("SPT_GEMM128") != nullptr;  // A/B switch for measurements
     const bool use256 = variant == 2 || (variant == 0 && !force128);
     const bool fits32 = (int64_t)g.M * g.lda < (1ll << 31) && (int64_t)g.N * g.ldw < (1ll << 31);
-    if (dtype == DT_BF16 && use256 && fits32 && g.N % G2_BN == 0 && g.K % 64 == 0) {
-        switch (epi) {
-            case EPI_BIAS: launch_256<EPI_BIAS>(g, batch, st); return;
-            case EPI_BIAS_GELU: launch_256<EPI_BIAS_GELU>(g, batch, st); return;
-            case EPI_BIAS_GELU_POS: launch_256<EPI_BIAS_GELU_POS>(g, batch, st); return;
-            case EPI_BIAS_RESID: launch_256<EPI_BIAS_RESID>(g, batch, st); return;
-            case EPI_KVSPLIT: launch_256<EPI_KVSPLIT>(g, batch, st); return;
-        }
+    if (dtype != DT_F32 && use256 && fits32 && g.N % G2_BN == 0 && g.K % 64 == 0) {
+        if (dtype == DT_F16) { SPT_GEMM256_CASES(true) }
+        else { SPT_GEMM256_CASES(false) }
     }
-    if (dtype == DT_BF16) {
-        switch (epi) {
-            SPT_GEMM_CASE(bf16, EPI_BIAS)
-            SPT_GEMM_CASE(bf16, EPI_BIAS_GELU)
-            SPT_GEMM_CASE(bf16, EPI_BIAS_GELU_POS)
-            SPT_GEMM_CASE(bf16, EPI_BIAS_RESID)
-            SPT_GEMM_CASE(bf16, EPI_KVSPLIT)
-        }
-    } else {
-        switch (epi) {
-            SPT_GEMM_CASE(float, EPI_BIAS)
-            SPT_GEMM_CASE(float, EPI_BIAS_GELU)
-            SPT_GEMM_CASE(float, EPI_BIAS_GELU_POS)
-            SPT_GEMM_CASE(float, EPI_BIAS_RESID)
-            SPT_GEMM_CASE(float, EPI_KVSPLIT)
-        }
-    }
-#undef SPT_GEMM_CASE
+    if (dtype == DT_BF16) { SPT_GEMM_CASES(bf16) }
+    else if (dtype == DT_F16) { SPT_GEMM_CASES(f16) }
+    else { SPT_GEMM_CASES(float) }
+#undef SPT_GEMM_CASES
+#undef SPT_GEMM256_CASES
     throw std::runtime_error("gemm_nt: bad epilogue");
 }
 

@@ -93,6 +93,8 @@ void gen_weights(int store_dtype, void* dst, int64_t n, uint64_t seed, uint32_t 
     const float scale = ldexpf(1.0f, scale_exp);
     if (store_dtype == DT_BF16)
         hipLaunchKernelGGL(gen_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, st, (bf16*)dst, n, seed, tid, kind, scale);
+    else if (store_dtype == DT_F16)
+        hipLaunchKernelGGL(gen_kernel<f16>, dim3(grid_for(n)), dim3(256), 0, st, (f16*)dst, n, seed, tid, kind, scale);
     else
         hipLaunchKernelGGL(gen_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, (float*)dst, n, seed, tid, kind, scale);
 }
@@ -184,6 +186,8 @@ void tensor_checksum(int dtype, const void* src, int64_t n, double* out2, hipStr
     if (g > 1024) g = 1024;
     if (dtype == DT_BF16)
         hipLaunchKernelGGL(checksum_kernel<bf16>, dim3(g), dim3(256), 0, st, (const bf16*)src, n, out2);
+    else if (dtype == DT_F16)
+        hipLaunchKernelGGL(checksum_kernel<f16>, dim3(g), dim3(256), 0, st, (const f16*)src, n, out2);
     else
         hipLaunchKernelGGL(checksum_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)src, n, out2);
 }

@@ -64,6 +64,11 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ x, in
     }
 }
 
+template <> __device__ __forceinline__ void store4<f16>(f16* p, float a, float b, float c, float d) {
+    typedef __attribute__((ext_vector_type(4))) _Float16 h4;
+    *(h4*)p = h4{(f16)a, (f16)b, (f16)c, (f16)d};
+}
+
 template <typename T>
 void ln_dispatch(const float* x, int M, int d, const float* w, const float* b, T* y, hipStream_t st) {
     dim3 grid(cdiv(M, 4));
@@ -90,6 +95,7 @@ __global__ void to_f32_kernel(const T* __restrict__ s, float* __restrict__ d, in
 void layernorm(int dtype, const float* x, int M, int d, const float* w, const float* b, void* y, hipStream_t st) {
     if (d % 4) throw std::runtime_error("layernorm: d % 4");
     if (dtype == DT_BF16) ln_dispatch<bf16>(x, M, d, w, b, (bf16*)y, st);
+    else if (dtype == DT_F16) ln_dispatch<f16>(x, M, d, w, b, (f16*)y, st);
     else ln_dispatch<float>(x, M, d, w, b, (float*)y, st);
 }
 
@@ -99,6 +105,8 @@ void to_f32(int dtype, const void* src, float* dst, int64_t n, hipStream_t st) {
     if (g < 1) g = 1;
     if (dtype == DT_BF16)
         hipLaunchKernelGGL(to_f32_kernel<bf16>, dim3((int)g), dim3(256), 0, st, (const bf16*)src, dst, n);
+    else if (dtype == DT_F16)
+        hipLaunchKernelGGL(to_f32_kernel<f16>, dim3((int)g), dim3(256), 0, st, (const f16*)src, dst, n);
     else
         hipLaunchKernelGGL(to_f32_kernel<float>, dim3((int)g), dim3(256), 0, st, (const float*)src, dst, n);
 }

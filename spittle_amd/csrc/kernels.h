@@ -5,7 +5,7 @@
 
 namespace spt {
 
-enum { DT_F32 = 0, DT_BF16 = 1 };
+enum { DT_F32 = 0, DT_BF16 = 1, DT_F16 = 2 };  // DT_F16: the Parakeet encoder only
 
 // ------------------------------------------------------------------ GEMM (k_gemm.hip)
 // Cross-attention K/V cache layout: per decoder layer [ceil(T/32)][B][H][2][32][64] -- 32-key
@@ -18,7 +18,10 @@ __host__ __device__ inline int64_t kv_offset(int l, int kvi, int b, int h, int t
            (t & 31) * 64 + e;
 }
 
-enum { EPI_BIAS = 0, EPI_BIAS_GELU = 1, EPI_BIAS_GELU_POS = 2, EPI_BIAS_RESID = 3, EPI_KVSPLIT = 4 };
+// EPI_BIAS_RESID: f32 C += alpha * (acc + bias); EPI_BIAS_F32: f32 C = alpha * (acc + bias);
+// SWISH / RELU: activation of acc + bias in the storage dtype
+enum { EPI_BIAS = 0, EPI_BIAS_GELU = 1, EPI_BIAS_GELU_POS = 2, EPI_BIAS_RESID = 3, EPI_KVSPLIT = 4,
+       EPI_BIAS_SWISH = 5, EPI_BIAS_RELU = 6, EPI_BIAS_F32 = 7 };
 
 struct GemmArgs {
     const void* A; int lda; int64_t sA;   // A rows (+ batch stride, elements)
@@ -28,6 +31,7 @@ struct GemmArgs {
     void* C; int ldc; int64_t sC;         // output rows (+ batch stride)
     const float* pos;                     // EPI_BIAS_GELU_POS: [M][N] f32
     int kv_B, kv_T, kv_H;                 // EPI_KVSPLIT: dest = the cross K/V cache (kv_offset)
+    float alpha = 1.0f;                   // EPI_BIAS_RESID / EPI_BIAS_F32 scale
 };
 void gemm_nt(int dtype, int epi, const GemmArgs& g, int batch, hipStream_t st);
 // variant 0: automatic (bf16 N % 256 == 0 -> 256 x 256 tile); 1: 128 x 128 tile; 2: prefer 256 x 256

@@ -1,0 +1,344 @@
+"""Host-side mirror of transcribe-rs' ParakeetEngine surface, over the spt_parakeet_* C ABI.
+
+Reference interface (transcribe-rs 0.2.3, as /root/reference/src-tauri/src/managers/
+transcription.rs uses it):
+  * ``ParakeetEngine::new()`` + ``load_model_with_params(&path, ParakeetModelParams::int8())``
+                                                             (transcription.rs:278-297)
+  * ``transcribe_samples(Vec<f32>, Some(ParakeetInferenceParams {
+        timestamp_granularity: TimestampGranularity::Segment, ..Default::default() }))``
+                                                             (transcription.rs:505-513)
+  * ``unload_model()``                                       (transcription.rs:175-208)
+  * ``TranscriptionResult { text, segments }``; the app uses ``.text`` (transcription.rs:537-546)
+
+Model sources: ``"synthetic:parakeet-tdt-0.6b-v3[:layers=N][:seed=S]"`` (seeded weights, the
+benchmark), or a NeMo ``.nemo`` checkpoint (a tar holding model_config.yaml, model_weights.ckpt
+and the tokenizer), mapped tensor by tensor onto the engine (load_nemo).  The app's catalog
+model is the ONNX int8 export of the same network; ONNX graphs are not parsed here.
+Everything below the boundary runs on the GPU (libspittle_hip.so); there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import enum
+import io
+import os
+import tarfile
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib as L
+from .engine import TranscriptionError, TranscriptionResult, TranscriptionSegment
+
+
+class TimestampGranularity(enum.IntEnum):
+    Token = L.SPT_PK_TS_TOKEN
+    Word = L.SPT_PK_TS_WORD
+    Segment = L.SPT_PK_TS_SEGMENT
+
+
+@dataclass
+class ParakeetModelParams:
+    dtype: str = "f16"            # "f16" (BASELINE config: fp16 encoder) | "f32" | "bf16"
+    device: int = 0
+    max_batch: int = 8
+    max_seconds: float = 30.0     # chunk length of one device pass
+    seed: int = 1234
+
+    @staticmethod
+    def int8() -> "ParakeetModelParams":
+        """The app's choice (transcription.rs:281).  The int8 ONNX export's quantisation is not
+        reproduced; the network runs with an fp16 encoder."""
+        return ParakeetModelParams()
+
+    @staticmethod
+    def fp32() -> "ParakeetModelParams":
+        return ParakeetModelParams(dtype="f32")
+
+
+@dataclass
+class ParakeetInferenceParams:
+    timestamp_granularity: TimestampGranularity = TimestampGranularity.Token
+    max_symbols: int = 10         # TDT greedy: tokens per encoder frame (NeMo default)
+
+
+@dataclass
+class ParakeetResult(TranscriptionResult):
+    """TranscriptionResult plus the token-level output (frames are 80 ms encoder frames)."""
+    frames: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int32))
+    n_chunks: int = 0
+
+
+_DT = {"f32": L.SPT_DTYPE_F32, "bf16": L.SPT_DTYPE_BF16, "f16": L.SPT_DTYPE_F16}
+
+
+def _check(lib, ctx, st):
+    if st != L.SPT_OK:
+        msg = lib.spt_parakeet_last_error(ctx)
+        raise TranscriptionError(st, msg.decode() if msg else "")
+
+
+class ParakeetEngine:
+    def __init__(self):
+        self._lib = L.load()
+        self._ctx = None
+        self.model_spec: Optional[str] = None
+
+    # ---- transcribe-rs surface
+    def load_model_with_params(self, path: str, params: Optional[ParakeetModelParams] = None) -> None:
+        params = params or ParakeetModelParams.int8()
+        self.unload_model()
+        path = str(path)
+        if path.startswith("synthetic:"):
+            self._create(path, params, empty=False)
+            return
+        nemo = _find_nemo(path)
+        if nemo is None:
+            raise TranscriptionError(L.SPT_ERR_LOAD, f"{path}: no .nemo checkpoint (ONNX exports are not supported)")
+        load_nemo(self, nemo, params)
+
+    def load_model(self, path: str) -> None:
+        self.load_model_with_params(path, None)
+
+    def unload_model(self) -> None:
+        if self._ctx:
+            self._lib.spt_parakeet_destroy(self._ctx)
+            self._ctx = None
+            self.model_spec = None
+
+    def transcribe_samples(self, samples, params: Optional[ParakeetInferenceParams] = None) -> ParakeetResult:
+        return self.transcribe_batch([samples], params)[0]
+
+    def __del__(self):
+        try:
+            self.unload_model()
+        except Exception:
+            pass
+
+    # ---- batched / device entry points
+    def transcribe_batch(self, batch: Sequence, params: Optional[ParakeetInferenceParams] = None) -> List[ParakeetResult]:
+        ctx = self._need()
+        arrs = [np.ascontiguousarray(np.asarray(x, dtype=np.float32).ravel()) for x in batch]
+        n = len(arrs)
+        ptrs = (C.POINTER(C.c_float) * n)(*[a.ctypes.data_as(C.POINTER(C.c_float)) for a in arrs])
+        ns = (C.c_size_t * n)(*[a.size for a in arrs])
+        outs = (C.POINTER(L.PkResult) * n)()
+        ip = self._infer(params)
+        _check(self._lib, ctx, self._lib.spt_parakeet_transcribe_batch(ctx, ptrs, ns, n, C.byref(ip), outs))
+        return [self._take(o) for o in outs]
+
+    def transcribe_device(self, pcm_dev_ptr: int, stride: int, n_samples: Sequence[int],
+                          params: Optional[ParakeetInferenceParams] = None) -> List[ParakeetResult]:
+        ctx = self._need()
+        n = len(n_samples)
+        ns = (C.c_size_t * n)(*n_samples)
+        outs = (C.POINTER(L.PkResult) * n)()
+        ip = self._infer(params)
+        _check(self._lib, ctx, self._lib.spt_parakeet_transcribe_batch_device(ctx, C.c_void_p(pcm_dev_ptr), stride, ns,
+                                                                              n, C.byref(ip), outs))
+        return [self._take(o) for o in outs]
+
+    def set_tensor(self, tid: int, data) -> None:
+        a = np.ascontiguousarray(np.asarray(data, dtype=np.float32).ravel())
+        _check(self._lib, self._ctx, self._lib.spt_parakeet_set_tensor(self._need(), int(tid),
+                                                                       a.ctypes.data_as(C.POINTER(C.c_float)), a.size))
+
+    def tensor_numel(self, tid: int) -> int:
+        n = C.c_int64()
+        st = self._lib.spt_parakeet_tensor_numel(self._need(), int(tid), C.byref(n))
+        return n.value if st == L.SPT_OK else -1
+
+    def set_vocab(self, pieces: Sequence[str]) -> None:
+        arr = (C.c_char_p * len(pieces))(*[p.encode() for p in pieces])
+        _check(self._lib, self._ctx, self._lib.spt_parakeet_set_vocab(self._need(), arr, len(pieces)))
+
+    def info(self) -> Dict[str, int]:
+        i = L.PkModelInfo()
+        _check(self._lib, self._ctx, self._lib.spt_parakeet_info(self._need(), C.byref(i)))
+        return {k: getattr(i, k) for k, _ in L.PkModelInfo._fields_}
+
+    def timings(self) -> Dict[str, float]:
+        t = L.PkTimings()
+        _check(self._lib, self._ctx, self._lib.spt_parakeet_get_timings(self._need(), C.byref(t)))
+        return {k: getattr(t, k) for k, _ in L.PkTimings._fields_}
+
+    def debug_mel(self, pcm) -> np.ndarray:
+        a = np.ascontiguousarray(np.asarray(pcm, dtype=np.float32).ravel())
+        out = np.empty((self.info()["n_mels"], a.size // 160 + 1), np.float32)
+        _check(self._lib, self._ctx, self._lib.spt_parakeet_debug_mel(self._need(), a.ctypes.data_as(C.POINTER(C.c_float)),
+                                                                      a.size, out.ctypes.data_as(C.POINTER(C.c_float))))
+        return out
+
+    def debug_encode(self, mel: np.ndarray) -> np.ndarray:
+        mel = np.ascontiguousarray(mel, dtype=np.float32)
+        T = mel.shape[1]
+        T3 = T
+        for _ in range(3):
+            T3 = (T3 - 1) // 2 + 1
+        out = np.empty((T3, self.info()["d"]), np.float32)
+        _check(self._lib, self._ctx, self._lib.spt_parakeet_debug_encode(self._need(), mel.ctypes.data_as(C.POINTER(C.c_float)),
+                                                                         T, out.ctypes.data_as(C.POINTER(C.c_float))))
+        return out
+
+    def debug_decode(self, enc: np.ndarray, max_symbols: int = 10) -> ParakeetResult:
+        enc = np.ascontiguousarray(enc, dtype=np.float32)
+        out = C.POINTER(L.PkResult)()
+        _check(self._lib, self._ctx, self._lib.spt_parakeet_debug_decode(self._need(), enc.ctypes.data_as(C.POINTER(C.c_float)),
+                                                                         enc.shape[0], max_symbols, C.byref(out)))
+        return self._take(out)
+
+    def debug_weight_checksum(self, tid: int):
+        o = (C.c_double * 2)()
+        st = self._lib.spt_parakeet_debug_weight_checksum(self._need(), int(tid), o)
+        if st == L.SPT_ERR_UNSUPPORTED:
+            return None
+        _check(self._lib, self._ctx, st)
+        return float(o[0]), float(o[1])
+
+    # ---- internals
+    def _create(self, spec: str, params: ParakeetModelParams, empty: bool) -> None:
+        if params.dtype not in _DT:
+            raise ValueError(f"dtype must be one of {sorted(_DT)}")
+        mp = L.PkModelParams()
+        self._lib.spt_parakeet_default_model_params(C.byref(mp))
+        mp.dtype = _DT[params.dtype]
+        mp.device = params.device
+        mp.max_batch = params.max_batch
+        mp.max_seconds = params.max_seconds
+        mp.seed = params.seed
+        mp.flags = L.SPT_PK_WEIGHTS_EMPTY if empty else 0
+        err = C.create_string_buffer(512)
+        ctx = C.c_void_p()
+        st = self._lib.spt_parakeet_create(spec.encode(), C.byref(mp), C.byref(ctx), err, 512)
+        if st != L.SPT_OK:
+            raise TranscriptionError(st, err.value.decode())
+        self._ctx = ctx
+        self.model_spec = spec
+
+    def _need(self):
+        if not self._ctx:
+            raise TranscriptionError(L.SPT_ERR_INVALID_ARG, "no model loaded")
+        return self._ctx
+
+    def _infer(self, params: Optional[ParakeetInferenceParams]) -> L.PkInferParams:
+        params = params or ParakeetInferenceParams()
+        ip = L.PkInferParams()
+        self._lib.spt_parakeet_default_infer_params(C.byref(ip))
+        ip.max_symbols = int(params.max_symbols)
+        ip.timestamp_granularity = int(params.timestamp_granularity)
+        return ip
+
+    def _take(self, p) -> ParakeetResult:
+        r = p.contents
+        try:
+            n = r.n_tokens
+            toks = np.ctypeslib.as_array(r.tokens, shape=(n,)).copy() if n else np.zeros(0, np.int32)
+            frames = np.ctypeslib.as_array(r.frames, shape=(n,)).copy() if n else np.zeros(0, np.int32)
+            t1 = np.ctypeslib.as_array(r.logit, shape=(n,)).copy() if n else np.zeros(0, np.float32)
+            t2 = np.ctypeslib.as_array(r.runner_up, shape=(n,)).copy() if n else np.zeros(0, np.float32)
+            segs = [TranscriptionSegment(start=r.segments[i].start, end=r.segments[i].end,
+                                         text=(r.segments[i].text or b"").decode("utf-8", "replace"),
+                                         i0=r.segments[i].i0, n_tokens=r.segments[i].n_tokens)
+                    for i in range(r.n_segments)]
+            return ParakeetResult(text=(r.text or b"").decode("utf-8", "replace"), segments=segs, tokens=toks,
+                                  top1=t1, top2=t2, frames=frames, n_chunks=r.n_chunks)
+        finally:
+            self._lib.spt_parakeet_result_free(p)
+
+
+# ------------------------------------------------------------------------------------------------
+# NeMo checkpoints
+def nemo_key_map(n_layers: int) -> Dict[str, int]:
+    """NeMo FastConformer-TDT state-dict keys -> engine tensor ids (oracle/po_model.c table)
+    [upstream NeMo module names, recalled]."""
+    m = {}
+    pre = "encoder.pre_encode."
+    for i, k in ((1, "conv.0"), (3, "conv.2"), (5, "conv.3"), (7, "conv.5"), (9, "conv.6"), (11, "out")):
+        m[pre + k + ".weight"] = i
+        m[pre + k + ".bias"] = i + 1
+    names = [("norm_feed_forward1", 0), ("feed_forward1.linear1", 2), ("feed_forward1.linear2", 4),
+             ("norm_self_att", 6), ("self_attn.linear_q", 8), ("self_attn.linear_k", 10), ("self_attn.linear_v", 12),
+             ("self_attn.linear_out", 14), ("norm_conv", 19), ("conv.pointwise_conv1", 21),
+             ("conv.depthwise_conv", 23), ("conv.pointwise_conv2", 29), ("norm_feed_forward2", 31),
+             ("feed_forward2.linear1", 33), ("feed_forward2.linear2", 35), ("norm_out", 37)]
+    for l in range(n_layers):
+        b, p = 1000 + 64 * l, f"encoder.layers.{l}."
+        for nm, off in names:
+            m[p + nm + ".weight"] = b + off
+            m[p + nm + ".bias"] = b + off + 1
+        m[p + "self_attn.linear_pos.weight"] = b + 16
+        m[p + "self_attn.pos_bias_u"] = b + 17
+        m[p + "self_attn.pos_bias_v"] = b + 18
+        for nm, off in (("weight", 25), ("bias", 26), ("running_mean", 27), ("running_var", 28)):
+            m[p + "conv.batch_norm." + nm] = b + off
+    m["decoder.prediction.embed.weight"] = 90000
+    for j in range(2):
+        for nm, off in (("weight_ih", 1), ("weight_hh", 2), ("bias_ih", 3), ("bias_hh", 4)):
+            m[f"decoder.prediction.dec_rnn.lstm.{nm}_l{j}"] = 90000 + off + 4 * j
+    for nm, i in (("joint.enc", 90009), ("joint.pred", 90011), ("joint.joint_net.2", 90013)):
+        m[nm + ".weight"] = i
+        m[nm + ".bias"] = i + 1
+    return m
+
+
+def _find_nemo(path: str) -> Optional[str]:
+    if os.path.isfile(path) and path.endswith(".nemo"):
+        return path
+    if os.path.isdir(path):
+        for f in sorted(os.listdir(path)):
+            if f.endswith(".nemo"):
+                return os.path.join(path, f)
+    return None
+
+
+def _nemo_dims(cfg: dict) -> Dict[str, int]:
+    enc, dec, joint = cfg["encoder"], cfg["decoder"], cfg["joint"]
+    return {"n_mels": int(enc.get("feat_in", 128)), "d": int(enc["d_model"]), "n_layers": int(enc["n_layers"]),
+            "n_heads": int(enc["n_heads"]), "ff": int(enc["d_model"]) * int(enc.get("ff_expansion_factor", 4)),
+            "sub_ch": int(enc.get("subsampling_conv_channels", 256)), "conv_k": int(enc.get("conv_kernel_size", 9)),
+            "pred": int(dec["prednet"]["pred_hidden"]), "n_vocab": int(joint["num_classes"]),
+            "n_dur": len(cfg.get("model_defaults", {}).get("tdt_durations", [0, 1, 2, 3, 4]))}
+
+
+def load_nemo(engine: ParakeetEngine, path: str, params: ParakeetModelParams,
+              pieces_loader: Optional[Callable[[bytes], List[str]]] = None) -> None:
+    """Load a NeMo FastConformer-TDT checkpoint: the config gives the shape, the state dict
+    (torch.load(weights_only=True): nothing in the file is executed) the tensors, the
+    SentencePiece model the vocabulary.  The engine is created empty and filled tensor by tensor."""
+    import torch
+    import yaml
+
+    with tarfile.open(path, "r:*") as tf:
+        members = {os.path.basename(m.name): m for m in tf.getmembers() if m.isfile()}
+        cfg = yaml.safe_load(tf.extractfile(members["model_config.yaml"]).read())
+        sd = torch.load(io.BytesIO(tf.extractfile(members["model_weights.ckpt"]).read()), map_location="cpu",
+                        weights_only=True)
+        tok = next((members[k] for k in members if k.endswith("tokenizer.model")), None)
+        tok_bytes = tf.extractfile(tok).read() if tok is not None else None
+    dims = _nemo_dims(cfg)
+    name = "parakeet-tdt-0.6b-v3" if dims["d"] == 1024 else "parakeet-test-small"
+    engine._create(f"synthetic:{name}:layers={dims['n_layers']}", params, empty=True)
+    info = engine.info()
+    for k in ("n_mels", "d", "n_heads", "ff", "sub_ch", "conv_k", "pred", "n_vocab", "n_dur"):
+        if info[k] != dims[k]:
+            engine.unload_model()
+            raise TranscriptionError(L.SPT_ERR_LOAD, f"{path}: {k}={dims[k]} is not a supported Parakeet shape")
+    kmap = nemo_key_map(dims["n_layers"])
+    seen = set()
+    for key, tid in kmap.items():
+        if key not in sd:
+            engine.unload_model()
+            raise TranscriptionError(L.SPT_ERR_LOAD, f"{path}: missing tensor {key}")
+        engine.set_tensor(tid, sd[key].detach().float().cpu().numpy())
+        seen.add(tid)
+    if tok_bytes is not None:
+        loader = pieces_loader or _sentencepiece_pieces
+        engine.set_vocab(loader(tok_bytes))
+    engine.model_spec = path
+
+
+def _sentencepiece_pieces(model_bytes: bytes) -> List[str]:
+    import sentencepiece as spm
+    sp = spm.SentencePieceProcessor(model_proto=model_bytes)
+    return [sp.id_to_piece(i) for i in range(sp.get_piece_size())]

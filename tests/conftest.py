@@ -12,11 +12,15 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; run with -m gpu")
 
 
-@pytest.fixture(autouse=True)
+@pytest.fixture(scope="session", autouse=True)
 def _torch_hip_first(request):
-    """GPU tests: initialise torch's bundled HIP runtime before the library's /opt/rocm one
-    (the order bench.py uses); the other order left torch without a device on one box."""
-    if request.node.get_closest_marker("gpu") is not None:
+    """GPU runs: initialise torch's bundled HIP runtime before the library's /opt/rocm one (the
+    order bench.py uses).  The other order leaves torch without a device ("No HIP GPUs are
+    available"), so this is session-scoped: it must precede module-scoped engine fixtures."""
+    if any(item.get_closest_marker("gpu") is not None for item in request.session.items):
         import torch
-        torch.cuda.init()
+        try:
+            torch.cuda.init()
+        except RuntimeError:  # no GPU here (a CPU run that selected GPU tests): they fail on their own
+            pass
     yield
