@@ -38,6 +38,9 @@ N_STEPS = 128
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
 MFMA_PEAK_BF16_TFS = 2500.0  # dense bf16
 FP32_PEAK_TFS = 157.3        # f32 MFMA = vector rate
+MFMA_PEAK_F16_TFS = 2500.0   # dense fp16 (same rate as bf16)
+PK_SPEC = "synthetic:parakeet-tdt-0.6b-v3"
+PK_PUBLISHED_RTFX = 5.0      # README.md:151: Parakeet V3 "~5x real-time speed", CPU (i5), ONNX int8
 
 
 def metric_for(model: str) -> str:
@@ -57,6 +60,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-app-latency", action="store_true", help="skip the B=1 whisper_full (app default) latency")
     ap.add_argument("--no-probe", action="store_true", help="skip the per-kernel HIP-event probes")
+    ap.add_argument("--no-parakeet", action="store_true", help="skip the Parakeet-V3 (BASELINE config 5) lines")
+    ap.add_argument("--parakeet-only", action="store_true", help="only the Parakeet-V3 lines (developer runs)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL) for the real run; gloo only to rehearse N > 1 ranks on one GPU")
     ap.add_argument("--no-weight-bcast", action="store_true",
@@ -214,6 +219,100 @@ def phase_rooflines(info: dict, phases: dict, B: int, decode_steps: int, dtype: 
     return out
 
 
+def parakeet_encoder_flops(info: dict, T: int) -> int:
+    """Algorithmic FLOPs of one utterance's Parakeet encoder pass at T mel frames (SURVEY §8d
+    style): subsampling convolutions + linear, the per-layer GEMMs (two half-FFNs, q/k/v/out,
+    the convolution module's pointwise pair), the relative-position projection, attention
+    (q.k, q.p and p.v over the T3 x T3 pairs), and the joint's encoder projection."""
+    h = lambda t: (t - 1) // 2 + 1
+    d, ff, C, L, P, K = info["d"], info["ff"], info["sub_ch"], info["n_layers"], info["pred"], info["conv_k"]
+    T1, T2, T3 = h(T), h(h(T)), h(h(h(T)))
+    F1, F2, F3 = h(info["n_mels"]), h(h(info["n_mels"])), h(h(h(info["n_mels"])))
+    sub = 2 * 9 * C * T1 * F1 + 2 * 9 * C * (T2 * F2 + T3 * F3) + 2 * C * C * (T2 * F2 + T3 * F3) + 2 * C * F3 * d * T3
+    layer = T3 * (2 * 2 * 2 * d * ff + 2 * 4 * d * d + 2 * 3 * d * d + 2 * d * K) + 6 * T3 * T3 * d
+    pos = 2 * (2 * T3 - 1) * d * d * L
+    return int(sub + L * layer + pos + 2 * T3 * d * P)
+
+
+def parakeet_bench(device: int, steps: int, warmup: int, with_cpu: bool) -> dict:
+    """BASELINE config 5 (BASELINE.json configs[4]): Parakeet-V3 -- synthetic
+    parakeet-tdt-0.6b-v3 weights (NeMo FastConformer-TDT shape, 24 layers, d 1024), fp16 encoder,
+    f32 TDT greedy decoding, the app's Segment timestamps, host PCM in, text out.
+      * streaming: 64 concurrent 1 s windows per pass (RTFx = 64 s / pass wall time), and one
+        1 s window alone (the latency of a single stream's window);
+      * offline: 8 x 30 s chunks per pass (the app's whole-recording call, batched).
+    cpu_baseline: the oracle (C restatement, fp32, OpenMP) on one 5 s utterance end to end."""
+    import numpy as np
+    from spittle_amd import ParakeetEngine, ParakeetInferenceParams, ParakeetModelParams, TimestampGranularity
+    from spittle_amd.synth import synth_audio
+    e = ParakeetEngine()
+    e.load_model_with_params(PK_SPEC, ParakeetModelParams(dtype="f16", device=device, max_batch=64, max_seconds=30.0))
+    info = e.info()
+    prm = ParakeetInferenceParams(timestamp_granularity=TimestampGranularity.Segment)
+
+    def run(batch):
+        for _ in range(warmup):
+            e.transcribe_batch(batch, prm)
+        ts, res = [], None
+        for _ in range(steps):
+            t0 = time.perf_counter()
+            res = e.transcribe_batch(batch, prm)
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)), float(np.sum(ts)), res, e.timings()
+
+    out = {"model": PK_SPEC, "dtype": "f16 encoder, f32 prediction network + joint",
+           "data": "synthetic (BASELINE.md §3 seeded 16 kHz signal; random-init weights)"}
+    only = os.environ.get("PK_BENCH_ONLY", "")  # developer profiling: one workload
+    w1 = [synth_audio(3000 + i)[:16000] for i in range(64)]
+    if only == "offline":
+        w1 = w1[:1]
+    med, tot, res, ph = run(w1)
+    flops = 64 * parakeet_encoder_flops(info, 16000 // 160 + 1)
+    tf = flops / (ph["encoder_ms"] * 1e-3) / 1e12
+    out["streaming_1s_b64"] = {"rtfx": round(64 * steps / tot, 2), "ms_per_pass_median": round(med * 1e3, 3),
+                               "phases_ms": {k: round(v, 3) for k, v in ph.items() if k.endswith("_ms")},
+                               "decode_steps": ph["n_steps"], "tokens_first_window": len(res[0].tokens),
+                               "encoder_roofline": {"bound": "mfma", "flops_per_call": flops, "achieved": round(tf, 1),
+                                                    "peak": MFMA_PEAK_F16_TFS, "unit": "TFLOP/s",
+                                                    "frac": round(tf / MFMA_PEAK_F16_TFS, 4)}}
+    med, tot, res, ph = run(w1[:1])
+    out["streaming_1s_b1_latency_ms"] = {"median": round(med * 1e3, 3),
+                                         "phases_ms": {k: round(v, 3) for k, v in ph.items() if k.endswith("_ms")},
+                                         "decode_steps": ph["n_steps"]}
+    w30 = [synth_audio(i) for i in range(8)]
+    if only == "stream":
+        w30 = [w30[0][:16000]]
+    med, tot, res, ph = run(w30)
+    flops = 8 * parakeet_encoder_flops(info, 480000 // 160 + 1)
+    tf = flops / (ph["encoder_ms"] * 1e-3) / 1e12
+    out["offline_30s_b8"] = {"rtfx": round(8 * 30.0 * steps / tot, 2), "ms_per_pass_median": round(med * 1e3, 3),
+                             "phases_ms": {k: round(v, 3) for k, v in ph.items() if k.endswith("_ms")},
+                             "decode_steps": ph["n_steps"], "tokens_first_chunk": len(res[0].tokens),
+                             "encoder_roofline": {"bound": "mfma", "flops_per_call": flops, "achieved": round(tf, 1),
+                                                  "peak": MFMA_PEAK_F16_TFS, "unit": "TFLOP/s",
+                                                  "frac": round(tf / MFMA_PEAK_F16_TFS, 4)}}
+    out["vs_published_cpu_rtfx"] = {"published": PK_PUBLISHED_RTFX, "source": "README.md:151 (i5 CPU, ONNX int8)",
+                                    "streaming_ratio": round(out["streaming_1s_b64"]["rtfx"] / PK_PUBLISHED_RTFX, 1)}
+    e.unload_model()
+    if with_cpu:
+        from oracle import parakeet as PO
+        cpu = host_cpu()
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(cpu["affinity_cpus"] or 1, 16)
+        PO.set_threads(threads)
+        m = PO.Model(PO.dims_for("parakeet-tdt-0.6b-v3"), 1234, PO.W_F32)
+        x = synth_audio(3100)[:16000 * 5]
+        t0 = time.perf_counter()
+        enc = m.encode(PO.mel(x))
+        m.decode(enc)
+        dt = time.perf_counter() - t0
+        m.close()
+        out["cpu_baseline"] = {"value": round(5.0 / dt, 3), "unit": "audio-sec/wall-sec", "cores": threads,
+                               "kind": "port", "cpu_model": cpu["model"],
+                               "sample": f"1 x 5 s utterance, parakeet-tdt-0.6b-v3 dims fp32, {threads} OpenMP threads, "
+                                         f"mel + encoder + TDT greedy {dt:.2f}s (timed whole)"}
+    return out
+
+
 def app_latency(eng, dur_s=(5, 10, 30)) -> dict:
     """The app's real call (transcription.rs:494-503): one utterance (B = 1), whisper_full with
     its default parameters (timestamps on, temperature fallback 0.2 / best_of 5), language
@@ -268,6 +367,11 @@ def main():
             dist.init_process_group(args.dist_backend)
         assert dist.get_world_size() == args.gpus
     dev = torch.device("cuda", local)
+    if args.parakeet_only:
+        torch.cuda.synchronize()
+        print(json.dumps({"parakeet": parakeet_bench(local, args.steps, args.warmup, not args.no_cpu_baseline)}),
+              flush=True)
+        return
 
     from spittle_amd import WhisperEngine, WhisperInferenceParams, WhisperModelParams
     from spittle_amd.dist import broadcast_weights, max_over_ranks, shard_range
@@ -347,6 +451,10 @@ def main():
             app = app_latency(eng)
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.model, args.decode_steps)
+    pk = None
+    if rank == 0 and world == 1 and not args.no_parakeet:
+        eng.unload_model()  # free the Whisper arenas first
+        pk = parakeet_bench(local, min(args.steps, 10), max(1, args.warmup), not args.no_cpu_baseline)
     if rank == 0:
         out = {
             "metric": metric_for(args.model), "value": round(value, 3), "unit": "audio-sec/wall-sec", "n_gpus": world,
@@ -371,6 +479,8 @@ def main():
             out["ms_per_step_per_rank"] = rank_ms
         if wload:
             out["weight_load"] = wload
+        if pk:
+            out["parakeet_v3"] = pk
         print(json.dumps(out), flush=True)
     eng.unload_model()
     if world > 1:

@@ -1,12 +1,12 @@
-//! Raw bindings to `include/spittle_hip.h` (ABI 5), the C boundary of the MI355X-native Whisper
-//! backend.  One item per declaration of the header, same names, same layouts (x86-64 SysV; the
+//! Raw bindings to `include/spittle_hip.h` (ABI 6), the C boundary of the MI355X-native Whisper
+//! and Parakeet-V3 backend.  One item per declaration of the header, same names, same layouts (x86-64 SysV; the
 //! layouts are checked field by field against gcc by tests/test_capi.py).  Safe wrappers live in
 //! the `spittle-hip` crate.
 #![allow(non_camel_case_types)]
 
 use std::os::raw::{c_char, c_int, c_void};
 
-pub const SPT_ABI_VERSION: c_int = 5;
+pub const SPT_ABI_VERSION: c_int = 6;
 
 pub type spt_status = c_int;
 pub const SPT_OK: spt_status = 0;
@@ -20,6 +20,7 @@ pub const SPT_ERR_INTERNAL: spt_status = 6;
 pub type spt_dtype = c_int;
 pub const SPT_DTYPE_F32: spt_dtype = 0;
 pub const SPT_DTYPE_BF16: spt_dtype = 1;
+pub const SPT_DTYPE_F16: spt_dtype = 2;
 
 pub const SPT_SUPPRESS_BLANK: u32 = 1;
 pub const SPT_NO_TIMESTAMPS: u32 = 2;
@@ -230,4 +231,146 @@ extern "C" {
         n_out: *mut i32,
     ) -> spt_status;
     pub fn spt_debug_ggml_dequant(ggml_type: i32, src: *const c_void, n: i64, dst: *mut f32) -> spt_status;
+
+    // ---- ABI 6: Parakeet-V3
+    pub fn spt_parakeet_default_model_params(p: *mut spt_pk_model_params);
+    pub fn spt_parakeet_default_infer_params(p: *mut spt_pk_infer_params);
+    pub fn spt_parakeet_create(
+        model_spec: *const c_char,
+        params: *const spt_pk_model_params,
+        out: *mut *mut spt_pk_ctx,
+        err: *mut c_char,
+        errlen: usize,
+    ) -> spt_status;
+    pub fn spt_parakeet_destroy(ctx: *mut spt_pk_ctx);
+    pub fn spt_parakeet_last_error(ctx: *const spt_pk_ctx) -> *const c_char;
+    pub fn spt_parakeet_info(ctx: *const spt_pk_ctx, info: *mut spt_pk_model_info) -> spt_status;
+    pub fn spt_parakeet_tensor_numel(ctx: *const spt_pk_ctx, tensor_id: i32, n: *mut i64) -> spt_status;
+    pub fn spt_parakeet_set_tensor(ctx: *mut spt_pk_ctx, tensor_id: i32, data: *const f32, n: i64) -> spt_status;
+    pub fn spt_parakeet_set_vocab(ctx: *mut spt_pk_ctx, pieces: *const *const c_char, n: i32) -> spt_status;
+    pub fn spt_parakeet_transcribe(
+        ctx: *mut spt_pk_ctx,
+        pcm16k: *const f32,
+        n_samples: usize,
+        params: *const spt_pk_infer_params,
+        out: *mut *mut spt_pk_result,
+    ) -> spt_status;
+    pub fn spt_parakeet_transcribe_batch(
+        ctx: *mut spt_pk_ctx,
+        pcm: *const *const f32,
+        n_samples: *const usize,
+        batch: usize,
+        params: *const spt_pk_infer_params,
+        out: *mut *mut spt_pk_result,
+    ) -> spt_status;
+    pub fn spt_parakeet_transcribe_batch_device(
+        ctx: *mut spt_pk_ctx,
+        pcm_dev: *const f32,
+        stride: usize,
+        n_samples: *const usize,
+        batch: usize,
+        params: *const spt_pk_infer_params,
+        out: *mut *mut spt_pk_result,
+    ) -> spt_status;
+    pub fn spt_parakeet_result_free(r: *mut spt_pk_result);
+    pub fn spt_parakeet_get_timings(ctx: *const spt_pk_ctx, t: *mut spt_pk_timings) -> spt_status;
+    pub fn spt_parakeet_debug_mel(ctx: *mut spt_pk_ctx, pcm16k: *const f32, n_samples: usize, out: *mut f32) -> spt_status;
+    pub fn spt_parakeet_debug_encode(ctx: *mut spt_pk_ctx, mel: *const f32, t: i32, out: *mut f32) -> spt_status;
+    pub fn spt_parakeet_debug_decode(
+        ctx: *mut spt_pk_ctx,
+        enc: *const f32,
+        t3: i32,
+        max_symbols: i32,
+        out: *mut *mut spt_pk_result,
+    ) -> spt_status;
+    pub fn spt_parakeet_debug_weight_checksum(ctx: *mut spt_pk_ctx, tensor_id: i32, out2: *mut f64) -> spt_status;
+}
+
+// ---- ABI 6: Parakeet-V3 types
+pub const SPT_PK_WEIGHTS_EMPTY: u32 = 1;
+pub type spt_pk_granularity = c_int;
+pub const SPT_PK_TS_TOKEN: spt_pk_granularity = 0;
+pub const SPT_PK_TS_WORD: spt_pk_granularity = 1;
+pub const SPT_PK_TS_SEGMENT: spt_pk_granularity = 2;
+
+#[repr(C)]
+pub struct spt_pk_ctx {
+    _private: [u8; 0],
+}
+
+#[repr(C)]
+#[derive(Clone, Copy, Debug)]
+pub struct spt_pk_model_params {
+    pub dtype: i32,
+    pub device: i32,
+    pub max_batch: i32,
+    pub max_seconds: f32,
+    pub seed: u64,
+    pub flags: u32,
+    pub reserved0: i32,
+}
+
+#[repr(C)]
+#[derive(Clone, Copy, Debug)]
+pub struct spt_pk_infer_params {
+    pub max_symbols: i32,
+    pub timestamp_granularity: i32,
+}
+
+#[repr(C)]
+pub struct spt_pk_segment {
+    pub start: f64,
+    pub end: f64,
+    pub text: *mut c_char,
+    pub i0: i32,
+    pub n_tokens: i32,
+}
+
+#[repr(C)]
+pub struct spt_pk_result {
+    pub text: *mut c_char,
+    pub tokens: *mut i32,
+    pub frames: *mut i32,
+    pub logit: *mut f32,
+    pub runner_up: *mut f32,
+    pub n_tokens: i32,
+    pub n_segments: i32,
+    pub segments: *mut spt_pk_segment,
+    pub n_chunks: i32,
+    pub reserved0: i32,
+}
+
+#[repr(C)]
+#[derive(Clone, Copy, Debug, Default)]
+pub struct spt_pk_model_info {
+    pub n_mels: i32,
+    pub d: i32,
+    pub n_layers: i32,
+    pub n_heads: i32,
+    pub ff: i32,
+    pub sub_ch: i32,
+    pub conv_k: i32,
+    pub pred: i32,
+    pub n_vocab: i32,
+    pub n_dur: i32,
+    pub dtype: i32,
+    pub max_batch: i32,
+    pub max_samples: i32,
+    pub reserved0: i32,
+    pub weight_bytes: i64,
+    pub workspace_bytes: i64,
+}
+
+#[repr(C)]
+#[derive(Clone, Copy, Debug, Default)]
+pub struct spt_pk_timings {
+    pub mel_ms: f64,
+    pub encoder_ms: f64,
+    pub decode_ms: f64,
+    pub total_ms: f64,
+    pub h2d_ms: f64,
+    pub n_steps: i32,
+    pub batch: i32,
+    pub enc_frames: i32,
+    pub reserved0: i32,
 }

@@ -1,5 +1,5 @@
-//! `HipWhisperEngine`: the `transcribe_rs::TranscriptionEngine` surface Spittle binds to,
-//! backed by the MI355X-native Whisper library (`libspittle_hip.so`, C ABI 5).
+//! `HipWhisperEngine` and `HipParakeetEngine`: the `transcribe_rs::TranscriptionEngine` surfaces
+//! Spittle binds to, backed by the MI355X-native library (`libspittle_hip.so`, C ABI 6).
 //!
 //! What it replaces in the app (/root/reference/src-tauri/src/managers/transcription.rs):
 //!
@@ -26,6 +26,7 @@ use std::os::raw::c_char;
 use std::path::Path;
 
 use spittle_hip_sys as sys;
+use transcribe_rs::engines::parakeet::{ParakeetInferenceParams, TimestampGranularity};
 use transcribe_rs::engines::whisper::WhisperInferenceParams;
 use transcribe_rs::{TranscriptionEngine, TranscriptionResult, TranscriptionSegment};
 
@@ -304,5 +305,157 @@ impl Drop for HipWhisperReplicas {
             // SAFETY: each context is destroyed once
             unsafe { sys::spt_ctx_destroy(c) };
         }
+    }
+}
+
+/// Device-side Parakeet parameters (`spt_pk_model_params`).  `int8()` mirrors the app's
+/// `ParakeetModelParams::int8()` (transcription.rs:281); the network runs with an fp16 encoder.
+#[derive(Clone, Copy, Debug)]
+pub struct HipParakeetModelParams {
+    pub fp16: bool,
+    pub device: i32,
+    pub max_batch: i32,
+    pub max_seconds: f32,
+}
+
+impl HipParakeetModelParams {
+    pub fn int8() -> Self {
+        Self { fp16: true, device: 0, max_batch: 8, max_seconds: 30.0 }
+    }
+}
+
+impl Default for HipParakeetModelParams {
+    fn default() -> Self {
+        Self::int8()
+    }
+}
+
+/// Parakeet-V3 (FastConformer-TDT) on one MI355X.  What it replaces: `LoadedEngine::Parakeet`
+/// (transcription.rs:278-297 load, :505-513 `transcribe_samples` with
+/// `TimestampGranularity::Segment`).  The model path is a synthetic spec; a NeMo checkpoint is
+/// mapped onto the context tensor by tensor with `set_tensor`.
+pub struct HipParakeetEngine {
+    ctx: *mut sys::spt_pk_ctx,
+}
+
+// SAFETY: as for HipWhisperEngine (calls serialised by the app's Mutex; not thread-affine)
+unsafe impl Send for HipParakeetEngine {}
+
+impl HipParakeetEngine {
+    pub fn new() -> Self {
+        Self { ctx: std::ptr::null_mut() }
+    }
+
+    fn last_error(&self) -> String {
+        // SAFETY: accepts any context pointer (a static string for null)
+        unsafe { CStr::from_ptr(sys::spt_parakeet_last_error(self.ctx)).to_string_lossy().into_owned() }
+    }
+
+    /// One weight tensor (f32, NeMo layout) by the id table of oracle/po_model.c.
+    pub fn set_tensor(&mut self, tensor_id: i32, data: &[f32]) -> Result<(), Box<dyn Error>> {
+        // SAFETY: data is valid for its length during the call
+        let st = unsafe { sys::spt_parakeet_set_tensor(self.ctx, tensor_id, data.as_ptr(), data.len() as i64) };
+        if st != sys::SPT_OK {
+            return Err(status_error("set_tensor", st, self.last_error()));
+        }
+        Ok(())
+    }
+}
+
+impl Default for HipParakeetEngine {
+    fn default() -> Self {
+        Self::new()
+    }
+}
+
+fn granularity(g: &TimestampGranularity) -> i32 {
+    match g {
+        TimestampGranularity::Token => sys::SPT_PK_TS_TOKEN,
+        TimestampGranularity::Word => sys::SPT_PK_TS_WORD,
+        TimestampGranularity::Segment => sys::SPT_PK_TS_SEGMENT,
+    }
+}
+
+impl TranscriptionEngine for HipParakeetEngine {
+    type InferenceParams = ParakeetInferenceParams;
+    type ModelParams = HipParakeetModelParams;
+
+    fn load_model_with_params(&mut self, model_path: &Path, params: HipParakeetModelParams) -> Result<(), Box<dyn Error>> {
+        self.unload_model();
+        let spec = CString::new(model_path.to_string_lossy().as_bytes())?;
+        let mut mp = std::mem::MaybeUninit::<sys::spt_pk_model_params>::uninit();
+        // SAFETY: fills every field
+        let mut mp = unsafe {
+            sys::spt_parakeet_default_model_params(mp.as_mut_ptr());
+            mp.assume_init()
+        };
+        mp.dtype = if params.fp16 { sys::SPT_DTYPE_F16 } else { sys::SPT_DTYPE_F32 };
+        mp.device = params.device;
+        mp.max_batch = params.max_batch;
+        mp.max_seconds = params.max_seconds;
+        let mut err = vec![0 as c_char; 1024];
+        let mut ctx = std::ptr::null_mut();
+        // SAFETY: valid C strings and out-pointers for the duration of the call
+        let st = unsafe { sys::spt_parakeet_create(spec.as_ptr(), &mp, &mut ctx, err.as_mut_ptr(), err.len()) };
+        if st != sys::SPT_OK {
+            // SAFETY: the library NUL-terminates err
+            let msg = unsafe { CStr::from_ptr(err.as_ptr()) }.to_string_lossy().into_owned();
+            return Err(status_error("model load", st, msg));
+        }
+        self.ctx = ctx;
+        Ok(())
+    }
+
+    fn unload_model(&mut self) {
+        if !self.ctx.is_null() {
+            // SAFETY: created by spt_parakeet_create, destroyed once
+            unsafe { sys::spt_parakeet_destroy(self.ctx) };
+            self.ctx = std::ptr::null_mut();
+        }
+    }
+
+    fn transcribe_samples(
+        &mut self,
+        samples: Vec<f32>,
+        params: Option<ParakeetInferenceParams>,
+    ) -> Result<TranscriptionResult, Box<dyn Error>> {
+        if self.ctx.is_null() {
+            return Err("Model is not loaded for transcription.".into());
+        }
+        let mut ip = sys::spt_pk_infer_params { max_symbols: 10, timestamp_granularity: sys::SPT_PK_TS_SEGMENT };
+        // SAFETY: fills every field
+        unsafe { sys::spt_parakeet_default_infer_params(&mut ip) };
+        if let Some(p) = params.as_ref() {
+            ip.timestamp_granularity = granularity(&p.timestamp_granularity);
+        }
+        let mut out = std::ptr::null_mut();
+        // SAFETY: samples outlives the call; out receives a library-owned result
+        let st = unsafe { sys::spt_parakeet_transcribe(self.ctx, samples.as_ptr(), samples.len(), &ip, &mut out) };
+        if st != sys::SPT_OK {
+            return Err(status_error("transcription", st, self.last_error()));
+        }
+        // SAFETY: a successful call returns a live result, read then freed once
+        unsafe {
+            let res = &*out;
+            let text = if res.text.is_null() { String::new() } else { CStr::from_ptr(res.text).to_string_lossy().into_owned() };
+            let segments = (0..res.n_segments.max(0) as usize)
+                .map(|i| {
+                    let s = &*res.segments.add(i);
+                    TranscriptionSegment {
+                        start: s.start as f32,
+                        end: s.end as f32,
+                        text: if s.text.is_null() { String::new() } else { CStr::from_ptr(s.text).to_string_lossy().into_owned() },
+                    }
+                })
+                .collect();
+            sys::spt_parakeet_result_free(out);
+            Ok(TranscriptionResult { text, segments: Some(segments) })
+        }
+    }
+}
+
+impl Drop for HipParakeetEngine {
+    fn drop(&mut self) {
+        self.unload_model();
     }
 }

@@ -69,6 +69,8 @@ __device__ __forceinline__ void epi_store(const GemmArgs& g, int bz, int row, co
         ((T*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col] = from_f<T>(fmaxf(v, 0.0f));
     } else if constexpr (EPI == EPI_BIAS_F32) {
         ((float*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col] = g.alpha * v;
+    } else if constexpr (EPI == EPI_PARTIAL) {
+        ((float*)g.C + (size_t)blockIdx.y * g.c_split)[(size_t)row * g.ldc + e.col] = v;
     } else if constexpr (EPI == EPI_BIAS_GELU) {
         ((T*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col] = from_f<T>(gelu_tanh(v));
     } else if constexpr (EPI == EPI_BIAS_GELU_POS) {
@@ -94,8 +96,9 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
     const int tm = wg / nnt, tn = wg - tm * nnt;
     const int m0 = tm * BM, n0 = tn * BN;
     const int bz = blockIdx.z;
-    const T* A = (const T*)g.A + (size_t)bz * g.sA;
-    const T* W = (const T*)g.W;
+    const int Kc = g.K / g.ksplit;  // this workgroup's K range: [blockIdx.y * Kc, + Kc)
+    const T* A = (const T*)g.A + (size_t)bz * g.sA + (size_t)blockIdx.y * Kc;
+    const T* W = (const T*)g.W + (size_t)blockIdx.y * Kc;
 
     // per-lane source pointers for the 4 A pieces and 4 W pieces this wave stages
     const char* srcA[4];
@@ -126,7 +129,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const int nkt = g.K * (int)sizeof(T) / SLAB;
+    const int nkt = Kc * (int)sizeof(T) / SLAB;
     const int fr = lane & 15, fq = lane >> 4;
 
     stage(0, 0);
@@ -239,9 +242,10 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     const int tm = wg / nnt, tn = wg - tm * nnt;
     const int m0 = tm * G2_BM, n0 = tn * G2_BN;
     const int bz = blockIdx.z;
-    const bf16* A = (const bf16*)g.A + (size_t)bz * g.sA;
-    const bf16* W = (const bf16*)g.W;
-    const int nkt = g.K / 64;
+    const int Kc = g.K / g.ksplit;
+    const bf16* A = (const bf16*)g.A + (size_t)bz * g.sA + (size_t)blockIdx.y * Kc;
+    const bf16* W = (const bf16*)g.W + (size_t)blockIdx.y * Kc;
+    const int nkt = Kc / 64;
 
     // staging sources: half-tile h of A (or W), instruction i (0, 1) of this wave -> 8 rows
     const int prow = lane >> 3, pch = lane & 7;
@@ -369,7 +373,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     // would be 2- or 4-byte stores at a row stride).  bf16 outputs: one pass of 128 rows,
     // row stride 144 B; f32 outputs: two passes of 64 rows, row stride 272 B (the 16-byte pad
     // spreads the four row groups a store instruction writes over distinct banks).
-    constexpr bool F32OUT = EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU_POS || EPI == EPI_BIAS_F32;
+    constexpr bool F32OUT = EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU_POS || EPI == EPI_BIAS_F32 || EPI == EPI_PARTIAL;
     constexpr int ESZ = F32OUT ? 4 : 2;
     constexpr int RS = 64 * ESZ + 16;          // LDS row stride (bytes)
     constexpr int PR = F32OUT ? 64 : 128;      // rows per pass
@@ -417,6 +421,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
                 const int kvi = rem / d, hh = (rem - kvi * d) >> 6, el = rem & 63;
                 const int bb = row / g.kv_T, t = row - bb * g.kv_T;
                 *(uint4*)((bf16*)g.C + kv_offset(l, kvi, bb, hh, t, el, g.kv_B, g.kv_H, g.kv_T)) = v;
+            } else if constexpr (EPI == EPI_PARTIAL) {
+                *(uint4*)((float*)g.C + (size_t)blockIdx.y * g.c_split + (size_t)row * g.ldc + col) = v;
             } else {
                 float* cp = (float*)g.C + (size_t)bz * g.sC + (size_t)row * g.ldc + col;
                 float4 o = *(const float4*)&v;
@@ -440,14 +446,14 @@ void launch_256(const GemmArgs& g, int batch, hipStream_t st) {
                                       G2_LDS_ALL));
         attr = true;
     }
-    dim3 grid(cdiv(g.M, G2_BM) * (g.N / G2_BN), 1, batch);
+    dim3 grid(cdiv(g.M, G2_BM) * (g.N / G2_BN), g.ksplit, batch);
     hipLaunchKernelGGL((gemm256_kernel<EPI, F16>), grid, dim3(512), G2_LDS_ALL, st, g);
     SPT_LAUNCH_CHECK();
 }
 
 template <typename T, int EPI>
 void launch_t(const GemmArgs& g, int batch, hipStream_t st) {
-    dim3 grid(cdiv(g.M, BM) * (g.N / BN), 1, batch);
+    dim3 grid(cdiv(g.M, BM) * (g.N / BN), g.ksplit, batch);
     hipLaunchKernelGGL((gemm_nt_kernel<T, EPI>), grid, dim3(256), 0, st, g);
 }
 
@@ -457,7 +463,9 @@ void gemm_nt(int dtype, int epi, const GemmArgs& g, int batch, hipStream_t st) {
 
 void gemm_nt_variant(int dtype, int epi, const GemmArgs& g, int batch, int variant, hipStream_t st) {
     const int esz = dtype == DT_F32 ? 4 : 2;
-    if (g.N % BN != 0 || (g.K * esz) % SLAB != 0 || g.M <= 0)
+    if (g.ksplit < 1 || g.K % g.ksplit || (g.ksplit > 1 && epi != EPI_PARTIAL))
+        throw std::runtime_error("gemm_nt: split-K needs EPI_PARTIAL and K % ksplit == 0");
+    if (g.N % BN != 0 || (g.K / g.ksplit * esz) % SLAB != 0 || g.M <= 0)
         throw std::runtime_error("gemm_nt: unsupported shape M=" + std::to_string(g.M) + " N=" +
                                  std::to_string(g.N) + " K=" + std::to_string(g.K));
 #define SPT_GEMM_CASES(T)                                                          \
@@ -470,6 +478,7 @@ void gemm_nt_variant(int dtype, int epi, const GemmArgs& g, int batch, int varia
         case EPI_BIAS_SWISH: launch_t<T, EPI_BIAS_SWISH>(g, batch, st); return;    \
         case EPI_BIAS_RELU: launch_t<T, EPI_BIAS_RELU>(g, batch, st); return;      \
         case EPI_BIAS_F32: launch_t<T, EPI_BIAS_F32>(g, batch, st); return;        \
+        case EPI_PARTIAL: launch_t<T, EPI_PARTIAL>(g, batch, st); return;          \
     }
 #define SPT_GEMM256_CASES(F)                                                       \
     switch (epi) {                                                                 \
@@ -481,11 +490,12 @@ void gemm_nt_variant(int dtype, int epi, const GemmArgs& g, int batch, int varia
         case EPI_BIAS_SWISH: launch_256<EPI_BIAS_SWISH, F>(g, batch, st); return;  \
         case EPI_BIAS_RELU: launch_256<EPI_BIAS_RELU, F>(g, batch, st); return;    \
         case EPI_BIAS_F32: launch_256<EPI_BIAS_F32, F>(g, batch, st); return;      \
+        case EPI_PARTIAL: launch_256<EPI_PARTIAL, F>(g, batch, st); return;        \
     }
     static const bool force128 = getenv("SPT_GEMM128") != nullptr;  // A/B switch for measurements
     const bool use256 = variant == 2 || (variant == 0 && !force128);
     const bool fits32 = (int64_t)g.M * g.lda < (1ll << 31) && (int64_t)g.N * g.ldw < (1ll << 31);
-    if (dtype != DT_F32 && use256 && fits32 && g.N % G2_BN == 0 && g.K % 64 == 0) {
+    if (dtype != DT_F32 && use256 && fits32 && g.N % G2_BN == 0 && (g.K / g.ksplit) % 64 == 0) {
         if (dtype == DT_F16) { SPT_GEMM256_CASES(true) }
         else { SPT_GEMM256_CASES(false) }
     }

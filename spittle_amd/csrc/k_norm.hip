@@ -69,6 +69,77 @@ template <> __device__ __forceinline__ void store4<f16>(f16* p, float a, float b
     *(h4*)p = h4{(f16)a, (f16)b, (f16)c, (f16)d};
 }
 
+// LayerNorm with the pending split-K product of a residual GEMM folded in first
+template <typename T, int NV>
+__global__ __launch_bounds__(256) void ln_pend_kernel(float* __restrict__ x, int M, int d, const float* __restrict__ slab,
+                                                      int ks, int64_t sst, const float* __restrict__ pbias, float alpha,
+                                                      const float* __restrict__ w, const float* __restrict__ bb,
+                                                      T* __restrict__ y, int write_x) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const int n4 = d >> 2;
+    float4* xr = (float4*)(x + (size_t)row * d);
+    float4 v[NV];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int idx = lane + 64 * i;
+        if (idx < n4) {
+            float4 p = *(const float4*)(slab + (size_t)row * d + 4 * idx);
+            for (int q = 1; q < ks; ++q) {
+                const float4 u = *(const float4*)(slab + q * sst + (size_t)row * d + 4 * idx);
+                p.x += u.x; p.y += u.y; p.z += u.z; p.w += u.w;
+            }
+            const float4 pb = ((const float4*)pbias)[idx], x0 = xr[idx];
+            v[i] = make_float4(x0.x + alpha * (p.x + pb.x), x0.y + alpha * (p.y + pb.y), x0.z + alpha * (p.z + pb.z),
+                               x0.w + alpha * (p.w + pb.w));
+            if (write_x) xr[idx] = v[i];
+            s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+        } else {
+            v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+    const float mean = wave_sum(s) / (float)d;
+    float s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int idx = lane + 64 * i;
+        if (idx < n4) {
+            const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, e = v[i].w - mean;
+            s2 += (a * a + b * b) + (c * c + e * e);
+        }
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(s2) / (float)d + 1e-5f);
+    const float4* w4 = (const float4*)w;
+    const float4* b4 = (const float4*)bb;
+    T* yr = y + (size_t)row * d;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int idx = lane + 64 * i;
+        if (idx < n4) {
+            const float4 g = w4[idx], o = b4[idx];
+            store4<T>(yr + 4 * idx, (v[i].x - mean) * rstd * g.x + o.x, (v[i].y - mean) * rstd * g.y + o.y,
+                      (v[i].z - mean) * rstd * g.z + o.z, (v[i].w - mean) * rstd * g.w + o.w);
+        }
+    }
+}
+
+template <typename T>
+void ln_pend_dispatch(float* x, int M, int d, const float* slab, int ks, int64_t sst, const float* pb, float alpha,
+                      const float* w, const float* b, T* y, int wx, hipStream_t st) {
+    dim3 grid(cdiv(M, 4));
+    switch (cdiv(d, 256)) {
+        case 1: hipLaunchKernelGGL((ln_pend_kernel<T, 1>), grid, dim3(256), 0, st, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx); break;
+        case 2: hipLaunchKernelGGL((ln_pend_kernel<T, 2>), grid, dim3(256), 0, st, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx); break;
+        case 3: hipLaunchKernelGGL((ln_pend_kernel<T, 3>), grid, dim3(256), 0, st, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx); break;
+        case 4: hipLaunchKernelGGL((ln_pend_kernel<T, 4>), grid, dim3(256), 0, st, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx); break;
+        case 5: hipLaunchKernelGGL((ln_pend_kernel<T, 5>), grid, dim3(256), 0, st, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx); break;
+        case 6: hipLaunchKernelGGL((ln_pend_kernel<T, 6>), grid, dim3(256), 0, st, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx); break;
+        default: throw std::runtime_error("layernorm_pend: d too large");
+    }
+}
+
 template <typename T>
 void ln_dispatch(const float* x, int M, int d, const float* w, const float* b, T* y, hipStream_t st) {
     dim3 grid(cdiv(M, 4));
@@ -97,6 +168,16 @@ void layernorm(int dtype, const float* x, int M, int d, const float* w, const fl
     if (dtype == DT_BF16) ln_dispatch<bf16>(x, M, d, w, b, (bf16*)y, st);
     else if (dtype == DT_F16) ln_dispatch<f16>(x, M, d, w, b, (f16*)y, st);
     else ln_dispatch<float>(x, M, d, w, b, (float*)y, st);
+}
+
+void layernorm_pend(int dtype, float* x, int M, int d, const float* slab, int ks, int64_t slab_stride,
+                    const float* pbias, float alpha, const float* w, const float* b, void* y, bool write_x,
+                    hipStream_t st) {
+    if (d % 4) throw std::runtime_error("layernorm_pend: d % 4");
+    if (dtype == DT_BF16) ln_pend_dispatch<bf16>(x, M, d, slab, ks, slab_stride, pbias, alpha, w, b, (bf16*)y, write_x, st);
+    else if (dtype == DT_F16) ln_pend_dispatch<f16>(x, M, d, slab, ks, slab_stride, pbias, alpha, w, b, (f16*)y, write_x, st);
+    else ln_pend_dispatch<float>(x, M, d, slab, ks, slab_stride, pbias, alpha, w, b, (float*)y, write_x, st);
+    SPT_LAUNCH_CHECK();
 }
 
 void to_f32(int dtype, const void* src, float* dst, int64_t n, hipStream_t st) {

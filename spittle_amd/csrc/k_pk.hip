@@ -12,6 +12,7 @@
 #include "pk_kernels.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace spt {
 
@@ -21,9 +22,6 @@ inline int grid_of(int64_t n, int tpb = 256) {
     int64_t g = (n + tpb - 1) / tpb;
     return (int)(g < 16384 ? (g > 0 ? g : 1) : 16384);
 }
-
-template <typename T> __device__ __forceinline__ T* tp(void* p) { return (T*)p; }
-template <typename T> __device__ __forceinline__ const T* tp(const void* p) { return (const T*)p; }
 
 // ---------------------------------------------------------------- front end
 __global__ __launch_bounds__(256) void frames_kernel(const float* __restrict__ pcm, int64_t stride,
@@ -96,50 +94,55 @@ __global__ __launch_bounds__(256) void mel_norm_kernel(float* __restrict__ mel, 
 }
 
 // ---------------------------------------------------------------- subsampling
+// one workgroup per output frame (t, b), a thread per channel (coalesced channel-last stores);
+// the three input frames it reads are staged in LDS
 template <typename T>
-__global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ mel, const int* __restrict__ lens,
-                                                    int B, int Tp, int F, const float* __restrict__ w,
-                                                    const float* __restrict__ bias, int C, T* __restrict__ y, int T1p,
-                                                    int F1) {
-    const int64_t total = (int64_t)B * T1p * F1 * C;
-    for (int64_t idx = blockIdx.x * 256ll + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
-        const int c = (int)(idx % C);
-        int64_t q = idx / C;
-        const int f = (int)(q % F1);
-        q /= F1;
-        const int t = (int)(q % T1p);
-        const int b = (int)(q / T1p);
-        const int Tb = min(lens[b * 4], Tp);
-        float acc = bias[c];
+__global__ __launch_bounds__(1024) void conv0_kernel(const float* __restrict__ mel, const int* __restrict__ lens,
+                                                     int Tp, int F, const float* __restrict__ w,
+                                                     const float* __restrict__ bias, int C, T* __restrict__ y, int T1p,
+                                                     int F1) {
+    extern __shared__ float rows[];  // [3][F]
+    const int t = blockIdx.x, b = blockIdx.y, c = threadIdx.x;
+    const int Tb = min(lens[b * 4], Tp);
+    for (int i = threadIdx.x; i < 3 * F; i += blockDim.x) {
+        const int tt = 2 * t - 1 + i / F;
+        rows[i] = (tt >= 0 && tt < Tb) ? mel[((size_t)b * Tp + tt) * F + i % F] : 0.0f;
+    }
+    __syncthreads();
+    float wc[9];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const int tt = 2 * t - 1 + i;
-            if (tt < 0 || tt >= Tb) continue;
+    for (int i = 0; i < 9; ++i) wc[i] = w[c * 9 + i];
+    const float bc = bias[c];
+    T* out = y + ((size_t)b * T1p + t) * F1 * C + c;
+    for (int f = 0; f < F1; ++f) {
+        float acc = bc;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
                 const int ff = 2 * f - 1 + j;
-                if (ff >= 0 && ff < F) acc += w[c * 9 + i * 3 + j] * mel[((size_t)b * Tp + tt) * F + ff];
+                if (ff >= 0 && ff < F) acc += wc[i * 3 + j] * rows[i * F + ff];
             }
-        }
-        y[idx] = from_f<T>(fmaxf(acc, 0.0f));
+        out[(size_t)f * C] = from_f<T>(fmaxf(acc, 0.0f));
     }
 }
 
+// depthwise 3x3 stride 2: one workgroup per output frame (t, b), a thread per channel
 template <typename T>
-__global__ __launch_bounds__(256) void dwconv_kernel(const T* __restrict__ x, const int* __restrict__ lens, int stage,
-                                                     int B, int Tip, int Fi, const float* __restrict__ w,
-                                                     const float* __restrict__ bias, int C, T* __restrict__ y, int Top,
-                                                     int Fo) {
-    const int64_t total = (int64_t)B * Top * Fo * C;
-    for (int64_t idx = blockIdx.x * 256ll + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
-        const int c = (int)(idx % C);
-        int64_t q = idx / C;
-        const int f = (int)(q % Fo);
-        q /= Fo;
-        const int t = (int)(q % Top);
-        const int b = (int)(q / Top);
-        const int Tb = min(lens[b * 4 + stage], Tip);
-        float acc = bias[c];
+__global__ __launch_bounds__(1024) void dwconv_kernel(const T* __restrict__ x, const int* __restrict__ lens, int stage,
+                                                      int Tip, int Fi, const float* __restrict__ w,
+                                                      const float* __restrict__ bias, int C, T* __restrict__ y, int Top,
+                                                      int Fo) {
+    const int t = blockIdx.x, b = blockIdx.y, c = threadIdx.x;
+    const int Tb = min(lens[b * 4 + stage], Tip);
+    float wc[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) wc[i] = w[c * 9 + i];
+    const float bc = bias[c];
+    const T* in = x + (size_t)b * Tip * Fi * C + c;
+    T* out = y + ((size_t)b * Top + t) * Fo * C + c;
+    for (int f = 0; f < Fo; ++f) {
+        float acc = bc;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             const int tt = 2 * t - 1 + i;
@@ -147,10 +150,10 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const T* __restrict__ x, co
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
                 const int ff = 2 * f - 1 + j;
-                if (ff >= 0 && ff < Fi) acc += w[c * 9 + i * 3 + j] * to_f<T>(x[(((size_t)b * Tip + tt) * Fi + ff) * C + c]);
+                if (ff >= 0 && ff < Fi) acc += wc[i * 3 + j] * to_f<T>(in[((size_t)tt * Fi + ff) * C]);
             }
         }
-        y[idx] = from_f<T>(acc);
+        out[(size_t)f * C] = from_f<T>(acc);
     }
 }
 
@@ -256,31 +259,207 @@ __global__ __launch_bounds__(64) void rel_attn_kernel(const T* __restrict__ qkv,
     }
 }
 
+// MFMA variant (fp16, head dim 64 or 128): one wave per 32 queries of one (head, utterance),
+// flash-style over 32-key tiles.  Per tile, with v_mfma_f32_32x32x16_f16:
+//   S^T  = K . (q + u)^T                 (keys x queries; a lane owns one query column)
+//   G^T  = P[r0 .. r0 + 63] . (q + v)^T  (the 63 relative positions the tile's (i, j) pairs use,
+//                                         r0 = Tp - 1 + j0 - i0 - 31)
+//   bd(i, j) = G^T[j - i + 31][i]        (NeMo's rel_shift: a per-lane row skew, through LDS)
+//   online softmax of (S^T + bd) / sqrt(dk); O^T += V^T . P^T, V^T read from LDS with
+//   ds_read_b64_tr_b16 (the accumulator layout of P^T is directly the B operand).
+template <int DK>
+__global__ __launch_bounds__(64) void rel_attn_mfma_kernel(const f16* __restrict__ qkv, const f16* __restrict__ p,
+                                                           int ldp, const float* __restrict__ pu,
+                                                           const float* __restrict__ pv, const int* __restrict__ lens,
+                                                           int Tp, int H, f16* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) char smem[32 * DK * 2 + 64 * 32 * 4];  // V tile [32][DK] | G [64][32]
+    SPT_LDS char* lv = (SPT_LDS char*)smem;
+    SPT_LDS float* G = (SPT_LDS float*)(smem + 32 * DK * 2);
+    const int lane = threadIdx.x, l32 = lane & 31, hf = lane >> 5;
+    const int i0 = blockIdx.x * 32, h = blockIdx.y, b = blockIdx.z;
+    const int d = H * DK, ld = 3 * d;
+    const int T3 = lens[b * 4 + 3];
+    f16* obase = out + (size_t)b * Tp * d + h * DK;
+    if (i0 >= T3) {  // padded frames: finite zeros
+        for (int e = lane; e < 32 * DK; e += 64) {
+            const int i = i0 + e / DK;
+            if (i < Tp) obase[(size_t)i * d + e % DK] = (f16)0.0f;
+        }
+        return;
+    }
+    const f16* base = qkv + (size_t)b * Tp * ld;
+    constexpr int NS = DK / 16;
+    f16x8 qu[NS], qv[NS];
+    {
+        const int qi = min(i0 + l32, Tp - 1);
+        const f16* qp = base + (size_t)qi * ld + h * DK + 8 * hf;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const f16x8 raw = *(const f16x8*)(qp + 16 * s);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int c = h * DK + 16 * s + 8 * hf + e;
+                qu[s][e] = (f16)((float)raw[e] + pu[c]);
+                qv[s][e] = (f16)((float)raw[e] + pv[c]);
+            }
+        }
+    }
+    const float sl2 = 1.4426950408889634f / sqrtf((float)DK);
+    float m_run = -INFINITY, l_run = 0.0f;
+    f32x16 o[DK / 32];
+#pragma unroll
+    for (int t = 0; t < DK / 32; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t][r] = 0.0f;
+    const int ntile = cdiv(T3, 32);
+    const int g4 = lane >> 4, i16 = lane & 15;
+    for (int jt = 0; jt < ntile; ++jt) {
+        const int j0 = jt * 32;
+        // V tile (32 keys x DK) -> registers; written to LDS after the score products
+        typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+        u32x4 vreg[DK / 16];
+#pragma unroll
+        for (int u = 0; u < DK / 16; ++u) {
+            const int c = lane + 64 * u;
+            const int key = min(j0 + c / (DK / 8), Tp - 1);
+            vreg[u] = *(const u32x4*)(base + (size_t)key * ld + 2 * d + h * DK + 8 * (c % (DK / 8)));
+        }
+        // S^T = K . QU^T
+        f32x16 sc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sc[r] = 0.0f;
+        {
+            const f16* kp = base + (size_t)min(j0 + l32, Tp - 1) * ld + d + h * DK + 8 * hf;
+#pragma unroll
+            for (int s = 0; s < NS; ++s)
+                sc = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const f16x8*)(kp + 16 * s), qu[s], sc, 0, 0, 0);
+        }
+        // G^T = P[r0 ..] . QV^T (two 32-row halves)
+        f32x16 g0, g1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { g0[r] = 0.0f; g1[r] = 0.0f; }
+        {
+            const int r0 = (Tp - 1) + j0 - i0 - 31;
+            const int pr0 = min(max(r0 + l32, 0), 2 * Tp - 2), pr1 = min(max(r0 + 32 + l32, 0), 2 * Tp - 2);
+            const f16* p0 = p + (size_t)pr0 * ldp + h * DK + 8 * hf;
+            const f16* p1 = p + (size_t)pr1 * ldp + h * DK + 8 * hf;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                g0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const f16x8*)(p0 + 16 * s), qv[s], g0, 0, 0, 0);
+                g1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const f16x8*)(p1 + 16 * s), qv[s], g1, 0, 0, 0);
+            }
+        }
+        __syncthreads();  // the previous tile's LDS reads are done
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * hf;
+            G[row * 32 + l32] = g0[r];
+            G[(row + 32) * 32 + l32] = g1[r];
+        }
+#pragma unroll
+        for (int u = 0; u < DK / 16; ++u) *(SPT_LDS u32x4*)(lv + (lane + 64 * u) * 16) = vreg[u];
+        __syncthreads();
+        float mloc = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int jl = (r & 3) + 8 * (r >> 2) + 4 * hf;
+            float v = (sc[r] + G[(jl - l32 + 31) * 32 + l32]) * sl2;
+            if (j0 + jl >= T3) v = -INFINITY;
+            sc[r] = v;
+            mloc = fmaxf(mloc, v);
+        }
+        mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+        const float m_new = fmaxf(m_run, mloc);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        m_run = m_new;
+        float ls = 0.0f;
+        f16x8 pf[2];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float e = __builtin_amdgcn_exp2f(sc[r] - m_new);
+            ls += e;
+            pf[r >> 3][r & 7] = (f16)e;
+        }
+        l_run = l_run * alpha + ls;
+#pragma unroll
+        for (int t = 0; t < DK / 32; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+        // O^T += V^T . P^T
+#pragma unroll
+        for (int dt = 0; dt < DK / 32; ++dt) {
+            const int col = 32 * dt + 16 * (g4 & 1) + 4 * (i16 & 3);
+#pragma unroll
+            for (int sp = 0; sp < 2; ++sp) {
+                const int key0 = 16 * sp + 4 * hf + (i16 >> 2);
+                const bf16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SPT_LDS bf16x4v*)(lv + key0 * DK * 2 + col * 2));
+                const bf16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SPT_LDS bf16x4v*)(lv + (key0 + 8) * DK * 2 + col * 2));
+                bf16x8 va;
+                va[0] = lo[0]; va[1] = lo[1]; va[2] = lo[2]; va[3] = lo[3];
+                va[4] = hi[0]; va[5] = hi[1]; va[6] = hi[2]; va[7] = hi[3];
+                o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, va), pf[sp], o[dt], 0, 0, 0);
+            }
+        }
+    }
+    const float inv = 1.0f / (l_run + __shfl_xor(l_run, 32, 64));
+    const int i = i0 + l32;
+    if (i < Tp) {
+        f16* orow = obase + (size_t)i * d;
+        const bool ok = i < T3;
+#pragma unroll
+        for (int dt = 0; dt < DK / 32; ++dt)
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg) {
+                const int dd = 32 * dt + 8 * gg + 4 * hf;
+                typedef __attribute__((ext_vector_type(4))) _Float16 h4;
+                const h4 v = ok ? h4{(f16)(o[dt][4 * gg] * inv), (f16)(o[dt][4 * gg + 1] * inv), (f16)(o[dt][4 * gg + 2] * inv),
+                                     (f16)(o[dt][4 * gg + 3] * inv)}
+                                : h4{(f16)0.0f, (f16)0.0f, (f16)0.0f, (f16)0.0f};
+                *(h4*)(orow + dd) = v;
+            }
+    }
+}
+
 // ---------------------------------------------------------------- convolution module
-template <typename T>
-__global__ __launch_bounds__(256) void conv_module_kernel(const T* __restrict__ a, const int* __restrict__ lens, int B,
-                                                          int Tp, int d, int K, const float* __restrict__ dw_w,
+// a workgroup per 16 output frames of one utterance, a thread per channel: the GLU of the 16 + K - 1
+// frames it needs is computed once into registers (not once per tap), then the depthwise taps,
+// BatchNorm and Swish
+constexpr int CM_TT = 16;
+template <typename T, int K>
+__global__ __launch_bounds__(256) void conv_module_kernel(const T* __restrict__ a, const int* __restrict__ lens, int Tp,
+                                                          int d, const float* __restrict__ dw_w,
                                                           const float* __restrict__ dw_b, const float* __restrict__ bn_g,
                                                           const float* __restrict__ bn_b, const float* __restrict__ bn_m,
                                                           const float* __restrict__ bn_v, T* __restrict__ out) {
-    const int64_t total = (int64_t)B * Tp * d;
-    for (int64_t idx = blockIdx.x * 256ll + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
-        const int i = (int)(idx % d);
-        const int64_t row = idx / d;
-        const int t = (int)(row % Tp), b = (int)(row / Tp);
-        const int T3 = lens[b * 4 + 3];
-        if (t >= T3) { out[idx] = from_f<T>(0.0f); continue; }
-        const float bs = bn_g[i] / sqrtf(bn_v[i] + 1e-5f), bt = bn_b[i] - bn_m[i] * bs;
-        float acc = dw_b[i];
-        for (int j = 0; j < K; ++j) {
-            const int tt = t - K / 2 + j;
-            if (tt < 0 || tt >= T3) continue;
-            const T* ar = a + ((size_t)b * Tp + tt) * 2 * d;
-            const float g = to_f<T>(ar[i]) * (1.0f / (1.0f + expf(-to_f<T>(ar[d + i]))));  // GLU
-            acc += dw_w[i * K + j] * g;
+    const int t0 = blockIdx.x * CM_TT, b = blockIdx.y;
+    const int T3 = lens[b * 4 + 3];
+    const T* ab = a + (size_t)b * Tp * 2 * d;
+    T* ob = out + (size_t)b * Tp * d;
+    for (int i = threadIdx.x; i < d; i += 256) {
+        float g[CM_TT + K - 1];
+#pragma unroll
+        for (int f = 0; f < CM_TT + K - 1; ++f) {
+            const int tt = t0 - K / 2 + f;
+            g[f] = 0.0f;
+            if (tt >= 0 && tt < T3) {
+                const float x = to_f<T>(ab[(size_t)tt * 2 * d + i]), gate = to_f<T>(ab[(size_t)tt * 2 * d + d + i]);
+                g[f] = x * (1.0f / (1.0f + expf(-gate)));  // GLU
+            }
         }
-        const float z = acc * bs + bt;
-        out[idx] = from_f<T>(z / (1.0f + expf(-z)));  // Swish
+        float wk[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) wk[j] = dw_w[i * K + j];
+        const float bs = bn_g[i] / sqrtf(bn_v[i] + 1e-5f), bt = bn_b[i] - bn_m[i] * bs, bias = dw_b[i];
+#pragma unroll
+        for (int f = 0; f < CM_TT; ++f) {
+            const int t = t0 + f;
+            if (t >= Tp) break;
+            float acc = bias;
+#pragma unroll
+            for (int j = 0; j < K; ++j) acc += wk[j] * g[f + j];
+            const float z = acc * bs + bt;
+            ob[(size_t)t * d + i] = from_f<T>(t < T3 ? z / (1.0f + expf(-z)) : 0.0f);  // Swish
+        }
     }
 }
 
@@ -310,106 +489,214 @@ __global__ void place_subperm_kernel(const float* __restrict__ s, int N, int C, 
 }
 
 // ---------------------------------------------------------------- TDT greedy step
-// y[b][n] partial over a K slab: lanes over n (W^T rows are contiguous in n), the slab's x
-// rows for every utterance staged in LDS as [k][BM] (one ds_read_b128 feeds four rows).
-template <int XM, int BM>
-__global__ __launch_bounds__(256) void gemv_t_kernel(PkGemvArgs a) {
-    extern __shared__ float xs[];  // [KC][BM]
-    const int KC = a.K / a.ksplit, s = blockIdx.y, k0 = s * KC;
-    const int P = a.P, B = a.B;
-    for (int idx = threadIdx.x; idx < KC * BM; idx += 256) {
-        const int k = idx % KC, b = idx / KC, kk = k0 + k;
-        float v = 0.0f;
-        if (b < B) {
-            if constexpr (XM == PKX_LSTM0) {
-                v = kk < P ? a.emb[(size_t)a.st[b].tok * P + kk] : a.h0[(size_t)b * P + kk - P];
-            } else if constexpr (XM == PKX_LSTM1) {
-                v = kk < P ? a.h0[(size_t)b * P + kk] : a.h1[(size_t)b * P + kk - P];
-            } else if constexpr (XM == PKX_PRED) {
-                v = a.h1[(size_t)b * P + kk];
+// One kernel per stage of a decode step, 512 threads = 8 K-groups.  A workgroup owns DO outputs;
+// a lane loads a float4 of W^T (4 consecutive outputs of one k row; a wave-load covers
+// 256 / DO k rows x DO outputs = 1 KB), the x rows of up to 16 utterances sit in LDS as [k][16]
+// (broadcast float4 reads), so each lane carries 4 outputs x 16 rows of accumulators.  Every
+// lane's weight loads for its K-group slice are issued together (8 per batch), the k rows of a
+// wave fold by xor shuffles and the 8 K-groups through LDS; the epilogue is the stage's own: the
+// LSTM cell (gate-interleaved W^T: a workgroup's 16 outputs are the i, f, g, o rows of 4 units),
+// the prediction projection, or the joint's per-workgroup top-2 + duration logits.
+constexpr int DG = 8, DR = 8;   // K-groups, rows per pass (accumulators: 4 outputs x 8 rows per lane)
+constexpr int XP = 12;          // LDS row stride of the staged x (8 rows + 4 pad: 16-byte rows, <= 2-way conflicts)
+
+__device__ __forceinline__ float sig_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// workgroup barrier for LDS hand-offs only: __syncthreads() is a release/acquire fence that
+// drains vmcnt, which would stall the in-flight weight loads held in registers across it
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int MODE, int DO, int NWM, int SE>
+__global__ __launch_bounds__(512) void dec_kernel(PkDecArgs a) {
+    constexpr int OQ = DO / 4;       // output quads per k row
+    constexpr int KS = 64 / OQ;      // k rows per wave-load
+    constexpr int NU = DO / 4;       // LSTM: units per workgroup
+    // NWM: wave-loads per lane held in registers (host checks K / 8 / KS <= NWM);
+    // SE: staged float4 per thread (host checks K / 4 * 16 <= 512 * SE)
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* xs = sm;                    // [K][XP]
+    float* red = sm + (size_t)a.K * XP;  // [DG][DR][DO]
+    const int tid = threadIdx.x, lane = tid & 63, kg = tid >> 6;
+    const int oq = lane % OQ, kq = lane / OQ;
+    const int n0 = blockIdx.x * DO;
+    const int KT = a.K / DG, kb = kg * KT, NW = KT / KS;
+    const int P = a.P;
+    // every operand of the stage is issued before anything waits: this lane's whole slice of the
+    // blocked W^T ([N / DO][K][DO]: a workgroup's slice is contiguous, a wave-load is 1 KB), then
+    // per row group the staged x rows and the epilogue's operands -- one memory round trip
+    float4 w[NWM];
+    {
+        const float* wcol = a.WT + (size_t)blockIdx.x * a.K * DO + (size_t)(kb + kq) * DO + 4 * oq;
+#pragma unroll
+        for (int u = 0; u < NWM; ++u)
+            w[u] = u < NW ? *(const float4*)(wcol + (size_t)u * KS * DO) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    for (int rg = 0; rg < a.B; rg += DR) {
+        const int R = min(DR, a.B - rg);
+        const int K4 = a.K / 4, NE = K4 * DR;
+        float4 v[SE];
+#pragma unroll
+        for (int u = 0; u < SE; ++u) {
+            const int idx = min(tid + 512 * u, NE - 1);
+            const int k = 4 * (idx / DR), r = idx % DR, b = rg + min(r, R - 1);
+            if constexpr (MODE == PKD_LSTM) {
+                const float* lo = a.xin + (size_t)b * P + k;
+                const float* hi = a.h_in + (size_t)b * P + (k - P);
+                v[u] = *(const float4*)(k < P ? lo : hi);
+            } else if constexpr (MODE == PKD_PRED) {
+                v[u] = *(const float4*)(a.xin + (size_t)b * P + k);
             } else {
-                const PkState sb = a.st[b];
-                float g;
-                if (sb.upd) {
-                    g = a.pred_b[kk];
-                    for (int q = 0; q < a.pred_split; ++q) g += a.pred_part[((size_t)q * B + b) * a.pred_Npad + kk];
-                    if (blockIdx.x == 0) a.gp[(size_t)b * P + kk] = g;
-                } else {
-                    g = a.gp[(size_t)b * P + kk];
-                }
-                const int t = min(sb.t, a.T3p - 1);
-                v = fmaxf(a.fe[((size_t)b * a.T3p + t) * P + kk] + g, 0.0f);  // ReLU(enc + pred)
+                const float4 e = *(const float4*)(a.fe + (size_t)b * P + k);  // the row's current frame
+                const float4 g = *(const float4*)(a.gp + (size_t)b * P + k);
+                v[u] = make_float4(fmaxf(e.x + g.x, 0.f), fmaxf(e.y + g.y, 0.f), fmaxf(e.z + g.z, 0.f),
+                                   fmaxf(e.w + g.w, 0.f));  // ReLU(enc + pred)
             }
         }
-        xs[k * BM + b] = v;
-    }
-    __syncthreads();
-    const int n = blockIdx.x * 256 + threadIdx.x;
-    float acc[BM];
+        // epilogue operands
+        float eb[4] = {0.f, 0.f, 0.f, 0.f}, eh = 0.f, ec = 0.f;
+        int eupd = 0;
+        if constexpr (MODE == PKD_LSTM) {
+            if (tid < DR * NU) {
+                const int jj = tid % NU, r = min(tid / NU, R - 1), j = blockIdx.x * NU + jj;
+                const size_t o = (size_t)(rg + r) * P + j;
 #pragma unroll
-    for (int b = 0; b < BM; ++b) acc[b] = 0.0f;
-    const float* w = a.WT + (size_t)k0 * a.Npad + n;
-#pragma unroll 4
-    for (int k = 0; k < KC; ++k) {
-        const float wv = w[(size_t)k * a.Npad];
+                for (int q = 0; q < 4; ++q) eb[q] = a.b0[q * P + j] + a.b1[q * P + j];
+                eh = a.h_in[o];
+                ec = a.c_in[o];
+                eupd = a.st[rg + r].upd;
+            }
+        } else if constexpr (MODE == PKD_PRED) {
+            if (tid < DR * DO) {
+                const int o = tid % DO, r = min(tid / DO, R - 1), n = min(n0 + o, a.N - 1);
+                eb[0] = a.b0[n];
+                eupd = a.st[rg + r].upd;
+            }
+        } else {
+            eb[0] = a.b0[min(n0 + (lane % DO), a.N - 1)];
+        }
+        lds_sync();  // the previous row group's LDS reads are done
 #pragma unroll
-        for (int b = 0; b < BM; b += 4) {
-            const float4 x4 = *(const float4*)&xs[k * BM + b];
-            acc[b] += wv * x4.x;
-            acc[b + 1] += wv * x4.y;
-            acc[b + 2] += wv * x4.z;
-            acc[b + 3] += wv * x4.w;
+        for (int u = 0; u < SE; ++u) {
+            const int idx = tid + 512 * u;
+            if (idx < NE) {
+                const int k = 4 * (idx / DR), r = idx % DR;
+                const bool ok = r < R;
+                xs[(k + 0) * XP + r] = ok ? v[u].x : 0.f;
+                xs[(k + 1) * XP + r] = ok ? v[u].y : 0.f;
+                xs[(k + 2) * XP + r] = ok ? v[u].z : 0.f;
+                xs[(k + 3) * XP + r] = ok ? v[u].w : 0.f;
+            }
+        }
+        lds_sync();
+        float acc[4][DR];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int r = 0; r < DR; ++r) acc[q][r] = 0.0f;
+#pragma unroll
+        for (int u = 0; u < NWM; ++u) {
+            if (u < NW) {
+                const float4* xr = (const float4*)(xs + (kb + kq + u * KS) * XP);
+#pragma unroll
+                for (int r4 = 0; r4 < DR / 4; ++r4) {
+                    const float4 x = xr[r4];
+                    const float xv[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        acc[0][4 * r4 + e] += w[u].x * xv[e];
+                        acc[1][4 * r4 + e] += w[u].y * xv[e];
+                        acc[2][4 * r4 + e] += w[u].z * xv[e];
+                        acc[3][4 * r4 + e] += w[u].w * xv[e];
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int r = 0; r < DR; ++r) {
+                float t = acc[q][r];
+#pragma unroll
+                for (int m = OQ; m < 64; m <<= 1) t += __shfl_xor(t, m, 64);
+                acc[q][r] = t;
+            }
+        if (kq == 0) {
+#pragma unroll
+            for (int r = 0; r < DR; ++r)
+                *(float4*)(red + ((size_t)kg * DR + r) * DO + 4 * oq) = make_float4(acc[0][r], acc[1][r], acc[2][r], acc[3][r]);
+        }
+        lds_sync();
+        for (int e = tid; e < DR * DO; e += 512) {  // fold the K-groups into slot 0
+            const int r = e / DO, o = e % DO;
+            float t = 0.0f;
+#pragma unroll
+            for (int g = 0; g < DG; ++g) t += red[((size_t)g * DR + r) * DO + o];
+            red[(size_t)r * DO + o] = t;
+        }
+        lds_sync();
+        if constexpr (MODE == PKD_LSTM) {
+            if (tid < DR * NU) {
+                const int jj = tid % NU, r = tid / NU;
+                if (r < R) {
+                    const int j = blockIdx.x * NU + jj;
+                    float g[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) g[q] = eb[q] + red[(size_t)r * DO + q * NU + jj];
+                    float h = eh, c = ec;
+                    if (eupd) {
+                        c = sig_(g[1]) * c + sig_(g[0]) * tanhf(g[2]);
+                        h = sig_(g[3]) * tanhf(c);
+                    }
+                    const size_t o = (size_t)(rg + r) * P + j;
+                    a.h_out[o] = h;
+                    a.c_out[o] = c;
+                }
+            }
+        } else if constexpr (MODE == PKD_PRED) {
+            if (tid < DR * DO) {
+                const int r = tid / DO, o = tid % DO, n = n0 + o;
+                if (r < R && n < a.N && eupd) a.gp[(size_t)(rg + r) * P + n] = eb[0] + red[(size_t)r * DO + o];
+            }
+        } else {
+            // joint logits of this workgroup's DO outputs: per row (one wave per row) the token
+            // top-2 (first index on ties) and the duration logits
+            for (int r = kg; r < R; r += DG) {
+                const int b = rg + r, n = n0 + lane;
+                const float val = (lane < DO && n < a.N) ? eb[0] + red[(size_t)r * DO + lane] : -INFINITY;
+                if (lane < DO && n > a.V && n < a.N) a.dur[(size_t)b * a.n_dur + (n - a.V - 1)] = val;
+                const float vt = n <= a.V ? val : -INFINITY;
+                const float v1 = wave_max(vt);
+                int i1 = (vt == v1 && lane < DO) ? n : 0x7fffffff;
+#pragma unroll
+                for (int m = 32; m > 0; m >>= 1) i1 = min(i1, __shfl_xor(i1, m, 64));
+                const float v2 = wave_max(n == i1 ? -INFINITY : vt);
+                if (lane == 0) a.part[(size_t)b * a.n_tiles + blockIdx.x] = make_float4(v1, __int_as_float(i1), v2, 0.0f);
+            }
         }
     }
-#pragma unroll
-    for (int b = 0; b < BM; ++b)
-        if (b < B) a.part[((size_t)s * B + b) * a.Npad + n] = acc[b];
 }
 
-__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
-
-__global__ __launch_bounds__(256) void lstm_cell_kernel(const float* __restrict__ part, int ksplit, int Npad,
-                                                        const float* __restrict__ b_ih, const float* __restrict__ b_hh,
-                                                        int B, int P, const PkState* __restrict__ st,
-                                                        float* __restrict__ h, float* __restrict__ c) {
-    const int idx = blockIdx.x * 256 + threadIdx.x;
-    if (idx >= B * P) return;
-    const int b = idx / P, j = idx - b * P;
-    if (!st[b].upd) return;
-    float g[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int n = q * P + j;
-        float v = b_ih[n] + b_hh[n];
-        for (int s = 0; s < ksplit; ++s) v += part[((size_t)s * B + b) * Npad + n];
-        g[q] = v;
-    }
-    const float ig = sigm(g[0]), fg = sigm(g[1]), gg = tanhf(g[2]), og = sigm(g[3]);
-    const float cn = fg * c[idx] + ig * gg;
-    c[idx] = cn;
-    h[idx] = og * tanhf(cn);
-}
-
-// one workgroup per utterance: joint logits (slab sums + bias), token top-2 and duration
-// argmax (first maximum wins, as the oracle's strict >), then the TDT bookkeeping
+// one workgroup per utterance: merge the joint's per-workgroup top-2 partials and the duration
+// logits (first maximum wins, as the oracle's strict >), the TDT bookkeeping, and the next
+// step's operand rows: the emitted token's embedding (LSTM layer 0 input) and the encoder
+// projection of the row's new frame
 __global__ __launch_bounds__(256) void joint_fin_kernel(PkFinArgs a) {
-    __shared__ float s1[256], s2[256], sd[256];
-    __shared__ int i1[256], id_[256];
+    __shared__ float s1[256], s2[256];
+    __shared__ int i1[256];
+    __shared__ PkState ns;
     const int b = blockIdx.x, tid = threadIdx.x;
     PkState* sb = a.st + b;
     if (sb->done) return;  // uniform
-    const int V = a.V, NO = V + 1 + a.n_dur;
-    float b1 = -INFINITY, b2 = -INFINITY, bdv = -INFINITY;
-    int t1 = 0x7fffffff, td = 0x7fffffff;
-    for (int n = tid; n < NO; n += 256) {
-        float v = a.bias[n];
-        for (int s = 0; s < a.ksplit; ++s) v += a.part[((size_t)s * a.B + b) * a.Npad + n];
-        if (n <= V) {
-            if (v > b1) { b2 = b1; b1 = v; t1 = n; }
-            else if (v > b2) b2 = v;
-        } else if (v > bdv) { bdv = v; td = n - V - 1; }
+    float b1 = -INFINITY, b2 = -INFINITY;
+    int t1 = 0x7fffffff;
+    for (int i = tid; i < a.n_tiles; i += 256) {
+        const float4 p = a.part[(size_t)b * a.n_tiles + i];
+        const int pi = __float_as_int(p.y);
+        const bool take = p.x > b1 || (p.x == b1 && pi < t1);
+        b2 = fmaxf(fmaxf(b2, p.z), take ? b1 : p.x);
+        if (take) { b1 = p.x; t1 = pi; }
     }
-    s1[tid] = b1; s2[tid] = b2; i1[tid] = t1; sd[tid] = bdv; id_[tid] = td;
+    s1[tid] = b1; s2[tid] = b2; i1[tid] = t1;
     __syncthreads();
     for (int o = 128; o > 0; o >>= 1) {
         if (tid < o) {
@@ -419,42 +706,67 @@ __global__ __launch_bounds__(256) void joint_fin_kernel(PkFinArgs a) {
             s1[tid] = take ? c1 : a1;
             i1[tid] = take ? ci : ai;
             s2[tid] = fmaxf(fmaxf(a2, c2), take ? a1 : c1);
-            const float e1 = sd[tid], e2 = sd[tid + o];
-            const int ei = id_[tid], ej = id_[tid + o];
-            if (e2 > e1 || (e2 == e1 && ej < ei)) { sd[tid] = e2; id_[tid] = ej; }
         }
         __syncthreads();
     }
-    if (tid != 0) return;
-    PkState s = *sb;
-    const int tk = i1[0];
-    int skip = id_[0];
-    if (tk != V) {
-        if (s.n_out < a.cap) {
-            const size_t o = (size_t)b * a.cap + s.n_out;
-            a.out_tok[o] = tk;
-            a.out_frame[o] = s.t;
-            a.out_t1[o] = s1[0];
-            a.out_t2[o] = s2[0];
+    if (tid == 0) {
+        PkState s = *sb;
+        const int V = a.V, tk = i1[0];
+        int skip = 0;
+        for (int k = 1; k < a.n_dur; ++k)
+            if (a.dur[(size_t)b * a.n_dur + k] > a.dur[(size_t)b * a.n_dur + skip]) skip = k;
+        if (tk != V) {
+            if (s.n_out < a.cap) {
+                const size_t o = (size_t)b * a.cap + s.n_out;
+                a.out_tok[o] = tk;
+                a.out_frame[o] = s.t;
+                a.out_t1[o] = s1[0];
+                a.out_t2[o] = s2[0];
+            }
+            s.n_out++;
+            s.upd = 1;
+            s.tok = tk;
+            s.at_t++;
+        } else {
+            s.upd = 0;
         }
-        s.n_out++;
-        s.upd = 1;
-        s.tok = tk;
-        s.at_t++;
-    } else {
-        s.upd = 0;
+        if (skip == 0 && (tk == V || s.at_t >= a.max_symbols)) skip = 1;
+        if (skip > 0) s.at_t = 0;
+        s.t += skip;
+        if (s.t >= a.lens[b * 4 + 3]) s.done = 1;
+        *sb = s;
+        ns = s;
     }
-    if (skip == 0 && (tk == V || s.at_t >= a.max_symbols)) skip = 1;
-    if (skip > 0) s.at_t = 0;
-    s.t += skip;
-    if (s.t >= a.lens[b * 4 + 3]) s.done = 1;
-    *sb = s;
+    __syncthreads();
+    const int P = a.P;
+    if (ns.upd)
+        for (int k = tid; k < P; k += 256) a.xemb[(size_t)b * P + k] = a.emb[(size_t)ns.tok * P + k];
+    const int t = min(ns.t, a.T3p - 1);
+    for (int k = tid; k < P; k += 256) a.fecur[(size_t)b * P + k] = a.fe[((size_t)b * a.T3p + t) * P + k];
 }
 
-__global__ void state_init_kernel(PkState* st, int B, int V, float* h, float* c, int n) {
+// rows start at t = 0 with the blank symbol pending: zero states, the blank's (zero) embedding,
+// frame 0's encoder projection
+__global__ void state_init_kernel(PkState* st, int B, int V, float* h, float* c, int n, float* xemb, float* fecur,
+                                  const float* fe, int T3p, int P) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i < B) st[i] = PkState{0, 0, 0, 0, 1, V};
     if (i < n) { h[i] = 0.0f; c[i] = 0.0f; }
+    if (i < B * P) {
+        const int b = i / P, k = i % P;
+        xemb[i] = 0.0f;
+        fecur[i] = fe[((size_t)b * T3p) * P + k];
+    }
+}
+
+__global__ void place_lstm_kernel(const float* __restrict__ s, int P, float* __restrict__ d, int row0) {
+    const int64_t total = (int64_t)4 * P * P;
+    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int n = (int)(i % (4 * P)), k = (int)(i / (4 * P));  // src [4P][P]: gate row n = q P + j
+        const int q = n / P, j = n % P;
+        // blocked [P / 4][2P][16] (kLstmDO = 16): workgroup j / 4 owns the i, f, g, o rows of 4 units
+        d[((size_t)(j / 4) * 2 * P + row0 + k) * 16 + q * 4 + (j % 4)] = s[(size_t)n * P + k];
+    }
 }
 
 }  // namespace
@@ -477,28 +789,31 @@ void pk_mel_norm(float* mel, const int* lens, int B, int Tp, int n_mels, hipStre
 
 void pk_conv0(int dtype, const float* mel, const int* lens, int B, int Tp, int F, const float* w, const float* bias,
               int C, void* y, int T1p, int F1, hipStream_t st) {
-    const int g = grid_of((int64_t)B * T1p * F1 * C);
+    if (C > 1024) throw std::runtime_error("pk_conv0: more than 1024 channels");
+    dim3 grid(T1p, B);
+    const size_t sm = (size_t)3 * F * 4;
     if (dtype == DT_F16)
-        hipLaunchKernelGGL(conv0_kernel<f16>, dim3(g), dim3(256), 0, st, mel, lens, B, Tp, F, w, bias, C, (f16*)y, T1p, F1);
+        hipLaunchKernelGGL(conv0_kernel<f16>, grid, dim3(C), sm, st, mel, lens, Tp, F, w, bias, C, (f16*)y, T1p, F1);
     else if (dtype == DT_BF16)
-        hipLaunchKernelGGL(conv0_kernel<bf16>, dim3(g), dim3(256), 0, st, mel, lens, B, Tp, F, w, bias, C, (bf16*)y, T1p, F1);
+        hipLaunchKernelGGL(conv0_kernel<bf16>, grid, dim3(C), sm, st, mel, lens, Tp, F, w, bias, C, (bf16*)y, T1p, F1);
     else
-        hipLaunchKernelGGL(conv0_kernel<float>, dim3(g), dim3(256), 0, st, mel, lens, B, Tp, F, w, bias, C, (float*)y, T1p, F1);
+        hipLaunchKernelGGL(conv0_kernel<float>, grid, dim3(C), sm, st, mel, lens, Tp, F, w, bias, C, (float*)y, T1p, F1);
     SPT_LAUNCH_CHECK();
 }
 
 void pk_dwconv(int dtype, const void* x, const int* lens, int stage, int B, int Tip, int Fi, const float* w,
                const float* bias, int C, void* y, int Top, int Fo, hipStream_t st) {
-    const int g = grid_of((int64_t)B * Top * Fo * C);
+    if (C > 1024) throw std::runtime_error("pk_dwconv: more than 1024 channels");
+    dim3 grid(Top, B);
     if (dtype == DT_F16)
-        hipLaunchKernelGGL(dwconv_kernel<f16>, dim3(g), dim3(256), 0, st, (const f16*)x, lens, stage, B, Tip, Fi, w, bias,
-                           C, (f16*)y, Top, Fo);
+        hipLaunchKernelGGL(dwconv_kernel<f16>, grid, dim3(C), 0, st, (const f16*)x, lens, stage, Tip, Fi, w, bias, C,
+                           (f16*)y, Top, Fo);
     else if (dtype == DT_BF16)
-        hipLaunchKernelGGL(dwconv_kernel<bf16>, dim3(g), dim3(256), 0, st, (const bf16*)x, lens, stage, B, Tip, Fi, w,
-                           bias, C, (bf16*)y, Top, Fo);
+        hipLaunchKernelGGL(dwconv_kernel<bf16>, grid, dim3(C), 0, st, (const bf16*)x, lens, stage, Tip, Fi, w, bias, C,
+                           (bf16*)y, Top, Fo);
     else
-        hipLaunchKernelGGL(dwconv_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)x, lens, stage, B, Tip, Fi, w,
-                           bias, C, (float*)y, Top, Fo);
+        hipLaunchKernelGGL(dwconv_kernel<float>, grid, dim3(C), 0, st, (const float*)x, lens, stage, Tip, Fi, w, bias, C,
+                           (float*)y, Top, Fo);
     SPT_LAUNCH_CHECK();
 }
 
@@ -515,6 +830,18 @@ void pk_rel_attn(int dtype, const void* qkv, const void* p, int ldp, const float
     if (dk % 8 || dk > 256) throw std::runtime_error("pk_rel_attn: head dim must be a multiple of 8, <= 256");
     const size_t smem = (size_t)(2 * dk + Tp) * 4;
     if (smem > 64 * 1024) throw std::runtime_error("pk_rel_attn: too many frames for the LDS score row");
+    static const bool valu = getenv("SPT_PK_ATTN_VALU") != nullptr;  // A/B switch
+    if (dtype == DT_F16 && !valu && (dk == 64 || dk == 128)) {
+        dim3 g(cdiv(Tp, 32), H, B);
+        if (dk == 128)
+            hipLaunchKernelGGL(rel_attn_mfma_kernel<128>, g, dim3(64), 0, st, (const f16*)qkv, (const f16*)p, ldp, pu, pv,
+                               lens, Tp, H, (f16*)out);
+        else
+            hipLaunchKernelGGL(rel_attn_mfma_kernel<64>, g, dim3(64), 0, st, (const f16*)qkv, (const f16*)p, ldp, pu, pv,
+                               lens, Tp, H, (f16*)out);
+        SPT_LAUNCH_CHECK();
+        return;
+    }
     dim3 grid(Tp, H, B);
     if (dtype == DT_F16)
         hipLaunchKernelGGL(rel_attn_kernel<f16>, grid, dim3(64), smem, st, (const f16*)qkv, (const f16*)p, ldp, pu, pv,
@@ -531,16 +858,17 @@ void pk_rel_attn(int dtype, const void* qkv, const void* p, int ldp, const float
 void pk_conv_module(int dtype, const void* a, const int* lens, int B, int Tp, int d, int K, const float* dw_w,
                     const float* dw_b, const float* bn_g, const float* bn_b, const float* bn_m, const float* bn_v,
                     void* out, hipStream_t st) {
-    const int g = grid_of((int64_t)B * Tp * d);
+    if (K != 9) throw std::runtime_error("pk_conv_module: depthwise kernel size 9 only");
+    dim3 grid(cdiv(Tp, CM_TT), B);
     if (dtype == DT_F16)
-        hipLaunchKernelGGL(conv_module_kernel<f16>, dim3(g), dim3(256), 0, st, (const f16*)a, lens, B, Tp, d, K, dw_w,
-                           dw_b, bn_g, bn_b, bn_m, bn_v, (f16*)out);
+        hipLaunchKernelGGL((conv_module_kernel<f16, 9>), grid, dim3(256), 0, st, (const f16*)a, lens, Tp, d, dw_w, dw_b,
+                           bn_g, bn_b, bn_m, bn_v, (f16*)out);
     else if (dtype == DT_BF16)
-        hipLaunchKernelGGL(conv_module_kernel<bf16>, dim3(g), dim3(256), 0, st, (const bf16*)a, lens, B, Tp, d, K, dw_w,
-                           dw_b, bn_g, bn_b, bn_m, bn_v, (bf16*)out);
+        hipLaunchKernelGGL((conv_module_kernel<bf16, 9>), grid, dim3(256), 0, st, (const bf16*)a, lens, Tp, d, dw_w, dw_b,
+                           bn_g, bn_b, bn_m, bn_v, (bf16*)out);
     else
-        hipLaunchKernelGGL(conv_module_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)a, lens, B, Tp, d, K,
-                           dw_w, dw_b, bn_g, bn_b, bn_m, bn_v, (float*)out);
+        hipLaunchKernelGGL((conv_module_kernel<float, 9>), grid, dim3(256), 0, st, (const float*)a, lens, Tp, d, dw_w,
+                           dw_b, bn_g, bn_b, bn_m, bn_v, (float*)out);
     SPT_LAUNCH_CHECK();
 }
 
@@ -565,36 +893,40 @@ void pk_place(int mode, int dtype, const float* src, int N, int K, void* dst, in
     SPT_LAUNCH_CHECK();
 }
 
-template <int XM>
-static void gemv_launch(const PkGemvArgs& a, hipStream_t s) {
-    if (a.Npad % 256 || a.K % a.ksplit) throw std::runtime_error("pk_gemv: bad shape");
-    const int KC = a.K / a.ksplit;
-    dim3 grid(a.Npad / 256, a.ksplit);
-#define PK_GEMV_BM(BMV)                                                                                   \
-    if (a.B <= BMV) {                                                                                     \
-        hipLaunchKernelGGL((gemv_t_kernel<XM, BMV>), grid, dim3(256), (size_t)KC * BMV * 4, s, a);        \
-        SPT_LAUNCH_CHECK();                                                                               \
-        return;                                                                                           \
-    }
-    PK_GEMV_BM(4) PK_GEMV_BM(8) PK_GEMV_BM(16) PK_GEMV_BM(32) PK_GEMV_BM(64)
-#undef PK_GEMV_BM
-    throw std::runtime_error("pk_gemv: more than 64 rows");
+constexpr int kDecSmemMax = 159 * 1024;  // dynamic LDS bound (the kernel's static rows table needs the rest)
+// outputs per workgroup of each stage (grids <= 256 workgroups: one round at one workgroup per CU)
+constexpr int kLstmDO = 16, kPredDO = 16, kJointDO = 64;
+// register-held wave-loads per lane and staged float4 per thread, sized for P <= 640
+constexpr int kNWL = 10, kSEL = 5, kNWP = 5, kSEP = 3, kNWJ = 20, kSEJ = 3;
+
+void pk_prepare() {
+    static bool done = false;  // > 64 KiB dynamic LDS: once per process, before any stream capture
+    if (done) return;
+    HIP_CHECK(hipFuncSetAttribute((const void*)dec_kernel<PKD_LSTM, kLstmDO, kNWL, kSEL>, hipFuncAttributeMaxDynamicSharedMemorySize, kDecSmemMax));
+    HIP_CHECK(hipFuncSetAttribute((const void*)dec_kernel<PKD_PRED, kPredDO, kNWP, kSEP>, hipFuncAttributeMaxDynamicSharedMemorySize, kDecSmemMax));
+    HIP_CHECK(hipFuncSetAttribute((const void*)dec_kernel<PKD_JOINT, kJointDO, kNWJ, kSEJ>, hipFuncAttributeMaxDynamicSharedMemorySize, kDecSmemMax));
+    done = true;
 }
 
-void pk_gemv(int xmode, const PkGemvArgs& a, hipStream_t s) {
-    switch (xmode) {
-        case PKX_LSTM0: gemv_launch<PKX_LSTM0>(a, s); return;
-        case PKX_LSTM1: gemv_launch<PKX_LSTM1>(a, s); return;
-        case PKX_PRED: gemv_launch<PKX_PRED>(a, s); return;
-        case PKX_JOINT: gemv_launch<PKX_JOINT>(a, s); return;
-    }
-    throw std::runtime_error("pk_gemv: bad mode");
-}
+int pk_joint_tile() { return kJointDO; }
 
-void pk_lstm_cell(const float* part, int ksplit, int Npad, const float* b_ih, const float* b_hh, int B, int P,
-                  const PkState* st, float* h, float* c, hipStream_t s) {
-    hipLaunchKernelGGL(lstm_cell_kernel, dim3(cdiv(B * P, 256)), dim3(256), 0, s, part, ksplit, Npad, b_ih, b_hh, B, P,
-                       st, h, c);
+void pk_decode_stage(int mode, const PkDecArgs& a, hipStream_t s) {
+    const int DO = mode == PKD_LSTM ? kLstmDO : mode == PKD_PRED ? kPredDO : kJointDO;
+    const int nwm = mode == PKD_LSTM ? kNWL : mode == PKD_PRED ? kNWP : kNWJ;
+    const int sem = mode == PKD_LSTM ? kSEL : mode == PKD_PRED ? kSEP : kSEJ;
+    if (a.K % (DG * 4) || a.ld % DO || a.B < 1 || a.B > 64 || (mode == PKD_LSTM && a.P % (DO / 4)) ||
+        a.K / 4 * DR > 512 * sem || (a.K / DG) % (256 / DO) || a.K / DG / (256 / DO) > nwm)
+        throw std::runtime_error("pk_decode_stage: bad shape");
+    const size_t smem = ((size_t)a.K * XP + (size_t)DG * DR * DO) * 4;
+    if (smem > (size_t)kDecSmemMax) throw std::runtime_error("pk_decode_stage: K too large for the LDS row stage");
+    const int grid = mode == PKD_LSTM ? a.P / (DO / 4) : a.ld / DO;
+    pk_prepare();
+    switch (mode) {
+        case PKD_LSTM: hipLaunchKernelGGL((dec_kernel<PKD_LSTM, kLstmDO, kNWL, kSEL>), dim3(grid), dim3(512), smem, s, a); break;
+        case PKD_PRED: hipLaunchKernelGGL((dec_kernel<PKD_PRED, kPredDO, kNWP, kSEP>), dim3(grid), dim3(512), smem, s, a); break;
+        case PKD_JOINT: hipLaunchKernelGGL((dec_kernel<PKD_JOINT, kJointDO, kNWJ, kSEJ>), dim3(grid), dim3(512), smem, s, a); break;
+        default: throw std::runtime_error("pk_decode_stage: bad mode");
+    }
     SPT_LAUNCH_CHECK();
 }
 
@@ -603,8 +935,29 @@ void pk_joint_fin(const PkFinArgs& a, hipStream_t s) {
     SPT_LAUNCH_CHECK();
 }
 
-void pk_state_init(PkState* st, int B, int V, float* h, float* c, int n, hipStream_t s) {
-    hipLaunchKernelGGL(state_init_kernel, dim3(cdiv(std::max(B, n), 256)), dim3(256), 0, s, st, B, V, h, c, n);
+void pk_state_init(PkState* st, int B, int V, float* h, float* c, int n, float* xemb, float* fecur, const float* fe,
+                   int T3p, int P, hipStream_t s) {
+    hipLaunchKernelGGL(state_init_kernel, dim3(cdiv(std::max(std::max(B, n), B * P), 256)), dim3(256), 0, s, st, B, V, h,
+                       c, n, xemb, fecur, fe, T3p, P);
+    SPT_LAUNCH_CHECK();
+}
+
+__global__ void place_blocked_kernel(const float* __restrict__ s, int N, int K, int DO, float* __restrict__ d) {
+    const int64_t total = (int64_t)N * K;
+    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int n = (int)(i % N), k = (int)(i / N);
+        d[((size_t)(n / DO) * K + k) * DO + n % DO] = s[(size_t)n * K + k];
+    }
+}
+
+void pk_place_blocked(const float* src, int N, int K, int mode, float* dst, hipStream_t s) {
+    const int DO = mode == PKD_PRED ? kPredDO : kJointDO;
+    hipLaunchKernelGGL(place_blocked_kernel, dim3(grid_of((int64_t)N * K)), dim3(256), 0, s, src, N, K, DO, dst);
+    SPT_LAUNCH_CHECK();
+}
+
+void pk_place_lstm(const float* src, int P, float* dst, int row0, hipStream_t s) {
+    hipLaunchKernelGGL(place_lstm_kernel, dim3(grid_of((int64_t)4 * P * P)), dim3(256), 0, s, src, P, dst, row0);
     SPT_LAUNCH_CHECK();
 }
 

@@ -20,8 +20,9 @@ __host__ __device__ inline int64_t kv_offset(int l, int kvi, int b, int h, int t
 
 // EPI_BIAS_RESID: f32 C += alpha * (acc + bias); EPI_BIAS_F32: f32 C = alpha * (acc + bias);
 // SWISH / RELU: activation of acc + bias in the storage dtype
+// EPI_PARTIAL: split-K slab s (grid.y) of the f32 product at C + s * c_split (no bias)
 enum { EPI_BIAS = 0, EPI_BIAS_GELU = 1, EPI_BIAS_GELU_POS = 2, EPI_BIAS_RESID = 3, EPI_KVSPLIT = 4,
-       EPI_BIAS_SWISH = 5, EPI_BIAS_RELU = 6, EPI_BIAS_F32 = 7 };
+       EPI_BIAS_SWISH = 5, EPI_BIAS_RELU = 6, EPI_BIAS_F32 = 7, EPI_PARTIAL = 8 };
 
 struct GemmArgs {
     const void* A; int lda; int64_t sA;   // A rows (+ batch stride, elements)
@@ -32,6 +33,7 @@ struct GemmArgs {
     const float* pos;                     // EPI_BIAS_GELU_POS: [M][N] f32
     int kv_B, kv_T, kv_H;                 // EPI_KVSPLIT: dest = the cross K/V cache (kv_offset)
     float alpha = 1.0f;                   // EPI_BIAS_RESID / EPI_BIAS_F32 scale
+    int ksplit = 1; int64_t c_split = 0;  // EPI_PARTIAL: K split over grid.y, slab stride (elements)
 };
 void gemm_nt(int dtype, int epi, const GemmArgs& g, int batch, hipStream_t st);
 // variant 0: automatic (bf16 N % 256 == 0 -> 256 x 256 tile); 1: 128 x 128 tile; 2: prefer 256 x 256
@@ -78,6 +80,11 @@ void mel_norm(int dtype, const float* mel_raw, const unsigned* mel_max, const in
 // y[m] = LN(x[m]) * w + b ; x f32 [M][d], y f32/bf16 [M][d]
 void layernorm(int dtype, const float* x, int M, int d, const float* w, const float* b, void* y,
                hipStream_t st);
+// x[m] += alpha * (slab_0[m] + .. + slab_{ks-1}[m] + pbias) (the pending split-K product of a
+// residual GEMM, in slab order), then y[m] = LN(x[m]) * w + b; write_x: store the summed x back
+void layernorm_pend(int dtype, float* x, int M, int d, const float* slab, int ks, int64_t slab_stride,
+                    const float* pbias, float alpha, const float* w, const float* b, void* y, bool write_x,
+                    hipStream_t st);
 // convert an activation buffer to f32 (debug / tests)
 void to_f32(int dtype, const void* src, float* dst, int64_t n, hipStream_t st);
 

@@ -119,18 +119,16 @@ ParakeetEngine::ParakeetEngine(const PkDims& dm, int dtype, int device, int max_
     T2max_ = halve(T1max_);
     T3max_ = halve(T2max_);
     const int P = dm_.pred;
-    P_pad_ = round_up(P, 256);
-    lstm_pad_ = round_up(4 * P, 256);
-    joint_pad_ = round_up(dm_.n_vocab + 1 + dm_.n_dur, 256);
-    lstm_split_ = 2 * P / 64;
-    pred_split_ = P / 64;
-    joint_split_ = P / 128;
+    P_pad_ = round_up(P, 64);
+    joint_pad_ = round_up(dm_.n_vocab + 1 + dm_.n_dur, 64);
+    joint_tiles_ = joint_pad_ / pk_joint_tile();
     cap_ = T3max_ * kMaxSymbols + 1;
     select();
     try {
         HIP_CHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
         ev_.resize(6);
         for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
+        pk_prepare();
         alloc_weights();
         alloc_workspace();
         upload_tables();
@@ -155,6 +153,8 @@ void ParakeetEngine::release() {
     if (st_) (void)hipStreamSynchronize(st_);
     for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
     graphs_.clear();
+    for (auto& kv : enc_graphs_) (void)hipGraphExecDestroy(kv.second);
+    enc_graphs_.clear();
     for (auto& e : ev_) if (e) (void)hipEventDestroy(e);
     ev_.clear();
     if (warena_) (void)hipFree(warena_);
@@ -254,22 +254,22 @@ void ParakeetEngine::alloc_weights() {
         }
         emb_ = f32t(90000, (int64_t)V1 * P, PLAIN, -2);
         for (int j = 0; j < 2; ++j) {
-            lstm_wt_[j] = F32((int64_t)2 * P * lstm_pad_);
-            add(90001 + 4 * j, (int64_t)4 * P * P, PLAIN, fanin_exp(P), PK_PLACE_TRANSPOSE, DT_F32, lstm_wt_[j], 4 * P, P,
-                lstm_pad_, 0);
-            add(90002 + 4 * j, (int64_t)4 * P * P, PLAIN, fanin_exp(P), PK_PLACE_TRANSPOSE, DT_F32, lstm_wt_[j], 4 * P, P,
-                lstm_pad_, P);
+            lstm_wt_[j] = F32((int64_t)2 * P * 4 * P);
+            add(90001 + 4 * j, (int64_t)4 * P * P, PLAIN, fanin_exp(P), PK_PLACE_LSTM, DT_F32, lstm_wt_[j], 4 * P, P,
+                4 * P, 0);
+            add(90002 + 4 * j, (int64_t)4 * P * P, PLAIN, fanin_exp(P), PK_PLACE_LSTM, DT_F32, lstm_wt_[j], 4 * P, P,
+                4 * P, P);
             lstm_bih_[j] = f32t(90003 + 4 * j, 4 * P, PLAIN, -5);
             lstm_bhh_[j] = f32t(90004 + 4 * j, 4 * P, PLAIN, -5);
         }
         jenc_w_ = f32t(90009, (int64_t)P * d, PLAIN, fanin_exp(d));
         jenc_b_ = f32t(90010, P, PLAIN, -5);
         jpred_wt_ = F32((int64_t)P * P_pad_);
-        add(90011, (int64_t)P * P, PLAIN, fanin_exp(P), PK_PLACE_TRANSPOSE, DT_F32, jpred_wt_, P, P, P_pad_, 0);
+        add(90011, (int64_t)P * P, PLAIN, fanin_exp(P), PK_PLACE_BLOCKED, PKD_PRED, jpred_wt_, P, P, P_pad_, 0);
         jpred_b_ = F32(P_pad_);
         add(90012, P, PLAIN, -5, PK_PLACE_COPY, DT_F32, jpred_b_);
         jout_wt_ = F32((int64_t)P * joint_pad_);
-        add(90013, (int64_t)NO * P, PLAIN, fanin_exp(P), PK_PLACE_TRANSPOSE, DT_F32, jout_wt_, NO, P, joint_pad_, 0);
+        add(90013, (int64_t)NO * P, PLAIN, fanin_exp(P), PK_PLACE_BLOCKED, PKD_JOINT, jout_wt_, NO, P, joint_pad_, 0);
         jout_b_ = F32(joint_pad_);
         add(90014, NO, PLAIN, -5, PK_PLACE_COPY, DT_F32, jout_b_);
         if (!pass) {
@@ -295,7 +295,9 @@ void ParakeetEngine::alloc_weights() {
 }
 
 void ParakeetEngine::place(const TSpec& t, const float* src) {
-    if (t.mode == PK_PLACE_TRANSPOSE) pk_place(PK_PLACE_TRANSPOSE, DT_F32, src, t.N, t.K, t.dst, t.ld, t.row0, 0, 0, st_);
+    if (t.mode == PK_PLACE_LSTM) pk_place_lstm(src, dm_.pred, (float*)t.dst, t.row0, st_);
+    else if (t.mode == PK_PLACE_BLOCKED) pk_place_blocked(src, t.N, t.K, t.dt, (float*)t.dst, st_);
+    else if (t.mode == PK_PLACE_TRANSPOSE) pk_place(PK_PLACE_TRANSPOSE, DT_F32, src, t.N, t.K, t.dst, t.ld, t.row0, 0, 0, st_);
     else if (t.mode == PK_PLACE_SUBPERM) pk_place(PK_PLACE_SUBPERM, t.dt, src, t.N, 0, t.dst, 0, 0, t.ld, t.row0, st_);
     else pk_place(PK_PLACE_COPY, t.dt, src, 1, (int)t.n, t.dst, 0, 0, 0, 0, st_);
     if (t.tid == 90000)  // the prediction network's blank row is zero (blank_as_pad)
@@ -346,13 +348,15 @@ void ParakeetEngine::alloc_workspace() {
         glu_ = c.take(M3 * 2 * d * esz_);
         cv_ = c.take(M3 * d * esz_);
         fe_ = (float*)c.take(M3 * P * 4);
+        slab_ = (float*)c.take(std::max<int64_t>(M3, 32768) * d * 4);  // split-K slabs: ks * M <= ~25k rows (gemm())
         state_ = (PkState*)c.take(B * sizeof(PkState));
-        h_ = (float*)c.take((int64_t)2 * B * P * 4);
-        c_ = (float*)c.take((int64_t)2 * B * P * 4);
+        h_ = (float*)c.take((int64_t)4 * B * P * 4);  // [layer][parity][B][P]
+        c_ = (float*)c.take((int64_t)4 * B * P * 4);
         gp_ = (float*)c.take((int64_t)B * P * 4);
-        lstm_part_ = (float*)c.take((int64_t)lstm_split_ * B * lstm_pad_ * 4);
-        pred_part_ = (float*)c.take((int64_t)pred_split_ * B * P_pad_ * 4);
-        joint_part_ = (float*)c.take((int64_t)joint_split_ * B * joint_pad_ * 4);
+        xemb_ = (float*)c.take((int64_t)B * P * 4);
+        fecur_ = (float*)c.take((int64_t)B * P * 4);
+        jpart_ = (float4*)c.take((int64_t)B * joint_tiles_ * 16);
+        dur_ = (float*)c.take((int64_t)B * dm_.n_dur * 4);
         out_tok_ = (int*)c.take((int64_t)B * cap_ * 4);
         out_frame_ = (int*)c.take((int64_t)B * cap_ * 4);
         out_t1_ = (float*)c.take((int64_t)B * cap_ * 4);
@@ -425,16 +429,36 @@ void ParakeetEngine::run_mel(const float* pcm_dev, int64_t stride, int B, int Tp
     pk_mel_norm(mel_, lens_, B, Tp, dm_.n_mels, st_);
 }
 
+// GEMM tile choice: the 256 x 256 tile whenever at least ~96 of its workgroups are in flight
+// (its MFMA efficiency beats the 128 x 128 tile's even with part of the chip idle), else the
+// 128 x 128 tile.  Residual products (EPI_PARTIAL, N = d) also split K over grid.y toward ~192
+// (256-tile) or ~512 (128-tile) workgroups; their f32 slabs are summed, with the bias and the
+// 1/2 FFN scale, by the LayerNorm that reads the residual next.  Returns the split used.
+int ParakeetEngine::gemm(int dt, int epi, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
+                         const float* bias, void* Cp, int ldc, float alpha) {
+    static const int t256 = getenv("SPT_GEMM_T256") ? atoi(getenv("SPT_GEMM_T256")) : 96;
+    int variant = 1, ks = 1;
+    if (dt != DT_F32 && N % 256 == 0 && K % 64 == 0) {
+        const int64_t t = (int64_t)cdiv(M, 256) * (N / 256);
+        int k2 = 1;
+        if (epi == EPI_PARTIAL)
+            while (k2 < 8 && t * k2 < 192 && K % (2 * k2) == 0 && (K / (2 * k2)) % 64 == 0 && K / (2 * k2) >= 256) k2 *= 2;
+        if (t * k2 >= t256) { variant = 2; ks = k2; }
+    }
+    if (variant == 1 && epi == EPI_PARTIAL) {
+        const int64_t t = (int64_t)cdiv(M, 128) * (N / 128);
+        while (ks < 8 && t * ks * 2 <= 512 && K % (2 * ks) == 0 && (K / (2 * ks)) % 64 == 0) ks *= 2;
+    }
+    GemmArgs g{};
+    g.A = A; g.lda = lda; g.W = W; g.ldw = ldw; g.M = M; g.N = N; g.K = K; g.bias = bias;
+    g.C = Cp; g.ldc = ldc; g.alpha = alpha; g.ksplit = ks; g.c_split = (int64_t)M * ldc;
+    gemm_nt_variant(dt, epi, g, 1, variant, st_);
+    SPT_LAUNCH_CHECK();
+    return ks;
+}
+
 void ParakeetEngine::run_encoder(int B, int Tp, int T1p, int T2p, int T3p) {
     const int C = dm_.sub_ch, d = dm_.d, H = dm_.n_heads, dk = d / H, ff = dm_.ff, Ln = dm_.n_layers;
-    auto gemm = [&](int dt, int epi, const void* A, int lda, const void* W, int ldw, int M, int N, int K, const float* bias,
-                    void* Cp, int ldc, float alpha = 1.0f) {
-        GemmArgs g{};
-        g.A = A; g.lda = lda; g.W = W; g.ldw = ldw; g.M = M; g.N = N; g.K = K; g.bias = bias;
-        g.C = Cp; g.ldc = ldc; g.alpha = alpha;
-        gemm_nt(dt, epi, g, 1, st_);
-        SPT_LAUNCH_CHECK();
-    };
     // ---- dw_striding subsampling (channel-last activations)
     pk_conv0(dt_, mel_, lens_, B, Tp, dm_.n_mels, c0_w_, c0_b_, C, y1_, T1p, F1_, st_);
     pk_dwconv(dt_, y1_, lens_, 1, B, T1p, F1_, dw1_w_, dw1_b_, C, y2a_, T2p, F2_, st_);
@@ -448,29 +472,31 @@ void ParakeetEngine::run_encoder(int B, int Tp, int T1p, int T2p, int T3p) {
     // ---- relative positions, projected for every layer at once
     pk_relpos(dt_, T3p, d, pe_, st_);
     gemm(dt_, EPI_BIAS, pe_, d, pos_w_, d, 2 * T3p - 1, Ln * d, d, nullptr, pp_, Ln * d);
+    const int64_t sst = (int64_t)M * d;
+    int ks;
     for (int l = 0; l < Ln; ++l) {
         const Layer& y = L_[l];
-        // 1/2 FFN
+        // 1/2 FFN; its product stays pending in the slabs until the next LayerNorm
         layernorm(dt_, x, M, d, y.ln1_w, y.ln1_b, xn_, st_);
         gemm(dt_, EPI_BIAS_SWISH, xn_, d, y.ff1_w1, d, M, ff, d, y.ff1_b1, ffh_, ff);
-        gemm(dt_, EPI_BIAS_RESID, ffh_, ff, y.ff1_w2, ff, M, d, ff, y.ff1_b2, x, d, 0.5f);
+        ks = gemm(dt_, EPI_PARTIAL, ffh_, ff, y.ff1_w2, ff, M, d, ff, nullptr, slab_, d);
         // rel-pos MHSA
-        layernorm(dt_, x, M, d, y.lna_w, y.lna_b, xn_, st_);
+        layernorm_pend(dt_, x, M, d, slab_, ks, sst, y.ff1_b2, 0.5f, y.lna_w, y.lna_b, xn_, true, st_);
         gemm(dt_, EPI_BIAS, xn_, d, y.qkv_w, d, M, 3 * d, d, y.qkv_b, qkv_, 3 * d);
         pk_rel_attn(dt_, qkv_, (const char*)pp_ + (size_t)l * d * esz_, Ln * d, y.pos_u, y.pos_v, lens_, B, T3p, H, dk,
                     ctx_, st_);
-        gemm(dt_, EPI_BIAS_RESID, ctx_, d, y.o_w, d, M, d, d, y.o_b, x, d);
+        ks = gemm(dt_, EPI_PARTIAL, ctx_, d, y.o_w, d, M, d, d, nullptr, slab_, d);
         // convolution module
-        layernorm(dt_, x, M, d, y.lnc_w, y.lnc_b, xn_, st_);
+        layernorm_pend(dt_, x, M, d, slab_, ks, sst, y.o_b, 1.0f, y.lnc_w, y.lnc_b, xn_, true, st_);
         gemm(dt_, EPI_BIAS, xn_, d, y.pw1_w, d, M, 2 * d, d, y.pw1_b, glu_, 2 * d);
         pk_conv_module(dt_, glu_, lens_, B, T3p, d, dm_.conv_k, y.dw_w, y.dw_b, y.bn_g, y.bn_b, y.bn_m, y.bn_v, cv_, st_);
-        gemm(dt_, EPI_BIAS_RESID, cv_, d, y.pw2_w, d, M, d, d, y.pw2_b, x, d);
+        ks = gemm(dt_, EPI_PARTIAL, cv_, d, y.pw2_w, d, M, d, d, nullptr, slab_, d);
         // 1/2 FFN
-        layernorm(dt_, x, M, d, y.ln2_w, y.ln2_b, xn_, st_);
+        layernorm_pend(dt_, x, M, d, slab_, ks, sst, y.pw2_b, 1.0f, y.ln2_w, y.ln2_b, xn_, true, st_);
         gemm(dt_, EPI_BIAS_SWISH, xn_, d, y.ff2_w1, d, M, ff, d, y.ff2_b1, ffh_, ff);
-        gemm(dt_, EPI_BIAS_RESID, ffh_, ff, y.ff2_w2, ff, M, d, ff, y.ff2_b2, x, d, 0.5f);
-        // LayerNorm out (f32) into the other residual buffer
-        layernorm(DT_F32, x, M, d, y.lno_w, y.lno_b, x2, st_);
+        ks = gemm(dt_, EPI_PARTIAL, ffh_, ff, y.ff2_w2, ff, M, d, ff, nullptr, slab_, d);
+        // LayerNorm out (f32) of x + the pending 1/2 FFN into the other residual buffer
+        layernorm_pend(DT_F32, x, M, d, slab_, ks, sst, y.ff2_b2, 0.5f, y.lno_w, y.lno_b, x2, false, st_);
         std::swap(x, x2);
     }
     // the joint's encoder projection of every frame (f32)
@@ -478,40 +504,72 @@ void ParakeetEngine::run_encoder(int B, int Tp, int T1p, int T2p, int T3p) {
     enc_out_ = x;
 }
 
-void ParakeetEngine::enqueue_step(int B, int T3p, int max_symbols, int cap) {
+// The encoder's ~16 launches per layer replayed as one hipGraph per (batch, padded frames) once
+// that shape has been seen twice (a stream of fixed windows, a batch of full chunks); shapes seen
+// once run eagerly, so arbitrary utterance lengths do not pay for graph instantiation.
+void ParakeetEngine::encode(int B, int Tp, int T1p, int T2p, int T3p) {
+    static const bool no_graph = getenv("SPT_NO_GRAPH") != nullptr;
+    const std::pair<int, int> key{B, Tp};
+    auto it = enc_graphs_.find(key);
+    if (it == enc_graphs_.end() && !no_graph && enc_seen_[key]++ >= 1 && enc_graphs_.size() < 32) {
+        hipGraph_t graph;
+        HIP_CHECK(hipStreamBeginCapture(st_, hipStreamCaptureModeThreadLocal));
+        run_encoder(B, Tp, T1p, T2p, T3p);
+        HIP_CHECK(hipStreamEndCapture(st_, &graph));
+        hipGraphExec_t exec;
+        HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+        HIP_CHECK(hipGraphDestroy(graph));
+        it = enc_graphs_.emplace(key, exec).first;
+        enc_out_graph_[key] = enc_out_;
+    }
+    if (it != enc_graphs_.end()) {
+        HIP_CHECK(hipGraphLaunch(it->second, st_));
+        enc_out_ = enc_out_graph_[key];
+    } else {
+        run_encoder(B, Tp, T1p, T2p, T3p);
+    }
+}
+
+void ParakeetEngine::enqueue_step(int B, int T3p, int max_symbols, int cap, int parity) {
     const int P = dm_.pred;
-    PkGemvArgs a{};
-    a.B = B; a.P = P; a.st = state_; a.emb = emb_; a.h0 = h_; a.h1 = h_ + (size_t)B * P;
-    a.WT = lstm_wt_[0]; a.Npad = lstm_pad_; a.K = 2 * P; a.ksplit = lstm_split_; a.part = lstm_part_;
-    pk_gemv(PKX_LSTM0, a, st_);
-    pk_lstm_cell(lstm_part_, lstm_split_, lstm_pad_, lstm_bih_[0], lstm_bhh_[0], B, P, state_, h_, c_, st_);
-    a.WT = lstm_wt_[1];
-    pk_gemv(PKX_LSTM1, a, st_);
-    pk_lstm_cell(lstm_part_, lstm_split_, lstm_pad_, lstm_bih_[1], lstm_bhh_[1], B, P, state_, h_ + (size_t)B * P,
-                 c_ + (size_t)B * P, st_);
-    a.WT = jpred_wt_; a.Npad = P_pad_; a.K = P; a.ksplit = pred_split_; a.part = pred_part_;
-    pk_gemv(PKX_PRED, a, st_);
-    a.WT = jout_wt_; a.Npad = joint_pad_; a.K = P; a.ksplit = joint_split_; a.part = joint_part_;
-    a.fe = fe_; a.T3p = T3p; a.pred_part = pred_part_; a.pred_split = pred_split_; a.pred_Npad = P_pad_;
-    a.pred_b = jpred_b_; a.gp = gp_;
-    pk_gemv(PKX_JOINT, a, st_);
+    const size_t BP = (size_t)B * P;
+    auto hbuf = [&](float* base, int layer, int par) { return base + ((size_t)layer * 2 + par) * BP; };
+    const int p = parity, q = parity ^ 1;
+    PkDecArgs a{};
+    a.B = B; a.P = P; a.V = dm_.n_vocab; a.n_dur = dm_.n_dur; a.st = state_;
+    // LSTM layer 0: x = [emb(token) | h0]
+    a.WT = lstm_wt_[0]; a.ld = 4 * P; a.K = 2 * P; a.N = 4 * P; a.b0 = lstm_bih_[0]; a.b1 = lstm_bhh_[0];
+    a.xin = xemb_; a.h_in = hbuf(h_, 0, p); a.c_in = hbuf(c_, 0, p); a.h_out = hbuf(h_, 0, q); a.c_out = hbuf(c_, 0, q);
+    pk_decode_stage(PKD_LSTM, a, st_);
+    // LSTM layer 1: x = [h0' | h1]
+    a.WT = lstm_wt_[1]; a.b0 = lstm_bih_[1]; a.b1 = lstm_bhh_[1]; a.xin = hbuf(h_, 0, q);
+    a.h_in = hbuf(h_, 1, p); a.c_in = hbuf(c_, 1, p); a.h_out = hbuf(h_, 1, q); a.c_out = hbuf(c_, 1, q);
+    pk_decode_stage(PKD_LSTM, a, st_);
+    // prediction projection of h1' (rows with a new token)
+    a.WT = jpred_wt_; a.ld = P_pad_; a.K = P; a.N = P; a.b0 = jpred_b_; a.b1 = nullptr; a.xin = hbuf(h_, 1, q); a.gp = gp_;
+    pk_decode_stage(PKD_PRED, a, st_);
+    // joint: ReLU(enc[t] + pred) -> logits -> per-workgroup top-2 + durations
+    a.WT = jout_wt_; a.ld = joint_pad_; a.K = P; a.N = dm_.n_vocab + 1 + dm_.n_dur; a.b0 = jout_b_;
+    a.fe = fecur_; a.part = jpart_; a.n_tiles = joint_tiles_; a.dur = dur_;
+    pk_decode_stage(PKD_JOINT, a, st_);
     PkFinArgs f{};
-    f.part = joint_part_; f.ksplit = joint_split_; f.Npad = joint_pad_; f.bias = jout_b_;
+    f.part = jpart_; f.n_tiles = joint_tiles_; f.dur = dur_;
     f.V = dm_.n_vocab; f.n_dur = dm_.n_dur; f.max_symbols = max_symbols; f.B = B; f.cap = cap; f.lens = lens_;
     f.st = state_; f.out_tok = out_tok_; f.out_frame = out_frame_; f.out_t1 = out_t1_; f.out_t2 = out_t2_;
+    f.P = P; f.T3p = T3p; f.emb = emb_; f.fe = fe_; f.xemb = xemb_; f.fecur = fecur_;
     pk_joint_fin(f, st_);
 }
 
 void ParakeetEngine::run_decode(int B, int T3p, int max_symbols, std::vector<PkUtt>* out) {
     const int P = dm_.pred;
-    pk_state_init(state_, B, dm_.n_vocab, h_, c_, 2 * B * P, st_);
+    pk_state_init(state_, B, dm_.n_vocab, h_, c_, 4 * B * P, xemb_, fecur_, fe_, T3p, P, st_);
     const GraphKey key{B, T3p, max_symbols};
     auto it = graphs_.find(key);
     static const bool no_graph = getenv("SPT_NO_GRAPH") != nullptr;
     if (it == graphs_.end() && !no_graph) {
         hipGraph_t graph;
         HIP_CHECK(hipStreamBeginCapture(st_, hipStreamCaptureModeThreadLocal));
-        for (int s = 0; s < kStepsPerGraph; ++s) enqueue_step(B, T3p, max_symbols, cap_);
+        for (int s = 0; s < kStepsPerGraph; ++s) enqueue_step(B, T3p, max_symbols, cap_, s & 1);
         HIP_CHECK(hipStreamEndCapture(st_, &graph));
         hipGraphExec_t exec;
         HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
@@ -523,7 +581,7 @@ void ParakeetEngine::run_decode(int B, int T3p, int max_symbols, std::vector<PkU
     hstate_.resize(B);
     int steps = 0;
     while (true) {
-        if (no_graph) for (int s = 0; s < kStepsPerGraph; ++s) enqueue_step(B, T3p, max_symbols, cap_);
+        if (no_graph) for (int s = 0; s < kStepsPerGraph; ++s) enqueue_step(B, T3p, max_symbols, cap_, s & 1);
         else HIP_CHECK(hipGraphLaunch(it->second, st_));
         steps += kStepsPerGraph;
         HIP_CHECK(hipMemcpyAsync(hstate_.data(), state_, B * sizeof(PkState), hipMemcpyDeviceToHost, st_));
@@ -568,7 +626,7 @@ void ParakeetEngine::transcribe_device(const float* pcm_dev, int64_t stride, con
     HIP_CHECK(hipMemcpyAsync(lens_, lens.data(), lens.size() * 4, hipMemcpyHostToDevice, st_));
     run_mel(pcm_dev, stride, B, Tp);
     HIP_CHECK(hipEventRecord(ev_[1], st_));
-    run_encoder(B, Tp, T1p, T2p, T3p);
+    encode(B, Tp, T1p, T2p, T3p);
     HIP_CHECK(hipEventRecord(ev_[2], st_));
     run_decode(B, T3p, max_symbols, out);
     float ms;
@@ -650,7 +708,7 @@ bool ParakeetEngine::debug_weight_checksum(int tid, double* out2) {
     auto it = table_.find(tid);
     if (it == table_.end()) return false;
     const TSpec& t = specs_[it->second];
-    if (t.mode == PK_PLACE_TRANSPOSE) return false;  // shares its W^T block with other tensors
+    if (t.mode == PK_PLACE_TRANSPOSE || t.mode == PK_PLACE_LSTM || t.mode == PK_PLACE_BLOCKED) return false;  // re-tiled
     select();
     HIP_CHECK(hipMemsetAsync(dsum_, 0, 16, st_));
     tensor_checksum(t.dt, t.dst, t.n, dsum_, st_);

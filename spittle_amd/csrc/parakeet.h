@@ -101,8 +101,11 @@ private:
     void frame_counts(const int* n, int B, std::vector<int>* lens, int* Tp, int* T1p, int* T2p, int* T3p) const;
     void run_mel(const float* pcm_dev, int64_t stride, int B, int Tp);
     void run_encoder(int B, int Tp, int T1p, int T2p, int T3p);
+    void encode(int B, int Tp, int T1p, int T2p, int T3p);  // run_encoder, graph-replayed for repeated shapes
+    int gemm(int dt, int epi, const void* A, int lda, const void* W, int ldw, int M, int N, int K, const float* bias,
+             void* Cp, int ldc, float alpha = 1.0f);
     void run_decode(int B, int T3p, int max_symbols, std::vector<PkUtt>* out);
-    void enqueue_step(int B, int T3p, int max_symbols, int cap);
+    void enqueue_step(int B, int T3p, int max_symbols, int cap, int parity);
 
     PkDims dm_;
     int dt_, dev_, max_batch_, max_samples_;
@@ -110,8 +113,7 @@ private:
     int esz_;
     int F1_, F2_, F3_;               // frequency bins after each stride-2 stage
     int Tmax_, T1max_, T2max_, T3max_;
-    int P_pad_, lstm_pad_, joint_pad_;  // W^T row lengths (multiples of 256)
-    int lstm_split_, pred_split_, joint_split_;
+    int P_pad_, joint_pad_, joint_tiles_;  // W^T row lengths (multiples of 64), joint workgroups
     hipStream_t st_ = nullptr;
     std::vector<hipEvent_t> ev_;
 
@@ -142,9 +144,12 @@ private:
     void *xn_ = nullptr, *ffh_ = nullptr, *qkv_ = nullptr, *pe_ = nullptr, *pp_ = nullptr, *ctx_ = nullptr;
     void *glu_ = nullptr, *cv_ = nullptr;
     float* fe_ = nullptr;
+    float* slab_ = nullptr;          // split-K partial products of the residual GEMMs [ks][M][d]
     PkState* state_ = nullptr;
     float *h_ = nullptr, *c_ = nullptr, *gp_ = nullptr;
-    float *lstm_part_ = nullptr, *pred_part_ = nullptr, *joint_part_ = nullptr;
+    float *xemb_ = nullptr, *fecur_ = nullptr;  // next step's LSTM-0 input rows, current-frame rows
+    float4* jpart_ = nullptr;
+    float* dur_ = nullptr;
     int *out_tok_ = nullptr, *out_frame_ = nullptr;
     float *out_t1_ = nullptr, *out_t2_ = nullptr;
     int cap_ = 0;
@@ -152,6 +157,9 @@ private:
     int64_t scratch_n_ = 0;
     double* dsum_ = nullptr;
     std::map<GraphKey, hipGraphExec_t> graphs_;
+    std::map<std::pair<int, int>, hipGraphExec_t> enc_graphs_;  // (B, Tp) -> encoder graph
+    std::map<std::pair<int, int>, int> enc_seen_;
+    std::map<std::pair<int, int>, float*> enc_out_graph_;
     std::vector<PkState> hstate_;
 
     PkTimings tm_;

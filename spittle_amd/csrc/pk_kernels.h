@@ -40,7 +40,7 @@ void pk_conv_module(int dtype, const void* a, const int* lens, int B, int Tp, in
                     void* out, hipStream_t st);
 
 // weight placement (f32 source on the device -> engine storage)
-enum { PK_PLACE_COPY = 0, PK_PLACE_TRANSPOSE = 1, PK_PLACE_SUBPERM = 2 };
+enum { PK_PLACE_COPY = 0, PK_PLACE_TRANSPOSE = 1, PK_PLACE_SUBPERM = 2, PK_PLACE_LSTM = 3, PK_PLACE_BLOCKED = 4 };
 // COPY: dst[i] = src[i] (dtype); TRANSPOSE: src [N][K] -> f32 dst[(row0 + k) * ld + n];
 // SUBPERM: src [N][C * F] (channel-major flatten) -> dst [N][F * C] (dtype)
 void pk_place(int mode, int dtype, const float* src, int N, int K, void* dst, int ld, int row0, int C, int F,
@@ -50,33 +50,48 @@ void pk_place(int mode, int dtype, const float* src, int N, int K, void* dst, in
 struct PkState {         // per row, device
     int t, at_t, n_out, done, upd, tok;
 };
-enum { PKX_LSTM0 = 0, PKX_LSTM1 = 1, PKX_PRED = 2, PKX_JOINT = 3 };
-struct PkGemvArgs {
-    const float* WT; int Npad, K;  // W^T [K][Npad]
-    int ksplit;                    // K / ksplit rows per split (split s -> part[s])
-    float* part;                   // [ksplit][B][Npad]
-    int B, P;
+// One decode step = LSTM layer 0, LSTM layer 1, prediction projection, joint, fin.  The LSTM
+// states ping-pong between two buffers per layer (a stage's workgroups read every unit of the
+// previous state while writing their own units of the next).
+enum { PKD_LSTM = 0, PKD_PRED = 1, PKD_JOINT = 2 };
+struct PkDecArgs {
+    const float* WT; int ld, K, N;  // blocked W^T [ld / DO][K][DO] (pk_place_lstm / pk_place_blocked); ld = padded N
+    const float* b0; const float* b1;  // LSTM: b_ih, b_hh; PRED / JOINT: bias
+    int B, P, V, n_dur;
     const PkState* st;
-    const float* emb;              // PKX_LSTM0: [V+1][P]
-    const float* h0; const float* h1;  // [B][P]
-    const float* fe; int T3p;      // PKX_JOINT: encoder projection [B*T3p][P]
-    const float* pred_part; int pred_split, pred_Npad; const float* pred_b;  // PKX_JOINT: gp = sum + b (upd rows)
-    float* gp;                     // [B][P] stored prediction projection
+    const float* xin;               // LSTM: input rows [B][P] (layer 0: the token embeddings); PRED: h1
+
+    const float* h_in; const float* c_in; float* h_out; float* c_out;  // LSTM state [B][P]
+    const float* fe;                // JOINT: each row's current-frame encoder projection [B][P]
+    float* gp;                      // PRED: out (rows with upd); JOINT: in [B][P]
+    float4* part; int n_tiles;      // JOINT: per-workgroup top-2 {v1, i1, v2, -} [B][n_tiles]
+    float* dur;                     // JOINT: duration logits [B][n_dur]
 };
-void pk_gemv(int xmode, const PkGemvArgs& a, hipStream_t s);
-// LSTM cell of the rows with upd: gates = sum of part slabs + b_ih + b_hh (i, f, g, o)
-void pk_lstm_cell(const float* part, int ksplit, int Npad, const float* b_ih, const float* b_hh, int B, int P,
-                  const PkState* st, float* h, float* c, hipStream_t s);
+void pk_decode_stage(int mode, const PkDecArgs& a, hipStream_t s);
+// one-time kernel attributes (before any stream capture)
+void pk_prepare();
+// outputs per workgroup of the joint stage (its top-2 partials per row: ld / pk_joint_tile())
+int pk_joint_tile();
 struct PkFinArgs {
-    const float* part; int ksplit, Npad;  // joint slabs
-    const float* bias;                    // [V + 1 + n_dur]
+    const float4* part; int n_tiles;
+    const float* dur;
     int V, n_dur, max_symbols, B, cap;
     const int* lens;                      // T3 per row at lens[b * 4 + 3]
     PkState* st;
+    int P, T3p;
+    const float* emb; const float* fe;    // embedding [V+1][P]; encoder projection [B*T3p][P]
+    float* xemb; float* fecur;            // out: next step's LSTM-0 input / current-frame row [B][P]
     int* out_tok; int* out_frame; float* out_t1; float* out_t2;  // [B][cap]
 };
 void pk_joint_fin(const PkFinArgs& a, hipStream_t s);
-// rows start at t = 0 with the blank symbol pending (upd, tok = V); h / c: n floats zeroed
-void pk_state_init(PkState* st, int B, int V, float* h, float* c, int n, hipStream_t s);
+// rows start at t = 0 with the blank symbol pending (upd, tok = V); h / c: n floats zeroed; xemb
+// zero (the blank row), fecur = frame 0 of fe [B*T3p][P]
+void pk_state_init(PkState* st, int B, int V, float* h, float* c, int n, float* xemb, float* fecur, const float* fe,
+                   int T3p, int P, hipStream_t s);
+// LSTM weight [4P][P] (gate rows i, f, g, o) -> rows row0.. of the blocked, gate-interleaved W^T
+// [P / 4][2P][16]
+void pk_place_lstm(const float* src, int P, float* dst, int row0, hipStream_t s);
+// W [N][K] -> the blocked W^T [ceil(N / DO)][K][DO] of the PKD_PRED / PKD_JOINT stage
+void pk_place_blocked(const float* src, int N, int K, int mode, float* dst, hipStream_t s);
 
 }  // namespace spt

@@ -47,7 +47,10 @@ def test_struct_layouts_match_header(tmp_path):
     """Every ctypes mirror has the size and field offsets gcc gives the header's structs."""
     import subprocess
     structs = {"spt_model_params": L.ModelParams, "spt_infer_params": L.InferParams, "spt_result": L.Result,
-               "spt_segment": L.Segment, "spt_model_info": L.ModelInfo, "spt_timings": L.Timings}
+               "spt_segment": L.Segment, "spt_model_info": L.ModelInfo, "spt_timings": L.Timings,
+               "spt_pk_model_params": L.PkModelParams, "spt_pk_infer_params": L.PkInferParams,
+               "spt_pk_segment": L.PkSegment, "spt_pk_result": L.PkResult, "spt_pk_model_info": L.PkModelInfo,
+               "spt_pk_timings": L.PkTimings}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
