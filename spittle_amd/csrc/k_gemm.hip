@@ -25,6 +25,7 @@
 #include "kernels.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 namespace spt {
@@ -438,6 +439,79 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Skinny GEMM (M <= 64 rows: a short streaming window, one utterance): the weight stream is the
+// whole cost, so the grid spreads W over >= 256 workgroups -- a workgroup owns 16 columns and a
+// K range (split-K over grid.y for the EPI_PARTIAL residual products), its 4 waves split that
+// range again.  Operands go straight from global memory into MFMA fragments
+// (v_mfma_f32_16x16x32_{bf16,f16}: a lane loads 16 B of one W row and 16 B of each 16-row A
+// block per k-step), four k-steps in flight; the waves' partial tiles are summed through LDS and
+// the epilogue is the shared epi_store.
+template <int EPI, bool F16, int MT>
+__global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g) {
+    __shared__ float red[4][MT * 16][17];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int fr = lane & 15, fq = lane >> 4;
+    const int n0 = blockIdx.x * 16;
+    const int Kc = g.K / g.ksplit, Kw = Kc / 4;
+    const int k0 = blockIdx.y * Kc + wid * Kw;
+    const bf16* wp = (const bf16*)g.W + (size_t)(n0 + fr) * g.ldw + k0 + 8 * fq;
+    const bf16* ap[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) ap[mt] = (const bf16*)g.A + (size_t)min(mt * 16 + fr, g.M - 1) * g.lda + k0 + 8 * fq;
+    f32x4 acc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int U = 4;
+    for (int k = 0; k < Kw; k += 32 * U) {
+        bf16x8 wf[U], af[U][MT];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int kk = min(k + 32 * u, Kw - 32);  // past the range: re-read, not accumulated below
+            wf[u] = *(const bf16x8*)(wp + kk);
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) af[u][mt] = *(const bf16x8*)(ap[mt] + kk);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (k + 32 * u >= Kw) break;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+                if constexpr (F16)
+                    acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, af[u][mt]),
+                                                                      __builtin_bit_cast(f16x8, wf[u]), acc[mt], 0, 0, 0);
+                else
+                    acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[u][mt], wf[u], acc[mt], 0, 0, 0);
+            }
+        }
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[wid][mt * 16 + 4 * fq + r][fr] = acc[mt][r];
+    __syncthreads();
+    typedef typename std::conditional<F16, f16, bf16>::type T;
+    for (int e = threadIdx.x; e < MT * 16 * 16; e += 256) {
+        const int row = e >> 4, c = e & 15;
+        if (row >= g.M) continue;
+        const float v = red[0][row][c] + red[1][row][c] + red[2][row][c] + red[3][row][c];
+        epi_store<T, EPI>(g, 0, row, epi_col<EPI>(g, n0 + c), v);
+    }
+}
+
+template <int EPI, bool F16>
+void launch_skinny(const GemmArgs& g, hipStream_t st) {
+    dim3 grid(g.N / 16, g.ksplit);
+    switch (cdiv(g.M, 16)) {
+        case 1: hipLaunchKernelGGL((gemm_skinny_kernel<EPI, F16, 1>), grid, dim3(256), 0, st, g); break;
+        case 2: hipLaunchKernelGGL((gemm_skinny_kernel<EPI, F16, 2>), grid, dim3(256), 0, st, g); break;
+        case 3: hipLaunchKernelGGL((gemm_skinny_kernel<EPI, F16, 3>), grid, dim3(256), 0, st, g); break;
+        case 4: hipLaunchKernelGGL((gemm_skinny_kernel<EPI, F16, 4>), grid, dim3(256), 0, st, g); break;
+        default: throw std::runtime_error("gemm_skinny: M > 64");
+    }
+    SPT_LAUNCH_CHECK();
+}
+
 template <int EPI, bool F16>
 void launch_256(const GemmArgs& g, int batch, hipStream_t st) {
     static bool attr = false;  // > 64 KiB dynamic LDS: set once per kernel
@@ -465,7 +539,7 @@ void gemm_nt_variant(int dtype, int epi, const GemmArgs& g, int batch, int varia
     const int esz = dtype == DT_F32 ? 4 : 2;
     if (g.ksplit < 1 || g.K % g.ksplit || (g.ksplit > 1 && epi != EPI_PARTIAL))
         throw std::runtime_error("gemm_nt: split-K needs EPI_PARTIAL and K % ksplit == 0");
-    if (g.N % BN != 0 || (g.K / g.ksplit * esz) % SLAB != 0 || g.M <= 0)
+    if (variant != 3 && (g.N % BN != 0 || (g.K / g.ksplit * esz) % SLAB != 0 || g.M <= 0))
         throw std::runtime_error("gemm_nt: unsupported shape M=" + std::to_string(g.M) + " N=" +
                                  std::to_string(g.N) + " K=" + std::to_string(g.K));
 #define SPT_GEMM_CASES(T)                                                          \
@@ -492,6 +566,24 @@ void gemm_nt_variant(int dtype, int epi, const GemmArgs& g, int batch, int varia
         case EPI_BIAS_F32: launch_256<EPI_BIAS_F32, F>(g, batch, st); return;      \
         case EPI_PARTIAL: launch_256<EPI_PARTIAL, F>(g, batch, st); return;        \
     }
+#define SPT_GEMM_SKINNY_CASES(F)                                                   \
+    switch (epi) {                                                                 \
+        case EPI_BIAS: launch_skinny<EPI_BIAS, F>(g, st); return;                  \
+        case EPI_BIAS_GELU: launch_skinny<EPI_BIAS_GELU, F>(g, st); return;        \
+        case EPI_BIAS_RESID: launch_skinny<EPI_BIAS_RESID, F>(g, st); return;      \
+        case EPI_BIAS_SWISH: launch_skinny<EPI_BIAS_SWISH, F>(g, st); return;      \
+        case EPI_BIAS_RELU: launch_skinny<EPI_BIAS_RELU, F>(g, st); return;        \
+        case EPI_BIAS_F32: launch_skinny<EPI_BIAS_F32, F>(g, st); return;          \
+        case EPI_PARTIAL: launch_skinny<EPI_PARTIAL, F>(g, st); return;            \
+    }
+    if (variant == 3) {  // skinny (M <= 64): bf16 / f16, N % 16, K / ksplit % 128
+        if (dtype == DT_F32 || g.M > 64 || g.N % 16 || (g.K / g.ksplit) % 128)
+            throw std::runtime_error("gemm_nt: skinny variant needs a 16-bit dtype, M <= 64, N % 16, (K / ksplit) % 128");
+        if (dtype == DT_F16) { SPT_GEMM_SKINNY_CASES(true) }
+        else { SPT_GEMM_SKINNY_CASES(false) }
+        throw std::runtime_error("gemm_nt: bad epilogue for the skinny variant");
+    }
+#undef SPT_GEMM_SKINNY_CASES
     static const bool force128 = getenv("SPT_GEMM128") != nullptr;  // A/B switch for measurements
     const bool use256 = variant == 2 || (variant == 0 && !force128);
     const bool fits32 = (int64_t)g.M * g.lda < (1ll << 31) && (int64_t)g.N * g.ldw < (1ll << 31);

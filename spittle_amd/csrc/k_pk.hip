@@ -421,10 +421,10 @@ __global__ __launch_bounds__(64) void rel_attn_mfma_kernel(const f16* __restrict
 }
 
 // ---------------------------------------------------------------- convolution module
-// a workgroup per 16 output frames of one utterance, a thread per channel: the GLU of the 16 + K - 1
-// frames it needs is computed once into registers (not once per tap), then the depthwise taps,
-// BatchNorm and Swish
-constexpr int CM_TT = 16;
+// a workgroup per 8 output frames x 256 channels of one utterance, a thread per channel: the GLU
+// of the 8 + K - 1 frames it needs is computed once into registers (not once per tap), then the
+// depthwise taps, BatchNorm and Swish
+constexpr int CM_TT = 8;
 template <typename T, int K>
 __global__ __launch_bounds__(256) void conv_module_kernel(const T* __restrict__ a, const int* __restrict__ lens, int Tp,
                                                           int d, const float* __restrict__ dw_w,
@@ -435,7 +435,9 @@ __global__ __launch_bounds__(256) void conv_module_kernel(const T* __restrict__ 
     const int T3 = lens[b * 4 + 3];
     const T* ab = a + (size_t)b * Tp * 2 * d;
     T* ob = out + (size_t)b * Tp * d;
-    for (int i = threadIdx.x; i < d; i += 256) {
+    {
+        const int i = blockIdx.z * 256 + threadIdx.x;
+        if (i >= d) return;
         float g[CM_TT + K - 1];
 #pragma unroll
         for (int f = 0; f < CM_TT + K - 1; ++f) {
@@ -859,7 +861,7 @@ void pk_conv_module(int dtype, const void* a, const int* lens, int B, int Tp, in
                     const float* dw_b, const float* bn_g, const float* bn_b, const float* bn_m, const float* bn_v,
                     void* out, hipStream_t st) {
     if (K != 9) throw std::runtime_error("pk_conv_module: depthwise kernel size 9 only");
-    dim3 grid(cdiv(Tp, CM_TT), B);
+    dim3 grid(cdiv(Tp, CM_TT), B, cdiv(d, 256));
     if (dtype == DT_F16)
         hipLaunchKernelGGL((conv_module_kernel<f16, 9>), grid, dim3(256), 0, st, (const f16*)a, lens, Tp, d, dw_w, dw_b,
                            bn_g, bn_b, bn_m, bn_v, (f16*)out);

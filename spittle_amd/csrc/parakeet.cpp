@@ -436,9 +436,18 @@ void ParakeetEngine::run_mel(const float* pcm_dev, int64_t stride, int B, int Tp
 // 1/2 FFN scale, by the LayerNorm that reads the residual next.  Returns the split used.
 int ParakeetEngine::gemm(int dt, int epi, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
                          const float* bias, void* Cp, int ldc, float alpha) {
-    static const int t256 = getenv("SPT_GEMM_T256") ? atoi(getenv("SPT_GEMM_T256")) : 96;
+    // SPT_GEMM_T256 / SPT_NO_SKINNY: read per call so tests can pin each variant (eager calls only:
+    // a captured encoder graph keeps the variants it was captured with)
+    const char* t256e = getenv("SPT_GEMM_T256");
+    const int t256 = t256e ? atoi(t256e) : 96;
+    const bool no_skinny = getenv("SPT_NO_SKINNY") != nullptr;
     int variant = 1, ks = 1;
-    if (dt != DT_F32 && N % 256 == 0 && K % 64 == 0) {
+    if (dt != DT_F32 && M <= 64 && N % 16 == 0 && K % 128 == 0 && !no_skinny) {
+        // skinny: >= 256 workgroups of 16 columns (residual products split K to get there)
+        variant = 3;
+        if (epi == EPI_PARTIAL)
+            while (ks < 8 && (N / 16) * ks < 256 && K % (2 * ks) == 0 && (K / (2 * ks)) % 128 == 0) ks *= 2;
+    } else if (dt != DT_F32 && N % 256 == 0 && K % 64 == 0) {
         const int64_t t = (int64_t)cdiv(M, 256) * (N / 256);
         int k2 = 1;
         if (epi == EPI_PARTIAL)

@@ -193,6 +193,23 @@ def test_encoder_f16_close_to_oracle(small16):
     assert rel < 4e-3, rel
 
 
+@pytest.mark.parametrize("variant", ["skinny", "tile128", "tile256"])
+def test_encoder_f16_gemm_variants(small16, variant, monkeypatch):
+    """Each fp16 GEMM path (skinny M <= 64, 128 x 128, 256 x 256) against the oracle: debug_encode
+    runs eagerly, and the tile thresholds are read per call."""
+    e, om = small16
+    if variant == "skinny":
+        pcm = synth_audio(30, 16000 * 3)            # 38 encoder frames
+    else:
+        pcm = synth_audio(31, 16000 * 8)            # 101 frames: M > 64
+        monkeypatch.setenv("SPT_GEMM_T256", "1" if variant == "tile256" else "1000000")
+    mel = P.mel(pcm)
+    g = e.debug_encode(mel)
+    o = om.encode(mel)
+    rel = np.sqrt(np.mean((g - o) ** 2) / np.mean(o ** 2))
+    assert rel < 4e-3, (variant, rel)
+
+
 def _fake_nemo(path, om, dims, n_layers):
     """A .nemo-shaped tar (config + torch state dict) from the oracle's tensors."""
     import torch
