@@ -54,6 +54,15 @@ __global__ void null_kernel(int* p) {
     if (threadIdx.x == 1023 && blockIdx.x == 100000) *p = 1;
 }
 
+// which XCD each block of a launch ran on (HW_REG_XCC_ID)
+__global__ void xcc_kernel(int* out) {
+    if (threadIdx.x == 0) {
+        unsigned v;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+        out[blockIdx.x] = (int)(v & 0xf);
+    }
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) {
         fprintf(stderr, "usage: ubench gemv|attn|gemm|layer|null ...\n");
@@ -70,6 +79,43 @@ int main(int argc, char** argv) {
         for (int g : {1, 80, 256, 1024}) {
             double us = time_us(st, iters, [&] { hipLaunchKernelGGL(null_kernel, dim3(g), dim3(256), 0, st, p); });
             printf("null grid=%d : %.2f us\n", g, us);
+        }
+        return 0;
+    }
+    if (what == "xcc") {
+        // block -> XCD placement over a sequence of dependent launches (graph and eager): is block b
+        // of every launch on XCD (x0 + b) % 8, and does x0 stay put from one launch to the next?
+        const int grids[] = {80, 240, 80, 80, 160, 160, 811, 64, 1, 80, 240, 160};
+        const int NG = sizeof(grids) / sizeof(int), REP = 4;
+        int* out = (int*)dalloc((size_t)NG * REP * 1024 * 4);
+        for (int mode = 0; mode < 2; ++mode) {
+            auto run = [&] {
+                for (int r = 0; r < REP; ++r)
+                    for (int i = 0; i < NG; ++i)
+                        hipLaunchKernelGGL(xcc_kernel, dim3(grids[i]), dim3(256), 0, st, out + (size_t)(r * NG + i) * 1024);
+            };
+            if (mode == 0) {
+                hipGraph_t gr;
+                hipGraphExec_t ge;
+                HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
+                run();
+                HIP_CHECK(hipStreamEndCapture(st, &gr));
+                HIP_CHECK(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
+                for (int k = 0; k < 3; ++k) HIP_CHECK(hipGraphLaunch(ge, st));
+            } else {
+                run();
+            }
+            HIP_CHECK(hipStreamSynchronize(st));
+            std::vector<int> h((size_t)NG * REP * 1024);
+            HIP_CHECK(hipMemcpy(h.data(), out, h.size() * 4, hipMemcpyDeviceToHost));
+            printf("xcc %s:", mode == 0 ? "graph" : "eager");
+            for (int l = 0; l < NG * REP; ++l) {
+                const int* o = h.data() + (size_t)l * 1024;
+                bool rr = true;
+                for (int b = 0; b < grids[l % NG]; ++b) rr = rr && o[b] == (o[0] + b) % 8;
+                printf(" %d:%d%s", grids[l % NG], o[0], rr ? "" : "!");
+            }
+            printf("\n");
         }
         return 0;
     }
