@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 6
+#define SPT_ABI_VERSION 7
 
 typedef enum {
     SPT_OK = 0,
@@ -340,6 +340,30 @@ spt_status spt_parakeet_debug_encode(spt_pk_ctx* ctx, const float* mel, int32_t 
 spt_status spt_parakeet_debug_decode(spt_pk_ctx* ctx, const float* enc, int32_t T3, int32_t max_symbols,
                                      spt_pk_result** out);
 spt_status spt_parakeet_debug_weight_checksum(spt_pk_ctx* ctx, int32_t tensor_id, double* out2);
+
+/* ================================================================================================
+ * ABI 7: the capture-side resampler.
+ *
+ * Replaces FrameResampler (src-tauri/src/audio_toolkit/audio/resampler.rs:7-104): rubato 0.16.2
+ * FftFixedIn<f32>(in_hz, out_hz, RESAMPLER_CHUNK_SIZE = 1024, 1, 1) behind 1024-sample input
+ * chunks, its output cut into frames of frame_samples (the recorder's 30 ms = 480 samples at
+ * 16 kHz, recorder.rs:264-268).  spt_resample runs one whole capture stream as
+ * FrameResampler::new + push(all samples) + finish (recorder.rs:330, 355): the concatenated
+ * frames, including finish's zero padding of the last input chunk and of the last frame.
+ * in_hz == out_hz: frames of the input, as FrameResampler does without rubato.
+ * ============================================================================================== */
+typedef struct spt_resampler spt_resampler;
+spt_status spt_resampler_create(int32_t in_hz, int32_t out_hz, int32_t frame_samples, int32_t device,
+                                spt_resampler** out, char* err, size_t errlen);
+/* rubato's unit sizes (0 when in_hz == out_hz) */
+spt_status spt_resampler_info(const spt_resampler* r, int32_t* fft_size_in, int32_t* fft_size_out);
+/* samples spt_resample writes for an n-sample stream (a multiple of frame_samples) */
+size_t spt_resample_output_len(const spt_resampler* r, size_t n_samples);
+/* pcm: host samples (borrowed); out: host buffer of at least spt_resample_output_len samples */
+spt_status spt_resample(spt_resampler* r, const float* pcm, size_t n_samples, float* out, size_t out_cap,
+                        size_t* n_out);
+const char* spt_resampler_last_error(const spt_resampler* r);
+void spt_resampler_destroy(spt_resampler* r);
 
 #ifdef __cplusplus
 }

@@ -6,7 +6,7 @@
 
 use std::os::raw::{c_char, c_int, c_void};
 
-pub const SPT_ABI_VERSION: c_int = 6;
+pub const SPT_ABI_VERSION: c_int = 7;
 
 pub type spt_status = c_int;
 pub const SPT_OK: spt_status = 0;
@@ -284,6 +284,35 @@ extern "C" {
         out: *mut *mut spt_pk_result,
     ) -> spt_status;
     pub fn spt_parakeet_debug_weight_checksum(ctx: *mut spt_pk_ctx, tensor_id: i32, out2: *mut f64) -> spt_status;
+
+    // ---- ABI 7: capture-side resampler (audio_toolkit/audio/resampler.rs FrameResampler)
+    pub fn spt_resampler_create(
+        in_hz: i32,
+        out_hz: i32,
+        frame_samples: i32,
+        device: i32,
+        out: *mut *mut spt_resampler,
+        err: *mut c_char,
+        errlen: usize,
+    ) -> spt_status;
+    pub fn spt_resampler_info(r: *const spt_resampler, fft_size_in: *mut i32, fft_size_out: *mut i32) -> spt_status;
+    pub fn spt_resample_output_len(r: *const spt_resampler, n_samples: usize) -> usize;
+    pub fn spt_resample(
+        r: *mut spt_resampler,
+        pcm: *const f32,
+        n_samples: usize,
+        out: *mut f32,
+        out_cap: usize,
+        n_out: *mut usize,
+    ) -> spt_status;
+    pub fn spt_resampler_last_error(r: *const spt_resampler) -> *const c_char;
+    pub fn spt_resampler_destroy(r: *mut spt_resampler);
+}
+
+/// Opaque capture-side resampler context (ABI 7).
+#[repr(C)]
+pub struct spt_resampler {
+    _private: [u8; 0],
 }
 
 // ---- ABI 6: Parakeet-V3 types

@@ -33,6 +33,9 @@ EXPORTS = [
     "spt_parakeet_transcribe_batch_device", "spt_parakeet_result_free", "spt_parakeet_get_timings",
     "spt_parakeet_debug_mel", "spt_parakeet_debug_encode", "spt_parakeet_debug_decode",
     "spt_parakeet_debug_weight_checksum",
+    # ABI 7: capture-side resampler
+    "spt_resampler_create", "spt_resampler_info", "spt_resample_output_len", "spt_resample",
+    "spt_resampler_last_error", "spt_resampler_destroy",
 ]
 SPT_PK_WEIGHTS_EMPTY = 1
 SPT_PK_TS_TOKEN, SPT_PK_TS_WORD, SPT_PK_TS_SEGMENT = 0, 1, 2
@@ -186,6 +189,19 @@ def load():
     L.spt_parakeet_debug_encode.argtypes = [vp, fp, C.c_int32, fp]
     L.spt_parakeet_debug_decode.argtypes = [vp, fp, C.c_int32, C.c_int32, PR]
     L.spt_parakeet_debug_weight_checksum.argtypes = [vp, C.c_int32, C.POINTER(C.c_double)]
+    L.spt_resampler_create.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.POINTER(vp), C.c_char_p,
+                                       C.c_size_t]
+    L.spt_resampler_create.restype = C.c_int
+    L.spt_resampler_info.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    L.spt_resampler_info.restype = C.c_int
+    L.spt_resample_output_len.argtypes = [vp, C.c_size_t]
+    L.spt_resample_output_len.restype = C.c_size_t
+    L.spt_resample.argtypes = [vp, fp, C.c_size_t, fp, C.c_size_t, C.POINTER(C.c_size_t)]
+    L.spt_resample.restype = C.c_int
+    L.spt_resampler_last_error.argtypes = [vp]
+    L.spt_resampler_last_error.restype = C.c_char_p
+    L.spt_resampler_destroy.argtypes = [vp]
+    L.spt_resampler_destroy.restype = None
     for fn in EXPORTS:
         if fn.startswith("spt_parakeet_") and fn not in ("spt_parakeet_default_model_params",
                                                           "spt_parakeet_default_infer_params", "spt_parakeet_destroy",

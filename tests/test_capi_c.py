@@ -24,7 +24,7 @@ def test_c_program_compiles_and_links(tmp_path):
     exe = _build(tmp_path)
     r = subprocess.run([exe, "synthetic:tiny", "--link-only"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
-    assert "ABI 6" in r.stdout
+    assert "ABI 7" in r.stdout
 
 
 @pytest.mark.gpu
