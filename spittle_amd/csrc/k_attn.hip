@@ -190,7 +190,20 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16* __restric
 // fragment (S^T = K . Q^T) and every V^T fragment (O^T += V^T . P^T) read from LDS feeds two
 // MFMAs instead of one, halving the LDS fragment traffic per flop, and a workgroup (256 queries)
 // stages each K/V tile for twice the queries, halving the L2 -> LDS traffic.
-template <int SUM>  // row sums: 0 packed f32 VALU, 1 scalar f32 VALU, 2 an MFMA with a ones operand
+// K-tile chunk swizzle: a ds_read_b128 serves 16 lanes (rows r0..r0+15 of one 16-byte chunk
+// column) per pass from one 256-byte bank window; rows are 128 B, so rows r and r + 8 share their
+// window half, and (r & 7) gives them the same slot (2-way conflict on every K read).  SW = 1
+// keys the swizzle on (r >> 1) & 7 instead: 16 distinct slots per pass.
+// V tiles (read by ds_read_b64_tr_b16: a pass covers keys k0..k0+3 x four 8-byte pieces of
+// two adjacent 16-byte chunk pairs) are unswizzled at SW bit 1 clear: keys k and k + 2 share
+// their bank-window half and slot (2-way).  SW bit 1 XORs the chunk index with 4 on keys with
+// bit 1 set: the 32 lanes of a pass then cover all 32 8-byte positions of the window.
+template <int SW>
+__device__ __forceinline__ int kswz(int r) { return (SW & 1) ? ((r >> 1) & 7) : (r & 7); }
+template <int SW>
+__device__ __forceinline__ int vswz(int r) { return (SW & 2) ? ((r & 2) << 1) : 0; }
+
+template <int SUM, int SW = 1>  // row sums: 0 packed f32 VALU, 1 scalar f32 VALU, 2 an MFMA with a ones operand
 __global__ __launch_bounds__(256, 2) void attn_bf16_q64_kernel(const bf16* __restrict__ qkv, int T, int H,
                                                                bf16* __restrict__ out) {
     __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128];  // [buf][K|V][64 keys][128 B]
@@ -219,8 +232,8 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_q64_kernel(const bf16* __res
             const int rt = 8 * p + prow;
             const int key = min(kt * 64 + rt, T - 1);
             const bf16* kr = base + (size_t)key * ld + d + h * 64;
-            glds16(kr + 8 * (pch ^ (rt & 7)), lds_k(buf) + p * 1024);
-            glds16(kr + d + 8 * pch, lds_v(buf) + p * 1024);
+            glds16(kr + 8 * (pch ^ kswz<SW>(rt)), lds_k(buf) + p * 1024);
+            glds16(kr + d + 8 * (pch ^ vswz<SW>(rt)), lds_v(buf) + p * 1024);
         }
     };
 
@@ -256,7 +269,7 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_q64_kernel(const bf16* __res
 #pragma unroll
             for (int st = 0; st < 4; ++st) {
                 const int c = 2 * st + hf;
-                const bf16x8 a = *(const SPT_LDS bf16x8*)(lk + row * 128 + ((c ^ (row & 7)) << 4));
+                const bf16x8 a = *(const SPT_LDS bf16x8*)(lk + row * 128 + ((c ^ kswz<SW>(row)) << 4));
                 s[0][kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[0][st], s[0][kt2], 0, 0, 0);
                 s[1][kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[1][st], s[1][kt2], 0, 0, 0);
             }
@@ -335,10 +348,11 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_q64_kernel(const bf16* __res
 #pragma unroll
                 for (int sp = 0; sp < 2; ++sp) {
                     const int key0 = 32 * kt2 + 16 * sp + 4 * hf + (i16 >> 2);
+                    const int cb = col * 2;  // byte in the V row: chunk cb >> 4, 8-byte half cb & 8
                     const bf16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (SPT_LDS bf16x4v*)(lv + key0 * 128 + col * 2));
+                        (SPT_LDS bf16x4v*)(lv + key0 * 128 + ((((cb >> 4) ^ vswz<SW>(key0)) << 4) | (cb & 15))));
                     const bf16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (SPT_LDS bf16x4v*)(lv + (key0 + 8) * 128 + col * 2));
+                        (SPT_LDS bf16x4v*)(lv + (key0 + 8) * 128 + ((((cb >> 4) ^ vswz<SW>(key0 + 8)) << 4) | (cb & 15))));
                     bf16x8 va;
                     va[0] = lo[0]; va[1] = lo[1]; va[2] = lo[2]; va[3] = lo[3];
                     va[4] = hi[0]; va[5] = hi[1]; va[6] = hi[2]; va[7] = hi[3];
@@ -495,11 +509,14 @@ __global__ __launch_bounds__(256, 1) void attn_f32_kernel(const float* __restric
 void enc_attention(int dtype, const void* qkv, int B, int T, int H, void* out, hipStream_t st) {
     static const bool q32 = getenv("SPT_ATTN_Q32") != nullptr;  // A/B switch: 32 queries per wave
     static const int sum = getenv("SPT_ATTN_SUM") ? atoi(getenv("SPT_ATTN_SUM")) : 0;
+    static const int swz = getenv("SPT_ATTN_SWZ") ? atoi(getenv("SPT_ATTN_SWZ")) : 1;
     if (dtype == DT_BF16 && !q32) {
         dim3 g(cdiv(T, 256), H, B);
         if (sum == 1) hipLaunchKernelGGL(attn_bf16_q64_kernel<1>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
         else if (sum == 2) hipLaunchKernelGGL(attn_bf16_q64_kernel<2>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
-        else hipLaunchKernelGGL(attn_bf16_q64_kernel<0>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
+        else if (swz == 0) hipLaunchKernelGGL((attn_bf16_q64_kernel<0, 0>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
+        else if (swz == 1) hipLaunchKernelGGL((attn_bf16_q64_kernel<0, 1>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
+        else hipLaunchKernelGGL((attn_bf16_q64_kernel<0, 3>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
         return;
     }
     dim3 grid(cdiv(T, 128), H, B);
