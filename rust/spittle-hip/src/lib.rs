@@ -1,5 +1,5 @@
 //! `HipWhisperEngine` and `HipParakeetEngine`: the `transcribe_rs::TranscriptionEngine` surfaces
-//! Spittle binds to, backed by the MI355X-native library (`libspittle_hip.so`, C ABI 6).
+//! Spittle binds to, backed by the MI355X-native library (`libspittle_hip.so`, C ABI 7), plus `HipFrameResampler`.
 //!
 //! What it replaces in the app (/root/reference/src-tauri/src/managers/transcription.rs):
 //!
@@ -457,5 +457,62 @@ impl TranscriptionEngine for HipParakeetEngine {
 impl Drop for HipParakeetEngine {
     fn drop(&mut self) {
         self.unload_model();
+    }
+}
+
+/// The capture-side resampler (ABI 7): `FrameResampler` of
+/// /root/reference/src-tauri/src/audio_toolkit/audio/resampler.rs:7-104 over the device.
+/// `process_stream` = `FrameResampler::new(in_hz, out_hz, frame_dur)` + `push(all)` + `finish`
+/// (recorder.rs:264-268, 330, 355): the concatenated frames of one recorded stream.  The app's
+/// streaming `push` per capture buffer stays on the host; a recording-level caller (or a batch
+/// re-import of a file) hands the whole stream over at once.
+pub struct HipFrameResampler {
+    r: *mut sys::spt_resampler,
+}
+
+// SAFETY: the context selects its device on every call and holds no thread-local state
+unsafe impl Send for HipFrameResampler {}
+
+impl HipFrameResampler {
+    pub fn new(in_hz: u32, out_hz: u32, frame_dur: std::time::Duration, device: i32) -> Result<Self, Box<dyn Error>> {
+        let frame_samples = (out_hz as f64 * frame_dur.as_secs_f64()).round() as i32;
+        if frame_samples <= 0 {
+            return Err("frame duration too short".into());
+        }
+        let mut r = std::ptr::null_mut();
+        let mut err = vec![0 as c_char; 512];
+        // SAFETY: out-pointer and error buffer are valid for the call
+        let st = unsafe {
+            sys::spt_resampler_create(in_hz as i32, out_hz as i32, frame_samples, device, &mut r, err.as_mut_ptr(), err.len())
+        };
+        if st != sys::SPT_OK {
+            // SAFETY: the library NUL-terminates the message inside the buffer
+            let msg = unsafe { CStr::from_ptr(err.as_ptr()) }.to_string_lossy().into_owned();
+            return Err(status_error("resampler", st, msg));
+        }
+        Ok(Self { r })
+    }
+
+    pub fn process_stream(&mut self, samples: &[f32]) -> Result<Vec<f32>, Box<dyn Error>> {
+        // SAFETY: a live context; the length query has no other effect
+        let need = unsafe { sys::spt_resample_output_len(self.r, samples.len()) };
+        let mut out = vec![0f32; need];
+        let mut n_out = 0usize;
+        // SAFETY: both buffers outlive the call and `out` holds `need` samples
+        let st = unsafe { sys::spt_resample(self.r, samples.as_ptr(), samples.len(), out.as_mut_ptr(), out.len(), &mut n_out) };
+        if st != sys::SPT_OK {
+            // SAFETY: the message lives in the context until its next call
+            let msg = unsafe { CStr::from_ptr(sys::spt_resampler_last_error(self.r)) }.to_string_lossy().into_owned();
+            return Err(status_error("resample", st, msg));
+        }
+        out.truncate(n_out);
+        Ok(out)
+    }
+}
+
+impl Drop for HipFrameResampler {
+    fn drop(&mut self) {
+        // SAFETY: created by spt_resampler_create, destroyed once
+        unsafe { sys::spt_resampler_destroy(self.r) };
     }
 }

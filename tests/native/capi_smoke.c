@@ -81,6 +81,35 @@ static int one_session(const char* spec, const float* pcm, size_t n) {
     return 0;
 }
 
+/* HipFrameResampler (rust/spittle-hip): create 48 kHz -> 16 kHz with 30 ms frames, one stream,
+ * destroy; the output length rule of FrameResampler::finish (resampler.rs:66-86) */
+static int resampler_session(void) {
+    spt_resampler* r = NULL;
+    char err[256] = {0};
+    CHECK(spt_resampler_create(48000, 16000, 480, 0, &r, err, sizeof err) == SPT_OK && r, err);
+    int32_t nin = 0, nout = 0;
+    CHECK(spt_resampler_info(r, &nin, &nout) == SPT_OK && nin == 1026 && nout == 342, "rubato unit sizes");
+    const size_t n = 48000 * 2 + 100;
+    float* x = (float*)malloc(n * sizeof(float));
+    for (size_t i = 0; i < n; ++i) x[i] = 0.5f * sinf(2.0f * 3.14159265f * 1000.0f * (float)i / 48000.0f);
+    const size_t need = spt_resample_output_len(r, n);
+    /* ceil(n / 1024) chunks of 1024 -> floor(. / 1026) units of 342 -> whole 480-sample frames */
+    const size_t units = ((n + 1023) / 1024 * 1024) / 1026;
+    CHECK(need == (units * 342 + 479) / 480 * 480, "output length");
+    float* y = (float*)malloc(need * sizeof(float));
+    size_t got = 0;
+    CHECK(spt_resample(r, x, n, y, need - 1, &got) == SPT_ERR_INVALID_ARG, "short output buffer");
+    CHECK(spt_resample(r, x, n, y, need, &got) == SPT_OK && got == need, spt_resampler_last_error(r));
+    double e = 0.0;
+    for (size_t i = 8000; i < 24000; ++i) e += (double)y[i] * y[i];
+    CHECK(fabs(sqrt(e / 16000.0) - 0.5 / sqrt(2.0)) < 2e-3, "1 kHz tone keeps its amplitude");
+    free(x);
+    free(y);
+    spt_resampler_destroy(r);
+    CHECK(spt_resampler_create(10, 16000, 480, 0, &r, err, sizeof err) == SPT_ERR_INVALID_ARG && !r, "bad rate");
+    return 0;
+}
+
 int main(int argc, char** argv) {
     const char* spec = argc > 1 ? argv[1] : "synthetic:tiny";
     printf("%s\n", spt_version());
@@ -96,6 +125,7 @@ int main(int argc, char** argv) {
                  0.05f * sinf(2.0f * 3.14159265f * 1234.5f * (float)i / 16000.0f);
     int rc = one_session(spec, pcm, n);
     if (!rc) rc = one_session(spec, pcm, n); /* unload, then load again */
+    if (!rc) rc = resampler_session();
     free(pcm);
     if (!rc) printf("capi_smoke ok\n");
     return rc;
