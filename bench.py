@@ -313,6 +313,44 @@ def parakeet_bench(device: int, steps: int, warmup: int, with_cpu: bool) -> dict
     return out
 
 
+def resampler_bench(device: int, with_cpu: bool) -> dict:
+    """Capture-side resampler (ABI 7): one 48 kHz capture stream per call (8 x 30 s
+    concatenated, host buffer in, 16 kHz frames out), FrameResampler::new + push(all) + finish.
+    Roofline: the unit GEMM's f32 MFMA FLOPs (2 * Kp * Np per rubato unit) over the call time."""
+    import numpy as np
+    from spittle_amd.resampler import FrameResampler
+    fin, secs = 48000, 240.0
+    rng = np.random.default_rng(1000)
+    x = np.clip(0.1 * rng.standard_normal(int(fin * secs)), -1, 1).astype(np.float32)
+    r = FrameResampler(fin, 16000, 0.030, device)
+    nin, nout = r.fft_sizes
+    for _ in range(2):
+        r.process_stream(x)
+    ts = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        r.process_stream(x)
+        ts.append(time.perf_counter() - t0)
+    t = sorted(ts)[len(ts) // 2]
+    units = (-(-len(x) // 1024) * 1024) // nin
+    kp, np_ = -(-nin // 32) * 32, -(-(2 * nout) // 128) * 128
+    flops = 2.0 * units * kp * np_
+    out = {"workload": f"one {secs:.0f} s 48 kHz stream -> 16 kHz 30 ms frames (rubato FftFixedIn units {nin}->{nout})",
+           "rtfx": round(secs / t, 1), "ms_per_call_median": round(t * 1e3, 3),
+           "gemm_roofline": {"bound": "mfma", "flops_per_call": flops, "achieved_tflops_whole_call": round(flops / t / 1e12, 2),
+                             "peak": 157.3, "unit": "TFLOP/s", "note": "whole call incl. H2D/D2H of the host buffers"}}
+    if with_cpu:
+        from oracle import resampler as R
+        xs = x[: fin * 30].astype(np.float64)
+        t0 = time.perf_counter()
+        R.resample_fast(xs, fin, 16000)
+        tc = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(30.0 / tc, 1), "unit": "audio-sec/wall-sec", "cores": 1, "kind": "port",
+                               "sample": "30 s of the same stream, numpy restatement of FftFixedIn (f64, block-parallel)"}
+    r.close()
+    return out
+
+
 def app_latency(eng, dur_s=(5, 10, 30)) -> dict:
     """The app's real call (transcription.rs:494-503): one utterance (B = 1), whisper_full with
     its default parameters (timestamps on, temperature fallback 0.2 / best_of 5), language
@@ -451,6 +489,9 @@ def main():
             app = app_latency(eng)
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.model, args.decode_steps)
+    rs = None
+    if rank == 0 and world == 1 and not args.no_parakeet:
+        rs = resampler_bench(local, not args.no_cpu_baseline)
     pk = None
     if rank == 0 and world == 1 and not args.no_parakeet:
         eng.unload_model()  # free the Whisper arenas first
@@ -481,6 +522,8 @@ def main():
             out["weight_load"] = wload
         if pk:
             out["parakeet_v3"] = pk
+        if rs:
+            out["resampler"] = rs
         print(json.dumps(out), flush=True)
     eng.unload_model()
     if world > 1:

@@ -13,7 +13,7 @@ tag = sys.argv[1] if len(sys.argv) > 1 else "r1"
 SEL = {
     "dec_cross_attn": lambda n: re.search(r"cross_attn_kernel<unsigned short, 1[,>]", n) is not None,
     "dec_logits": lambda n: "gemv_kernel<unsigned short, 4," in n,
-    "enc_fc1_gemm": lambda n: "gemm256_kernel<1>" in n,
+    "enc_fc1_gemm": lambda n: re.search(r"gemm256_kernel<1[,>]", n) is not None,
     # decoder GEMVs (template <T, MODE, ASRC, RG, ...>; MODE 0 bias, 1 bias+GELU, 2 partial, 3 QKV+cache,
     # 5 bias+residual; ASRC 0 direct, 16 + n LayerNorm over x + n pending slabs), batch 8 (RG 1)
     "dec_qkv": lambda n: "gemv_kernel<unsigned short, 3, 18, 1," in n,
