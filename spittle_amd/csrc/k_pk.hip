@@ -421,47 +421,63 @@ __global__ __launch_bounds__(64) void rel_attn_mfma_kernel(const f16* __restrict
 }
 
 // ---------------------------------------------------------------- convolution module
-// a workgroup per 8 output frames x 256 channels of one utterance, a thread per channel: the GLU
-// of the 8 + K - 1 frames it needs is computed once into registers (not once per tap), then the
-// depthwise taps, BatchNorm and Swish
-constexpr int CM_TT = 8;
+// a workgroup per 8 output frames x 1024 channels of one utterance, a thread per 4 adjacent
+// channels (8- / 16-byte loads and stores instead of one element per lane): the GLU of the
+// 8 + K - 1 frames it needs is computed once into registers (not once per tap), then the
+// depthwise taps, BatchNorm and Swish.  Sigmoids are exp2 + rcp (common.h sigmoidf_ / swish).
+constexpr int CM_TT = 8, CM_V = 4;
+template <typename T> struct Vec4;
+template <> struct Vec4<f16> { typedef __attribute__((ext_vector_type(4))) _Float16 type; };
+template <> struct Vec4<bf16> { typedef bf16x4v type; };
+template <> struct Vec4<float> { typedef f32x4 type; };
 template <typename T, int K>
 __global__ __launch_bounds__(256) void conv_module_kernel(const T* __restrict__ a, const int* __restrict__ lens, int Tp,
                                                           int d, const float* __restrict__ dw_w,
                                                           const float* __restrict__ dw_b, const float* __restrict__ bn_g,
                                                           const float* __restrict__ bn_b, const float* __restrict__ bn_m,
                                                           const float* __restrict__ bn_v, T* __restrict__ out) {
+    typedef typename Vec4<T>::type V4;
     const int t0 = blockIdx.x * CM_TT, b = blockIdx.y;
     const int T3 = lens[b * 4 + 3];
     const T* ab = a + (size_t)b * Tp * 2 * d;
     T* ob = out + (size_t)b * Tp * d;
-    {
-        const int i = blockIdx.z * 256 + threadIdx.x;
-        if (i >= d) return;
-        float g[CM_TT + K - 1];
+    const int i = (blockIdx.z * 256 + threadIdx.x) * CM_V;  // first of this thread's 4 channels
+    if (i >= d) return;
+    float g[CM_TT + K - 1][CM_V];
 #pragma unroll
-        for (int f = 0; f < CM_TT + K - 1; ++f) {
-            const int tt = t0 - K / 2 + f;
-            g[f] = 0.0f;
-            if (tt >= 0 && tt < T3) {
-                const float x = to_f<T>(ab[(size_t)tt * 2 * d + i]), gate = to_f<T>(ab[(size_t)tt * 2 * d + d + i]);
-                g[f] = x * (1.0f / (1.0f + expf(-gate)));  // GLU
-            }
+    for (int f = 0; f < CM_TT + K - 1; ++f) {
+        const int tt = t0 - K / 2 + f;
+#pragma unroll
+        for (int c = 0; c < CM_V; ++c) g[f][c] = 0.0f;
+        if (tt >= 0 && tt < T3) {
+            const V4 x = *(const V4*)(ab + (size_t)tt * 2 * d + i), gate = *(const V4*)(ab + (size_t)tt * 2 * d + d + i);
+#pragma unroll
+            for (int c = 0; c < CM_V; ++c) g[f][c] = to_f<T>((T)x[c]) * sigmoidf_(to_f<T>((T)gate[c]));  // GLU
         }
-        float wk[K];
+    }
+    float wk[CM_V][K], bs[CM_V], bt[CM_V], bias[CM_V];
 #pragma unroll
-        for (int j = 0; j < K; ++j) wk[j] = dw_w[i * K + j];
-        const float bs = bn_g[i] / sqrtf(bn_v[i] + 1e-5f), bt = bn_b[i] - bn_m[i] * bs, bias = dw_b[i];
+    for (int c = 0; c < CM_V; ++c) {
 #pragma unroll
-        for (int f = 0; f < CM_TT; ++f) {
-            const int t = t0 + f;
-            if (t >= Tp) break;
-            float acc = bias;
+        for (int j = 0; j < K; ++j) wk[c][j] = dw_w[(i + c) * K + j];
+        bs[c] = bn_g[i + c] / sqrtf(bn_v[i + c] + 1e-5f);
+        bt[c] = bn_b[i + c] - bn_m[i + c] * bs[c];
+        bias[c] = dw_b[i + c];
+    }
 #pragma unroll
-            for (int j = 0; j < K; ++j) acc += wk[j] * g[f + j];
-            const float z = acc * bs + bt;
-            ob[(size_t)t * d + i] = from_f<T>(t < T3 ? z / (1.0f + expf(-z)) : 0.0f);  // Swish
+    for (int f = 0; f < CM_TT; ++f) {
+        const int t = t0 + f;
+        if (t >= Tp) break;
+        V4 o;
+#pragma unroll
+        for (int c = 0; c < CM_V; ++c) {
+            float acc = bias[c];
+#pragma unroll
+            for (int j = 0; j < K; ++j) acc += wk[c][j] * g[f + j][c];
+            const float z = acc * bs[c] + bt[c];
+            o[c] = from_f<T>(t < T3 ? swish(z) : 0.0f);  // Swish
         }
+        *(V4*)(ob + (size_t)t * d + i) = o;
     }
 }
 
@@ -861,7 +877,8 @@ void pk_conv_module(int dtype, const void* a, const int* lens, int B, int Tp, in
                     const float* dw_b, const float* bn_g, const float* bn_b, const float* bn_m, const float* bn_v,
                     void* out, hipStream_t st) {
     if (K != 9) throw std::runtime_error("pk_conv_module: depthwise kernel size 9 only");
-    dim3 grid(cdiv(Tp, CM_TT), B, cdiv(d, 256));
+    if (d % CM_V) throw std::runtime_error("pk_conv_module: channels must be a multiple of 4");
+    dim3 grid(cdiv(Tp, CM_TT), B, cdiv(d, 256 * CM_V));
     if (dtype == DT_F16)
         hipLaunchKernelGGL((conv_module_kernel<f16, 9>), grid, dim3(256), 0, st, (const f16*)a, lens, Tp, d, dw_w, dw_b,
                            bn_g, bn_b, bn_m, bn_v, (f16*)out);
