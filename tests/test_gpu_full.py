@@ -87,6 +87,22 @@ def test_multi_window_seek(tiny):
     assert r.n_windows >= 2
 
 
+@pytest.mark.parametrize("seconds,seed", [(75, 72), (100, 74)])
+def test_long_input_seek_loop(tiny, seconds, seed):
+    """Inputs of 3-4+ windows: the seek loop, prompt_past conditioning across windows and segment
+    times relative to each window's seek, against the oracle's whisper_full restatement."""
+    e, om = tiny
+    n = int(seconds * 16000)
+    x = np.concatenate([O.synth_audio(seed + k) for k in range((n + 479999) // 480000)])[:n]
+    p = W.Params(max_tokens=16)
+    r = e.transcribe_samples(x, _params(max_new_tokens=16))
+    wins, segs, toks, _ = W.transcribe(om, x, p)
+    assert len(wins) >= 3
+    if _compare(r, wins, segs, toks):
+        assert r.n_windows == len(wins)
+    assert r.n_windows >= 3
+
+
 def test_too_short_and_empty(tiny):
     e, _ = tiny
     for n in (0, 100, 15000):  # < 1 s: whisper_full decodes nothing
