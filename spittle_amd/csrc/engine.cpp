@@ -107,7 +107,10 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     HIP_CHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     ev_.resize(8);
     for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
-    groups_.resize(n_groups_);
+    // a decoder pass stages at most max_rows_ rows in its LayerNorm GEMVs' LDS images; a batch
+    // above that is decoded as several groups (each sized for the whole batch, re-sliced per call)
+    max_rows_ = gemv_max_image_rows(dt_, dm_.d);
+    groups_.resize(std::max(n_groups_, cdiv(max_batch_, max_rows_)));
     for (auto& g : groups_) {
         HIP_CHECK(hipStreamCreateWithFlags(&g.st, hipStreamNonBlocking));
         HIP_CHECK(hipEventCreateWithFlags(&g.ev, hipEventDisableTiming));
@@ -809,11 +812,15 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
     const int P = rq.row_prefix.empty() ? (int)rq.prefix.size() : (int)rq.row_prefix[0].size();
     if (Tq < 1 || Tq > 4) throw std::runtime_error("prompt must have 1..4 tokens");
     if (B < 1 || B > 64) throw std::runtime_error("batch out of range");
-    // decoder passes carry at most 64 rows: a batch whose prompt rows exceed that prefills the
-    // prompt a chunk of tokens at a time (the same rows, positions and keys) and runs the
-    // logits pass on the last prompt token alone
-    const int cmax = std::max(1, std::min(4, 64 / B));
-    const int Tq_head = B * Tq > 64 ? 1 : Tq;
+    // decoder passes carry at most max_rows_ rows: a batch above that is split over decode
+    // groups, and a group whose prompt rows exceed it prefills the prompt a chunk of tokens at a
+    // time (the same rows, positions and keys) and runs the logits pass on the last prompt token
+    // alone
+    const int G = std::min((int)groups_.size(), std::max(std::min(n_groups_, B), cdiv(B, max_rows_)));
+    const int Bg = cdiv(B, G);  // the largest group
+    if (Bg > max_rows_) throw std::runtime_error("batch exceeds the decoder's rows per pass");
+    const int cmax = std::max(1, std::min(4, max_rows_ / Bg));
+    const int Tq_head = Bg * Tq > max_rows_ ? 1 : Tq;
     if (P > ctx / 2 + 1) throw std::runtime_error("prompt prefix longer than n_text_ctx / 2 + 1");
     for (int t : rq.prefix)
         if (t < 0 || t >= dm_.n_vocab) throw std::runtime_error("prompt token out of the vocabulary");
@@ -852,7 +859,6 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         }
     }
     // split the batch over the decode groups; each waits for the encoder / cross-K/V
-    const int G = std::min(n_groups_, B);
     HIP_CHECK(hipEventRecord(ev_[6], st_));
     std::vector<DecGroup*> act;
     for (int gi = 0, b0 = 0; gi < G; ++gi) {
@@ -947,7 +953,7 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
             dec_advance(g.ds, n, g.st);
         }
         auto prompt_tok = [&](int b, int t) { return (t == 1 && lang[b] >= 0) ? lang[b] : rq.prompt[t]; };
-        for (int c0 = 0; c0 < Tq - Tq_head; c0 += cmax) {  // only when B * Tq > 64
+        for (int c0 = 0; c0 < Tq - Tq_head; c0 += cmax) {  // only when Bg * Tq > max_rows_
             const int n = std::min(cmax, Tq - Tq_head - c0);
             upload_tokens(g, [&](int b, int t) { return prompt_tok(b, c0 + t); }, n);
             dec_embed(dt_, g.tok_in, g.B * n, n, dm_.d, tok_emb_, dec_pos_, g.ds, g.dx, g.st);
@@ -1109,6 +1115,9 @@ void Engine::beam_begin(const float* const* pcm, const int* n_samples, int B, co
     require_weights();
     if (rq.beam_k < 1 || rq.beam_k > 8) throw std::runtime_error("beam size must be in 1..8");
     if (n_groups_ != 1) throw std::runtime_error("beam search needs one decode group");
+    if (B > max_rows_)
+        throw std::runtime_error("beam search rows (utterances x beam_size) exceed the decoder's " +
+                                 std::to_string(max_rows_) + " rows per pass for this model");
     if (!kvtmp_) {
         const size_t bytes = (size_t)dm_.n_dec * 2 * max_batch_ * dm_.n_head * dm_.n_text_ctx * 64 * esz_;
         if (hipMalloc(&kvtmp_, bytes) != hipSuccess) {

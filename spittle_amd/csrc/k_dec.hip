@@ -1093,6 +1093,13 @@ void gemv_prepare(int dtype) {
     else gemv_attr_modes<float>();
 }
 
+int gemv_max_image_rows(int dtype, int K) {
+    const int esz = dtype == DT_BF16 ? 2 : 4;
+    int r = 64;
+    while (r > 1 && gv_img_bytes(r, K, esz) > GV_LDS_BYTES) --r;
+    return r;
+}
+
 void gemv(int dtype, int mode, int asrc, const GemvArgs& a_in, hipStream_t st) {
     if (a_in.R > 64 || a_in.R <= 0) throw std::runtime_error("gemv: rows must be in 1..64");
     const int ks = dtype == DT_BF16 ? 128 : 64;

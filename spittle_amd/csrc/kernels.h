@@ -127,6 +127,9 @@ constexpr int kMaxPend = 4;
 void gemv(int dtype, int mode, int asrc, const GemvArgs& a, hipStream_t st);
 // one-time per-process kernel attributes (call before any stream capture)
 void gemv_prepare(int dtype);
+// rows a LayerNorm / attention-merge GEMV can stage for K columns (its LDS image budget): the
+// decoder's rows per pass (large-v3 bf16: 38; f32 small: 31; <= 64)
+int gemv_max_image_rows(int dtype, int K);
 
 // x[b*Tq + t] = tok_emb[tok[b*Tq+t]] + pos_emb[pos0 + t]
 void dec_embed(int dtype, const int* tok, int R, int Tq, int d, const void* tok_emb,

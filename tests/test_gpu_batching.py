@@ -1,0 +1,92 @@
+"""Batch-shape edge cases of the decode driver (round-1 advisor findings).
+
+* max_batch 16 and 17 on a multilingual model: the prompt pass carries B x 4 rows, 64 and 68;
+  past the decoder's rows per pass (gemv_max_image_rows: 63 for f32 tiny) the prompt is
+  prefilled in chunks (engine.cpp run_decode).  Every sequence of a full batch must get the
+  result it gets alone, on the fast path and on the whisper_full path.
+* max_batch 40 at large-v3 width in bf16: a pass stages at most 38 rows, so the batch is decoded
+  as two groups; again each sequence must get its result alone.
+* SPT_DECODE_GROUPS=2 (the batch split over two streams): decode graphs are cached per
+  (group batch, total batch, group offset, ...), so B = 3, then 4, then 3 again must each give
+  the single-stream engine's tokens.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SEED = 4321
+
+
+def _params(**kw):
+    from spittle_amd import WhisperInferenceParams
+    kw.setdefault("language", "en")
+    kw.setdefault("temperature_inc", 0.0)
+    return WhisperInferenceParams(**kw)
+
+
+@pytest.fixture(scope="module")
+def cuda():
+    import torch
+    torch.zeros(1, device="cuda:0")
+
+
+@pytest.mark.parametrize("mb,dtype,spec", [(16, "f32", "synthetic:tiny:enc=2:dec=2"),
+                                            (17, "f32", "synthetic:tiny:enc=2:dec=2"),
+                                            (40, "bf16", "synthetic:large-v3:enc=1:dec=2")])
+def test_full_batches_past_the_row_limit(cuda, mb, dtype, spec):
+    from spittle_amd import WhisperEngine, WhisperModelParams
+    e = WhisperEngine(WhisperModelParams(dtype=dtype, max_batch=mb, seed=SEED))
+    e.load_model(spec)
+    tol = 1e-4 if dtype == "f32" else 0.05  # f32: ulps of ~12; bf16: one rounding flip's reach
+    try:
+        xs = [O.synth_audio(300 + i, 5 * 16000) for i in range(mb)]
+        fast = _params(no_timestamps=True, ignore_eot=True, max_new_tokens=8)
+        full = _params(max_new_tokens=6)
+        for p in (fast, full):
+            batch = e.transcribe_batch(xs, p)
+            assert len(batch) == mb
+            for i in (0, mb // 2, mb - 1):
+                alone = e.transcribe_samples(xs[i], p)
+                assert batch[i].tokens == alone.tokens, (mb, i)
+                # the chunked prompt prefill runs other kernel instantiations (one query per
+                # sequence instead of four) than the one-pass prompt alone: last-ulp differences
+                d1 = np.abs(np.asarray(batch[i].top1) - np.asarray(alone.top1))
+                assert d1.max() <= tol, (mb, i, d1.max())
+    finally:
+        e.unload_model()
+
+
+def test_decode_groups_reuse_graphs_across_batch_sizes(cuda):
+    from spittle_amd import WhisperEngine, WhisperModelParams
+
+    def make(groups):
+        old = os.environ.get("SPT_DECODE_GROUPS")
+        os.environ["SPT_DECODE_GROUPS"] = str(groups)
+        try:
+            e = WhisperEngine(WhisperModelParams(dtype="bf16", max_batch=4, seed=SEED))
+            e.load_model("synthetic:tiny:enc=2:dec=2")
+        finally:
+            if old is None:
+                del os.environ["SPT_DECODE_GROUPS"]
+            else:
+                os.environ["SPT_DECODE_GROUPS"] = old
+        return e
+
+    e1, e2 = make(1), make(2)
+    try:
+        p = _params(no_timestamps=True, ignore_eot=True, max_new_tokens=12)
+        for nb in (3, 4, 3, 2, 4):
+            xs = [O.synth_audio(400 + nb * 10 + i) for i in range(nb)]
+            r1 = e1.transcribe_batch(xs, p)
+            r2 = e2.transcribe_batch(xs, p)
+            for a, b in zip(r1, r2):
+                assert a.tokens == b.tokens, nb
+                assert np.array_equal(np.asarray(a.top1), np.asarray(b.top1)), nb
+    finally:
+        e1.unload_model()
+        e2.unload_model()
