@@ -147,6 +147,8 @@ void Engine::release() {
         if (g.ev) (void)hipEventDestroy(g.ev);
         if (g.st) (void)hipStreamDestroy(g.st);
     }
+    for (auto& kv : enc_graphs_) (void)hipGraphExecDestroy(kv.second);
+    enc_graphs_.clear();
     if (warena_) (void)hipFree(warena_);
     if (aarena_) (void)hipFree(aarena_);
     if (kvtmp_) (void)hipFree(kvtmp_);
@@ -650,6 +652,36 @@ void Engine::run_encoder(int B) {
     layernorm(dt_, x_, M, d, lnp_w_, lnp_b_, enc_out_, st_);
 }
 
+// The encoder is one fixed chain of launches per batch size (about 7 per layer, 230 for
+// large-v3): from the second call with a given B it replays a captured graph, which removes the
+// eager launch gaps between its kernels.  The first call runs eagerly, which also sets the
+// kernels' one-time attributes outside any capture.  SPT_NO_GRAPH / SPT_ENC_GRAPH=0: eager.
+void Engine::enqueue_encoder(int B) {
+    static const bool eager = getenv("SPT_NO_GRAPH") || (getenv("SPT_ENC_GRAPH") && atoi(getenv("SPT_ENC_GRAPH")) == 0);
+    if (eager || !enc_seen_.count(B)) {
+        enc_seen_.insert(B);
+        run_encoder(B);
+        return;
+    }
+    auto it = enc_graphs_.find(B);
+    if (it == enc_graphs_.end()) {
+        hipGraph_t graph;
+        HIP_CHECK(hipStreamBeginCapture(st_, hipStreamCaptureModeThreadLocal));
+        try {
+            run_encoder(B);
+        } catch (...) {
+            (void)hipStreamEndCapture(st_, &graph);
+            throw;
+        }
+        HIP_CHECK(hipStreamEndCapture(st_, &graph));
+        hipGraphExec_t exec;
+        HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+        HIP_CHECK(hipGraphDestroy(graph));
+        it = enc_graphs_.emplace(B, exec).first;
+    }
+    HIP_CHECK(hipGraphLaunch(it->second, st_));
+}
+
 void Engine::run_cross_kv(int B) {
     const int d = dm_.d, T = dm_.n_audio_ctx;
     GemmArgs g{};
@@ -1055,7 +1087,7 @@ void Engine::transcribe_device(const float* pcm_dev, int64_t stride, const int* 
     HIP_CHECK(hipEventRecord(ev_[1], st_));
     run_mel(pcm_dev, stride, B, nullptr);
     HIP_CHECK(hipEventRecord(ev_[2], st_));
-    run_encoder(B);
+    enqueue_encoder(B);
     HIP_CHECK(hipEventRecord(ev_[3], st_));
     run_cross_kv(B);
     HIP_CHECK(hipEventRecord(ev_[4], st_));

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include <map>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -163,6 +164,7 @@ private:
     void stage_pcm(const float* const* pcm, const int* n, int B);
     void run_mel(const float* pcm_dev, int64_t stride, int B, float* dbg);
     void run_encoder(int B);
+    void enqueue_encoder(int B);  // run_encoder, replayed from a per-B graph after the first call
     void run_cross_kv(int B);
     void run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1, float* top2, int* lang_out,
                     int* ts_state_out);
@@ -199,7 +201,9 @@ private:
     std::vector<EncL> enc_;
     std::vector<DecL> dec_;
     struct TRef { void* p; int64_t n; int dt; };
-    std::map<int, TRef> tref_;  // tensor id -> device location (for checksums)
+    std::map<int, TRef> tref_;
+    std::map<int, hipGraphExec_t> enc_graphs_;  // batch size -> captured encoder (enqueue_encoder)
+    std::set<int> enc_seen_;                     // batch sizes whose first, eager encoder call ran  // tensor id -> device location (for checksums)
 
     // ---- tables
     float *hann_ = nullptr, *sinv_ = nullptr, *cosv_ = nullptr, *filt_ = nullptr;
