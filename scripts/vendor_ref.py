@@ -37,3 +37,17 @@ us = tm(lambda: F.scaled_dot_product_attention(q, k, v))
 fl = 4.0 * 8 * 20 * 1500 * 1500 * 64
 print(json.dumps({"op": "torch_sdpa_encoder_attention", "shape": [8, 20, 1500, 64], "us": round(us, 2),
                   "TFLOP/s": round(fl / us / 1e6, 1), "frac_of_2500": round(fl / us / 1e6 / 2500, 3)}), flush=True)
+# the residual projections as the encoder needs them: bf16 operands, f32 residual C = D (beta = 1)
+# and bias, through hipBLASLt's mixed-precision path (torch.addmm(..., out_dtype=float32))
+for name, N, K in [("out_resid_f32", d, d), ("fc2_resid_f32", d, 4 * d)]:
+    a = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
+    x = torch.randn(M, N, device=dev, dtype=torch.float32)
+    b = torch.randn(N, device=dev, dtype=torch.float32)
+    try:
+        us = tm(lambda: x.copy_(torch.addmm(x, a, w.t(), out_dtype=torch.float32)).add_(b))
+        fl = 2.0 * M * N * K
+        print(json.dumps({"op": f"hipblaslt_addmm_{name}", "M": M, "N": N, "K": K, "us": round(us, 2),
+                          "TFLOP/s": round(fl / us / 1e6, 1), "note": "includes a copy-back and a bias add"}), flush=True)
+    except Exception as e:  # noqa: BLE001 -- a missing mixed-precision solution is a result too
+        print(json.dumps({"op": f"hipblaslt_addmm_{name}", "error": str(e)[:200]}), flush=True)
