@@ -267,7 +267,7 @@ def parakeet_bench(device: int, steps: int, warmup: int, with_cpu: bool) -> dict
     if only == "offline":
         w1 = w1[:1]
     med, tot, res, ph = run(w1)
-    flops = 64 * parakeet_encoder_flops(info, 16000 // 160 + 1)
+    flops = 64 * parakeet_encoder_flops(info, 16000 // 160)
     tf = flops / (ph["encoder_ms"] * 1e-3) / 1e12
     out["streaming_1s_b64"] = {"rtfx": round(64 * steps / tot, 2), "ms_per_pass_median": round(med * 1e3, 3),
                                "phases_ms": {k: round(v, 3) for k, v in ph.items() if k.endswith("_ms")},
@@ -283,7 +283,7 @@ def parakeet_bench(device: int, steps: int, warmup: int, with_cpu: bool) -> dict
     if only == "stream":
         w30 = [w30[0][:16000]]
     med, tot, res, ph = run(w30)
-    flops = 8 * parakeet_encoder_flops(info, 480000 // 160 + 1)
+    flops = 8 * parakeet_encoder_flops(info, 480000 // 160)
     tf = flops / (ph["encoder_ms"] * 1e-3) / 1e12
     out["offline_30s_b8"] = {"rtfx": round(8 * 30.0 * steps / tot, 2), "ms_per_pass_median": round(med * 1e3, 3),
                              "phases_ms": {k: round(v, 3) for k, v in ph.items() if k.endswith("_ms")},

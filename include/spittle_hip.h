@@ -332,10 +332,13 @@ spt_status spt_parakeet_transcribe_batch_device(spt_pk_ctx* ctx, const float* pc
                                                 const spt_pk_infer_params* params, spt_pk_result** out);
 void spt_parakeet_result_free(spt_pk_result* r);
 spt_status spt_parakeet_get_timings(const spt_pk_ctx* ctx, spt_pk_timings* t);
-/* test hooks: normalised log-mel [n_mels][n / 160 + 1]; encoder output [T3][d] of a mel
+/* test hooks: normalised log-mel [n_mels][max(1, n / 160)] (n / 160 valid frames, NeMo get_seq_len); encoder output [T3][d] of a mel
  * [n_mels][T]; sum|w| and sum w of a tensor as stored (transposed tensors: SPT_ERR_UNSUPPORTED) */
 spt_status spt_parakeet_debug_mel(spt_pk_ctx* ctx, const float* pcm16k, size_t n_samples, float* out);
 spt_status spt_parakeet_debug_encode(spt_pk_ctx* ctx, const float* mel, int32_t T, float* out);
+/* the encoder output [T3][d] (f32) of batch row b of the last transcribe call (the production
+ * path: graph-replayed or eager); out holds max_seconds' T3 rows; *T3 receives the row's count */
+spt_status spt_parakeet_debug_last_encoder(spt_pk_ctx* ctx, int32_t b, float* out, int32_t* T3);
 /* TDT greedy decoding of a given encoder output [T3][d] (f32): the decoder alone */
 spt_status spt_parakeet_debug_decode(spt_pk_ctx* ctx, const float* enc, int32_t T3, int32_t max_symbols,
                                      spt_pk_result** out);

@@ -63,6 +63,7 @@ def lib():
         L.po_mel.argtypes = [fp, C.c_int, C.c_int, fp]
         L.po_encode.argtypes = [C.c_void_p, fp, C.c_int, fp]
         L.po_decode.argtypes = [C.c_void_p, fp, C.c_int, C.c_int, ip, ip, fp, fp, C.c_int]
+        L.po_decode_gaps.argtypes = [C.c_void_p, fp, C.c_int, C.c_int, ip, ip, fp, fp, fp, C.c_int]
         L.po_tensor.restype = C.c_int64
         L.po_tensor.argtypes = [C.c_void_p, C.c_int, C.POINTER(fp)]
         _lib = L
@@ -141,3 +142,26 @@ class Model:
         n = lib().po_decode(self._p, _f(enc), int(T3), int(max_symbols), _i(toks), _i(frames), _f(t1), _f(t2), cap)
         n = min(n, cap)
         return toks[:n].copy(), frames[:n].copy(), t1[:n].copy(), t2[:n].copy()
+
+    def decode_gaps(self, enc: np.ndarray, max_symbols: int = 10):
+        """decode() plus the decision margins: gmin[i] is the smallest top-1/top-2 margin of any
+        token or duration decision leading to emission i; gmin[n] covers the evaluations after
+        the last emission."""
+        enc = np.ascontiguousarray(enc, dtype=np.float32)
+        T3 = enc.shape[0]
+        cap = T3 * max_symbols + 2
+        toks, frames = np.empty(cap, np.int32), np.empty(cap, np.int32)
+        t1, t2, g = np.empty(cap, np.float32), np.empty(cap, np.float32), np.empty(cap, np.float32)
+        n = lib().po_decode_gaps(self._p, _f(enc), int(T3), int(max_symbols), _i(toks), _i(frames), _f(t1), _f(t2),
+                                 _f(g), cap)
+        return toks[:n].copy(), frames[:n].copy(), t1[:n].copy(), t2[:n].copy(), g[:n + 1].copy()
+
+
+def first_disagreement(tok, frm, otok, ofrm, gmin) -> tuple[int, float]:
+    """Index of the first (token, frame) pair where a run departs from the oracle's, and the
+    oracle's smallest decision margin up to that point (inf when the runs agree throughout)."""
+    n = min(len(tok), len(otok))
+    i = next((k for k in range(n) if tok[k] != otok[k] or frm[k] != ofrm[k]), n)
+    if i == len(tok) == len(otok):
+        return i, float("inf")
+    return i, float(np.min(gmin[:i + 1]))

@@ -15,7 +15,7 @@
  *   preprocessor  NeMo FilterbankFeatures: pre-emphasis 0.97, STFT n_fft 512, hop 160,
  *                 400-sample symmetric Hann centred in the 512 window, centre padding of
  *                 256 zeros, power spectrum, 128 slaney mel bands (0-8 kHz), log(x + 2^-24),
- *                 per-feature normalisation over the utterance (unbiased std + 1e-5);
+ *                 per-feature normalisation over the n / 160 valid frames (unbiased std + 1e-5);
  *   encoder       ConvSubsampling "dw_striding" x8 (conv 3x3 s2 -> ReLU -> [dw 3x3 s2 ->
  *                 pw 1x1 -> ReLU] x 2 -> flatten (channel-major) -> linear), x * sqrt(d),
  *                 relative sinusoidal positions; 24 Conformer layers: 1/2 FFN (Swish), rel-pos
@@ -62,7 +62,7 @@ po_model* po_create(const po_dims* dims, uint64_t seed, int wdtype);
 void po_destroy(po_model* m);
 void po_set_threads(int n);
 
-/* frames of the preprocessor for n samples: n / 160 + 1 */
+/* valid frames of the preprocessor for n samples: n / 160 (NeMo get_seq_len) */
 int po_n_frames(int n_samples);
 /* encoder frames after the x8 subsampling of T mel frames */
 int po_n_enc_frames(int T);
@@ -74,6 +74,11 @@ int po_encode(po_model* m, const float* mel, int T, float* out);
  * the joint evaluation that emitted them; returns the count (<= cap) */
 int po_decode(po_model* m, const float* enc, int T3, int max_symbols, int* tokens, int* frames, float* top1,
               float* top2, int cap);
+/* po_decode plus gmin[i]: the smallest top-1/top-2 margin of any token or duration decision since
+ * emission i - 1 (inclusive of emission i); gmin[n] covers the evaluations after the last one
+ * (cap must exceed the count) -- the decision margin a GPU run's first disagreement is held to */
+int po_decode_gaps(po_model* m, const float* enc, int T3, int max_symbols, int* tokens, int* frames, float* top1,
+                   float* top2, float* gmin, int cap);
 /* a weight tensor by id (contract with the engine): its element count, or -1 */
 int64_t po_tensor(po_model* m, int tid, const float** data);
 

@@ -227,7 +227,9 @@ int64_t po_tensor(po_model* m, int tid, const float** data) {
 }
 
 /* ------------------------------------------------------------------ preprocessor */
-int po_n_frames(int n) { return n / 160 + 1; }
+/* valid frames: NeMo FilterbankFeatures.get_seq_len = (n + 2*256 - 512) // 160 (HF
+ * feature_extraction_parakeet.py:263-265); the STFT's last centred frame is not one of them */
+int po_n_frames(int n) { return n > 0 ? n / 160 : 0; }
 
 /* NeMo FilterbankFeatures (normalize="per_feature", log, mag_power 2, preemph 0.97,
  * n_fft 512, win 400 symmetric Hann, hop 160, centre padding, 128 slaney mels 0-8 kHz) */
@@ -309,7 +311,7 @@ int po_mel(const float* pcm, int n, int n_mels, float* out) {
 
 /* ------------------------------------------------------------------ encoder */
 int po_n_enc_frames(int T) {
-    for (int i = 0; i < 3; i++) T = (T - 1) / 2 + 1;
+    for (int i = 0; i < 3; i++) T = T > 0 ? (T - 1) / 2 + 1 : 0;
     return T;
 }
 
@@ -568,8 +570,8 @@ static void predict(const po_model* m, int tok, float* h /* [2][P] */, float* c,
     }
 }
 
-int po_decode(po_model* m, const float* enc, int T3, int max_symbols, int* tokens, int* frames, float* top1,
-              float* top2, int cap) {
+static int decode_core(po_model* m, const float* enc, int T3, int max_symbols, int* tokens, int* frames, float* top1,
+                       float* top2, float* gmin, int cap) {
     const po_dims* D = &m->dm;
     const int P = D->pred, d = D->d, V = D->n_vocab, NO = V + 1 + D->n_dur;
     /* the joint's encoder projection of every frame, once */
@@ -581,6 +583,7 @@ int po_decode(po_model* m, const float* enc, int T3, int max_symbols, int* token
     predict(m, V, h, c, gp);  /* start: the blank symbol */
     float* lg = malloc(sizeof(float) * NO);
     int n = 0, t = 0, at_t = 0;
+    float gacc = INFINITY;
     while (t < T3) {
         for (int k = 0; k < P; k++) {
             const float z = fe[(size_t)t * P + k] + gp[k];
@@ -598,8 +601,15 @@ int po_decode(po_model* m, const float* enc, int T3, int max_symbols, int* token
             else if (lg[o] > b2) b2 = lg[o];
         }
         int dk = 0;
-        for (int o = 1; o < D->n_dur; o++)
-            if (lg[V + 1 + o] > lg[V + 1 + dk]) dk = o;
+        float d1 = -INFINITY, d2 = -INFINITY;
+        for (int o = 0; o < D->n_dur; o++) {
+            const float v = lg[V + 1 + o];
+            if (v > d1) { d2 = d1; d1 = v; dk = o; }
+            else if (v > d2) d2 = v;
+        }
+        /* the closest decision (token or duration) since the previous emission */
+        const float g = fminf(b1 - b2, d1 - d2);
+        if (g < gacc) gacc = g;
         int skip = dk;  /* durations 0, 1, .., n_dur - 1 */
         if (tk != V) {
             if (n < cap) {
@@ -607,7 +617,9 @@ int po_decode(po_model* m, const float* enc, int T3, int max_symbols, int* token
                 frames[n] = t;
                 if (top1) top1[n] = b1;
                 if (top2) top2[n] = b2;
+                if (gmin) gmin[n] = gacc;
             }
+            gacc = INFINITY;
             n++;
             predict(m, tk, h, c, gp);
             at_t++;
@@ -616,7 +628,18 @@ int po_decode(po_model* m, const float* enc, int T3, int max_symbols, int* token
         if (skip > 0) at_t = 0;
         t += skip;
     }
+    if (gmin && n < cap) gmin[n] = gacc;  /* the evaluations after the last emission */
     free(lg);
     free(fe);
     return n;
+}
+
+int po_decode(po_model* m, const float* enc, int T3, int max_symbols, int* tokens, int* frames, float* top1,
+              float* top2, int cap) {
+    return decode_core(m, enc, T3, max_symbols, tokens, frames, top1, top2, NULL, cap);
+}
+
+int po_decode_gaps(po_model* m, const float* enc, int T3, int max_symbols, int* tokens, int* frames, float* top1,
+                   float* top2, float* gmin, int cap) {
+    return decode_core(m, enc, T3, max_symbols, tokens, frames, top1, top2, gmin, cap);
 }

@@ -276,6 +276,7 @@ extern "C" {
     pub fn spt_parakeet_get_timings(ctx: *const spt_pk_ctx, t: *mut spt_pk_timings) -> spt_status;
     pub fn spt_parakeet_debug_mel(ctx: *mut spt_pk_ctx, pcm16k: *const f32, n_samples: usize, out: *mut f32) -> spt_status;
     pub fn spt_parakeet_debug_encode(ctx: *mut spt_pk_ctx, mel: *const f32, t: i32, out: *mut f32) -> spt_status;
+    pub fn spt_parakeet_debug_last_encoder(ctx: *mut spt_pk_ctx, b: i32, out: *mut f32, t3: *mut i32) -> spt_status;
     pub fn spt_parakeet_debug_decode(
         ctx: *mut spt_pk_ctx,
         enc: *const f32,

@@ -31,7 +31,7 @@ EXPORTS = [
     "spt_parakeet_destroy", "spt_parakeet_last_error", "spt_parakeet_info", "spt_parakeet_tensor_numel",
     "spt_parakeet_set_tensor", "spt_parakeet_set_vocab", "spt_parakeet_transcribe", "spt_parakeet_transcribe_batch",
     "spt_parakeet_transcribe_batch_device", "spt_parakeet_result_free", "spt_parakeet_get_timings",
-    "spt_parakeet_debug_mel", "spt_parakeet_debug_encode", "spt_parakeet_debug_decode",
+    "spt_parakeet_debug_mel", "spt_parakeet_debug_encode", "spt_parakeet_debug_decode", "spt_parakeet_debug_last_encoder",
     "spt_parakeet_debug_weight_checksum",
     # ABI 7: capture-side resampler
     "spt_resampler_create", "spt_resampler_info", "spt_resample_output_len", "spt_resample",
@@ -188,6 +188,7 @@ def load():
     L.spt_parakeet_debug_mel.argtypes = [vp, fp, C.c_size_t, fp]
     L.spt_parakeet_debug_encode.argtypes = [vp, fp, C.c_int32, fp]
     L.spt_parakeet_debug_decode.argtypes = [vp, fp, C.c_int32, C.c_int32, PR]
+    L.spt_parakeet_debug_last_encoder.argtypes = [vp, C.c_int32, fp, C.POINTER(C.c_int32)]
     L.spt_parakeet_debug_weight_checksum.argtypes = [vp, C.c_int32, C.POINTER(C.c_double)]
     L.spt_resampler_create.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.POINTER(vp), C.c_char_p,
                                        C.c_size_t]

@@ -434,6 +434,16 @@ spt_status spt_parakeet_debug_encode(spt_pk_ctx* ctx, const float* mel, int32_t 
     }
 }
 
+spt_status spt_parakeet_debug_last_encoder(spt_pk_ctx* ctx, int32_t b, float* out, int32_t* T3) {
+    if (!ctx || !out || !T3) return fail(ctx, SPT_ERR_INVALID_ARG, "null argument");
+    try {
+        *T3 = ctx->eng->debug_last_encoder(b, out);
+        return SPT_OK;
+    } catch (const std::exception& e) {
+        return fail(ctx, classify(e), e.what());
+    }
+}
+
 spt_status spt_parakeet_debug_decode(spt_pk_ctx* ctx, const float* enc, int32_t T3, int32_t max_symbols,
                                      spt_pk_result** out) {
     if (!ctx || !enc || !out) return fail(ctx, SPT_ERR_INVALID_ARG, "null argument");

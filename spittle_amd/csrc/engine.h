@@ -71,6 +71,7 @@ public:
     const ModelDims& dims() const { return dm_; }
     int dtype() const { return dt_; }
     int max_batch() const { return max_batch_; }
+    int max_rows() const { return max_rows_; }  // decoder rows one pass carries (beam search: one group)
     int64_t weight_bytes() const { return wbytes_; }
     bool weights_ready() const { return weights_ready_; }
     // D2D copies of the whole weight arena (device pointers on this engine's device, or any

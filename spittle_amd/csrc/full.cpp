@@ -269,7 +269,8 @@ void whisper_full_batch(Engine& e, const Vocab* vocab, const std::vector<const f
             for (auto& kv : by_len) {
                 const std::vector<int>& grp = kv.second;
                 const int P = (int)kv.first;
-                const int per = std::max(1, cap / dchunk);
+                // a beam call decodes as one group, so it carries at most the pass's rows
+                const int per = std::max(1, (beam ? std::min(cap, e.max_rows()) : cap) / dchunk);
                 for (size_t g0 = 0; g0 < grp.size(); g0 += per)
                 for (int d0 = 0; d0 < ndec; d0 += dchunk) {
                     const int nj = (int)std::min<size_t>(per, grp.size() - g0);

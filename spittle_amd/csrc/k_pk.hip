@@ -766,9 +766,9 @@ __global__ __launch_bounds__(256) void joint_fin_kernel(PkFinArgs a) {
 // rows start at t = 0 with the blank symbol pending: zero states, the blank's (zero) embedding,
 // frame 0's encoder projection
 __global__ void state_init_kernel(PkState* st, int B, int V, float* h, float* c, int n, float* xemb, float* fecur,
-                                  const float* fe, int T3p, int P) {
+                                  const float* fe, int T3p, int P, const int* __restrict__ lens) {
     const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i < B) st[i] = PkState{0, 0, 0, 0, 1, V};
+    if (i < B) st[i] = PkState{0, 0, 0, lens[i * 4 + 3] <= 0 ? 1 : 0, 1, V};  // no frames: nothing to decode
     if (i < n) { h[i] = 0.0f; c[i] = 0.0f; }
     if (i < B * P) {
         const int b = i / P, k = i % P;
@@ -954,10 +954,10 @@ void pk_joint_fin(const PkFinArgs& a, hipStream_t s) {
     SPT_LAUNCH_CHECK();
 }
 
-void pk_state_init(PkState* st, int B, int V, float* h, float* c, int n, float* xemb, float* fecur, const float* fe,
+void pk_state_init(PkState* st, int B, int V, float* h, float* c, int n, float* xemb, float* fecur, const float* fe, const int* lens,
                    int T3p, int P, hipStream_t s) {
     hipLaunchKernelGGL(state_init_kernel, dim3(cdiv(std::max(std::max(B, n), B * P), 256)), dim3(256), 0, s, st, B, V, h,
-                       c, n, xemb, fecur, fe, T3p, P);
+                       c, n, xemb, fecur, fe, T3p, P, lens);
     SPT_LAUNCH_CHECK();
 }
 

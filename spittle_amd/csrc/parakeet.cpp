@@ -29,6 +29,8 @@ constexpr int kStepsPerGraph = 8;
 int fanin_exp(int K) { return (int)floor(log2(sqrt(3.0 / (double)K)) + 0.5); }
 int round_up(int x, int m) { return (x + m - 1) / m * m; }
 int halve(int t) { return (t - 1) / 2 + 1; }
+// a stride-2 conv stage's valid length (0 stays 0)
+int sub_len(int t) { return t > 0 ? halve(t) : 0; }
 
 struct Carve {
     char* base;
@@ -114,7 +116,7 @@ ParakeetEngine::ParakeetEngine(const PkDims& dm, int dtype, int device, int max_
     F1_ = halve(dm_.n_mels);
     F2_ = halve(F1_);
     F3_ = halve(F2_);
-    Tmax_ = max_samples / PK_HOP + 1;
+    Tmax_ = max_samples / PK_HOP;
     T1max_ = halve(Tmax_);
     T2max_ = halve(T1max_);
     T3max_ = halve(T2max_);
@@ -403,11 +405,13 @@ void ParakeetEngine::frame_counts(const int* n, int B, std::vector<int>* lens, i
     int tp = 1;
     for (int b = 0; b < B; ++b) {
         if (n[b] < 0 || n[b] > max_samples_) throw std::runtime_error("utterance length out of range");
-        const int T = n[b] / PK_HOP + 1;
+        // valid frames: NeMo FilterbankFeatures.get_seq_len = n / hop (HF feature_extraction_parakeet.py:263);
+        // the STFT's last centred frame is not one of them.  Under 160 samples nothing is decoded.
+        const int T = n[b] / PK_HOP;
         (*lens)[b * 4 + 0] = T;
-        (*lens)[b * 4 + 1] = halve(T);
-        (*lens)[b * 4 + 2] = halve(halve(T));
-        (*lens)[b * 4 + 3] = halve(halve(halve(T)));
+        (*lens)[b * 4 + 1] = sub_len(T);
+        (*lens)[b * 4 + 2] = sub_len(sub_len(T));
+        (*lens)[b * 4 + 3] = sub_len(sub_len(sub_len(T)));
         tp = std::max(tp, T);
     }
     *Tp = tp;
@@ -571,7 +575,7 @@ void ParakeetEngine::enqueue_step(int B, int T3p, int max_symbols, int cap, int 
 
 void ParakeetEngine::run_decode(int B, int T3p, int max_symbols, std::vector<PkUtt>* out) {
     const int P = dm_.pred;
-    pk_state_init(state_, B, dm_.n_vocab, h_, c_, 4 * B * P, xemb_, fecur_, fe_, T3p, P, st_);
+    pk_state_init(state_, B, dm_.n_vocab, h_, c_, 4 * B * P, xemb_, fecur_, fe_, lens_, T3p, P, st_);
     const GraphKey key{B, T3p, max_symbols};
     auto it = graphs_.find(key);
     static const bool no_graph = getenv("SPT_NO_GRAPH") != nullptr;
@@ -630,6 +634,8 @@ void ParakeetEngine::transcribe_device(const float* pcm_dev, int64_t stride, con
     std::vector<int> lens;
     int Tp, T1p, T2p, T3p;
     frame_counts(n, B, &lens, &Tp, &T1p, &T2p, &T3p);
+    last_lens_ = lens;
+    last_T3p_ = T3p;
     HIP_CHECK(hipEventRecord(ev_[0], st_));
     HIP_CHECK(hipMemcpyAsync(nsamp_, n, B * 4, hipMemcpyHostToDevice, st_));
     HIP_CHECK(hipMemcpyAsync(lens_, lens.data(), lens.size() * 4, hipMemcpyHostToDevice, st_));
@@ -693,6 +699,17 @@ void ParakeetEngine::debug_encode(const float* mel_host, int T, float* out_host)
     run_encoder(1, T, T1, T2, T3);
     HIP_CHECK(hipMemcpyAsync(out_host, enc_out_, (size_t)T3 * dm_.d * 4, hipMemcpyDeviceToHost, st_));
     HIP_CHECK(hipStreamSynchronize(st_));
+}
+
+int ParakeetEngine::debug_last_encoder(int b, float* out_host) {
+    select();
+    if (b < 0 || (size_t)b * 4 >= last_lens_.size()) throw std::runtime_error("no such row in the last call");
+    const int T3 = last_lens_[b * 4 + 3];
+    HIP_CHECK(hipStreamSynchronize(st_));
+    if (T3 > 0)
+        HIP_CHECK(hipMemcpy(out_host, enc_out_ + (size_t)b * last_T3p_ * dm_.d, (size_t)T3 * dm_.d * 4,
+                            hipMemcpyDeviceToHost));
+    return T3;
 }
 
 void ParakeetEngine::debug_decode(const float* enc_host, int T3, int max_symbols, PkUtt* out) {

@@ -67,6 +67,8 @@ public:
     void debug_encode(const float* mel_host, int T, float* out_host);              // [T3][d] (f32)
     // TDT greedy decoding of a given encoder output [T3][d] (f32 host): the decoder alone
     void debug_decode(const float* enc_host, int T3, int max_symbols, PkUtt* out);
+    // the encoder output rows [T3][d] (f32) of batch row b of the last transcribe call; returns T3
+    int debug_last_encoder(int b, float* out_host);
     bool debug_weight_checksum(int tid, double* out2);
 
 private:
@@ -140,6 +142,8 @@ private:
     float *frames_ = nullptr, *spec_ = nullptr, *mel_ = nullptr;
     void *y1_ = nullptr, *y2a_ = nullptr, *y2_ = nullptr, *y3a_ = nullptr, *y3_ = nullptr;
     float* x_ = nullptr;
+    std::vector<int> last_lens_;  // the last transcribe call's per-row lengths {T, T1, T2, T3}
+    int last_T3p_ = 0;
     float* enc_out_ = nullptr;  // the residual buffer holding the last call's encoder output
     void *xn_ = nullptr, *ffh_ = nullptr, *qkv_ = nullptr, *pe_ = nullptr, *pp_ = nullptr, *ctx_ = nullptr;
     void *glu_ = nullptr, *cv_ = nullptr;

@@ -87,6 +87,7 @@ void pk_joint_fin(const PkFinArgs& a, hipStream_t s);
 // rows start at t = 0 with the blank symbol pending (upd, tok = V); h / c: n floats zeroed; xemb
 // zero (the blank row), fecur = frame 0 of fe [B*T3p][P]
 void pk_state_init(PkState* st, int B, int V, float* h, float* c, int n, float* xemb, float* fecur, const float* fe,
+                   const int* lens,
                    int T3p, int P, hipStream_t s);
 // LSTM weight [4P][P] (gate rows i, f, g, o) -> rows row0.. of the blocked, gate-interleaved W^T
 // [P / 4][2P][16]

@@ -165,10 +165,22 @@ class ParakeetEngine:
 
     def debug_mel(self, pcm) -> np.ndarray:
         a = np.ascontiguousarray(np.asarray(pcm, dtype=np.float32).ravel())
-        out = np.empty((self.info()["n_mels"], a.size // 160 + 1), np.float32)
+        out = np.empty((self.info()["n_mels"], max(1, a.size // 160)), np.float32)  # n // 160 valid frames (NeMo get_seq_len)
         _check(self._lib, self._ctx, self._lib.spt_parakeet_debug_mel(self._need(), a.ctypes.data_as(C.POINTER(C.c_float)),
                                                                       a.size, out.ctypes.data_as(C.POINTER(C.c_float))))
-        return out
+        return out[:, :a.size // 160]
+
+    def debug_last_encoder(self, b: int) -> np.ndarray:
+        """Encoder output rows [T3][d] of batch row b of the last transcribe call (the production path)."""
+        info = self.info()
+        T3max = info["max_samples"] // 160
+        for _ in range(3):
+            T3max = (T3max - 1) // 2 + 1
+        out = np.empty((max(T3max, 1), info["d"]), np.float32)
+        t3 = C.c_int32()
+        _check(self._lib, self._ctx, self._lib.spt_parakeet_debug_last_encoder(
+            self._need(), int(b), out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(t3)))
+        return out[:t3.value].copy()
 
     def debug_encode(self, mel: np.ndarray) -> np.ndarray:
         mel = np.ascontiguousarray(mel, dtype=np.float32)

@@ -46,7 +46,7 @@ def mel(pcm: np.ndarray, n_mels: int = 128) -> torch.Tensor:
     p = X.abs() ** 2
     m = torch.from_numpy(slaney_mel(n_mels)) @ p
     m = torch.log(m + 2.0 ** -24)
-    T = pcm.size // 160 + 1
+    T = pcm.size // 160          # valid frames (NeMo get_seq_len; HF feature_extraction_parakeet.py:263)
     m = m[:, :T]
     mean = m.mean(1, keepdim=True)
     std = torch.sqrt(((m - mean) ** 2).sum(1, keepdim=True) / (T - 1)) + 1e-5

@@ -5,7 +5,8 @@
   prefilled in chunks (engine.cpp run_decode).  Every sequence of a full batch must get the
   result it gets alone, on the fast path and on the whisper_full path.
 * max_batch 40 at large-v3 width in bf16: a pass stages at most 38 rows, so the batch is decoded
-  as two groups; again each sequence must get its result alone.
+  as two groups; again each sequence must get its result alone.  Beam search (one group per
+  call) packs utterances by the same limit: 20 utterances x 2 beams run as two calls.
 * SPT_DECODE_GROUPS=2 (the batch split over two streams): decode graphs are cached per
   (group batch, total batch, group offset, ...), so B = 3, then 4, then 3 again must each give
   the single-stream engine's tokens.
@@ -57,6 +58,15 @@ def test_full_batches_past_the_row_limit(cuda, mb, dtype, spec):
                 # sequence instead of four) than the one-pass prompt alone: last-ulp differences
                 d1 = np.abs(np.asarray(batch[i].top1) - np.asarray(alone.top1))
                 assert d1.max() <= tol, (mb, i, d1.max())
+        if mb == 40:
+            # beam search decodes as one group: 20 utterances x 2 beams = 40 rows > 38 must be
+            # packed into several engine calls (full.cpp), not rejected (r2 advisor finding)
+            beam = _params(beam_size=2, max_new_tokens=4)
+            us = xs[:20]
+            batch = e.transcribe_batch(us, beam)
+            for i in (0, 10, 19):
+                alone = e.transcribe_samples(us[i], beam)
+                assert batch[i].tokens == alone.tokens, ("beam", i)
     finally:
         e.unload_model()
 

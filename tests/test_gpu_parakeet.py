@@ -1,5 +1,6 @@
 """GPU parity of the Parakeet-V3 path (spt_parakeet_* ABI) against the CPU oracle
-(oracle/po_model.c, itself pinned to a PyTorch restatement in test_parakeet_oracle.py).
+(oracle/po_model.c, pinned to HF transformers' Parakeet port through tests/golden/parakeet_*.npz
+in test_parakeet_oracle_golden.py) and directly against those HF fixtures.
 Parity with the real ONNX engine is unpinned: no export or weights exist offline.
 
 Bars (written next to each test):
@@ -9,7 +10,9 @@ Bars (written next to each test):
     encoder output relative RMS error below 4e-3 (measured 4.0e-4 at full size) against the oracle run on the same rounded
     weights (activations are fp16 on the GPU, f32 in the oracle); the f32 decoder on a given
     encoder output is exact; end-to-end token agreement is recorded;
-  * batching, chunking of long utterances and the .nemo loader are exact (same tokens)."""
+  * batching, chunking of long utterances and the .nemo loader are exact (same tokens);
+  * token sequences are held to "equal until the oracle's closest token-or-duration decision
+    (P.first_disagreement) falls under the stated bar": an f32 run 2e-3, fp16 runs 0.05."""
 import io
 import json
 import os
@@ -77,7 +80,7 @@ def test_mel_matches_oracle(small32, n):
     g = e.debug_mel(pcm)
     o = P.mel(pcm)
     assert g.shape == o.shape
-    assert np.abs(g - o).max() < 2e-3  # f32 MFMA DFT vs f64 DFT, after per-feature normalisation
+    assert g.size == 0 or np.abs(g - o).max() < 2e-3  # f32 MFMA DFT vs f64 DFT, after per-feature normalisation
 
 
 def test_encoder_f32_matches_oracle(small32):
@@ -249,6 +252,83 @@ def test_nemo_checkpoint_loads(tmp_path, small32):
     e.unload_model()
 
 
+F32_GAP = 2e-3   # f32 engine: joint logits within 1e-3 of the oracle's
+F16_GAP = 5e-2   # fp16 encoder (rel. RMS ~4e-4 of O(1) rows) through the f32 joint
+
+
+def _hf(name):
+    g = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name + ".npz")))
+    return g, [(i, int(s), int(n)) for i, (s, n) in enumerate(zip(g["audio_seeds"], g["audio_lens"]))]
+
+
+def _agree(r, om, enc, bar, max_symbols=10):
+    t, f, _, _, gmin = om.decode_gaps(enc, max_symbols=max_symbols)
+    i, gap = P.first_disagreement(list(r.tokens), list(r.frames), list(t), list(f), gmin)
+    assert gap < bar or gap == float("inf"), (i, gap, len(t), len(r.tokens))
+    return i, len(t), gap
+
+
+@pytest.mark.parametrize("name,cfg,spec", [("parakeet_small", "test-small", "synthetic:parakeet-test-small"),
+                                           ("parakeet_v3_full", "parakeet-tdt-0.6b-v3",
+                                            "synthetic:parakeet-tdt-0.6b-v3")])
+def test_f32_engine_matches_hf_fixtures(name, cfg, spec):
+    """The GPU path (f32 engine) against HF transformers' ParakeetFeatureExtractor /
+    ParakeetEncoder / ParakeetForTDT.generate on the oracle's weights (make_golden_parakeet.py):
+    mel within 2e-3, encoder within 2e-3, tokens and frames identical to HF's greedy TDT search
+    (every fixture decision margin exceeds F32_GAP, checked by test_parakeet_oracle_golden)."""
+    from spittle_amd import ParakeetEngine, ParakeetModelParams
+    g, clips = _hf(name)
+    e = ParakeetEngine()
+    e.load_model_with_params(spec, ParakeetModelParams(dtype="f32", seed=int(g["seed"]), max_batch=2, max_seconds=4.0))
+    om = P.Model(P.dims_for(cfg), seed=int(g["seed"]))
+    for i, s, n in clips:
+        pcm = synth_audio(s, n)
+        mg, eg = g[f"mel_{i}"], g[f"enc_{i}"]
+        assert np.abs(e.debug_mel(pcm) - mg).max() < 2e-3
+        assert np.abs(e.debug_encode(mg) - eg).max() < 2e-3
+        r = e.transcribe_samples(pcm, _tok_params())
+        _, gap = P.first_disagreement(list(r.tokens), list(r.frames), list(g[f"tokens_{i}"]), list(g[f"frames_{i}"]),
+                                      om.decode_gaps(om.encode(P.mel(pcm)))[4])
+        assert gap == float("inf") or gap < F32_GAP, (i, gap)
+    e.unload_model()
+    om.close()
+
+
+def test_c5_streaming_b64_full_size():
+    """BASELINE config 5 at the bench's own shape: parakeet-tdt-0.6b-v3 (24 layers, d 1024), fp16
+    encoder, 64 concurrent 1 s windows in one pass (832 encoder rows: the tile-128/256 GEMMs),
+    the bench's windows (synth_audio(3000 + i)[:16000]).  The encoder rows of the production call
+    (eager, then graph-replayed on the third sighting -- bitwise equal) against the oracle on
+    identically fp16-rounded weights for every one of the 64 windows, and each window's tokens/frames
+    against the oracle's greedy search on its own encoder output, equal up to a decision margin
+    under F16_GAP.  Measured values: gpurun_out/parakeet_c5_b64.json."""
+    from spittle_amd import ParakeetInferenceParams, TimestampGranularity
+    P.set_threads(16)
+    e = _engine("synthetic:parakeet-tdt-0.6b-v3", "f16", max_batch=64, max_seconds=2.0)  # > 1 s: no chunking
+    om = P.Model(P.dims_for("parakeet-tdt-0.6b-v3"), seed=SEED, wdtype=P.W_F16)
+    w = [synth_audio(3000 + i)[:16000] for i in range(64)]
+    prm = ParakeetInferenceParams(timestamp_granularity=TimestampGranularity.Token)
+    runs = [e.transcribe_batch(w, prm) for _ in range(3)]   # eager, eager, graph (seen twice)
+    assert e.timings()["batch"] == 64
+    for a, b in zip(runs[1], runs[2]):
+        assert list(a.tokens) == list(b.tokens) and np.array_equal(a.top1, b.top1)
+    rec = []
+    for b in range(64):
+        g = e.debug_last_encoder(b)
+        o = om.encode(P.mel(w[b]))
+        assert g.shape == o.shape == (13, 1024)
+        rel = float(np.sqrt(np.mean((g - o) ** 2) / np.mean(o ** 2)))
+        assert rel < 4e-3, (b, rel)
+        i, n_or, gap = _agree(runs[2][b], om, o, F16_GAP)
+        rec.append({"window": b, "encoder_rel_rms": rel, "prefix_agreement": i, "oracle_tokens": n_or,
+                    "gpu_tokens": len(runs[2][b].tokens), "margin_at_departure": None if gap == float("inf") else gap})
+    os.makedirs(OUT, exist_ok=True)
+    json.dump({"config": "C5: parakeet-tdt-0.6b-v3 synthetic seed 7, fp16 encoder, 64 x 1 s windows, B = 64",
+               "windows": rec}, open(os.path.join(OUT, "parakeet_c5_b64.json"), "w"), indent=1)
+    e.unload_model()
+    om.close()
+
+
 def test_full_size_fp16():
     """parakeet-tdt-0.6b-v3 shape (24 layers, d 1024), fp16 encoder, 4 s: encoder vs the oracle
     on identically rounded weights; the decoder exact on a given encoder output; end-to-end
@@ -266,12 +346,12 @@ def test_full_size_fp16():
     t, f, t1, _ = om.decode(o)
     assert list(rd.tokens) == list(t) and list(rd.frames) == list(f)
     r = e.transcribe_samples(pcm, ParakeetInferenceParams(timestamp_granularity=TimestampGranularity.Token))
-    n = min(len(r.tokens), len(t))
-    first = next((i for i in range(n) if r.tokens[i] != t[i] or r.frames[i] != f[i]), n)
+    first, _, gap = _agree(r, om, o, F16_GAP)
     os.makedirs(OUT, exist_ok=True)
     json.dump({"config": "parakeet-tdt-0.6b-v3 synthetic seed 7, fp16 encoder, 4 s", "encoder_rel_rms": rel,
                "encoder_max_abs": float(np.abs(g - o).max()), "oracle_tokens": len(t), "gpu_tokens": len(r.tokens),
-               "prefix_agreement": first, "decoder_exact_on_oracle_encoder": True},
+               "prefix_agreement": first, "margin_at_departure": None if gap == float("inf") else gap,
+               "decoder_exact_on_oracle_encoder": True},
               open(os.path.join(OUT, "parakeet_fullsize.json"), "w"), indent=1)
     assert rel < 4e-3, rel
     e.unload_model()

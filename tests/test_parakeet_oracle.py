@@ -24,7 +24,7 @@ def small():
 def test_mel_matches_torch_stft(n):
     pcm = synth_audio(5, n)
     mo = P.mel(pcm)
-    assert mo.shape == (128, n // 160 + 1)
+    assert mo.shape == (128, n // 160)
     mt = pk.mel(pcm).numpy()
     assert np.abs(mo - mt).max() < 1e-3
 
@@ -59,9 +59,11 @@ def test_max_symbols_per_frame(small):
 
 
 def test_frame_counts():
-    assert P.n_frames(16000) == 101 and P.n_enc_frames(101) == 13
-    assert P.n_frames(480000) == 3001 and P.n_enc_frames(3001) == 376
-    assert P.n_frames(0) == 1 and P.n_enc_frames(1) == 1
+    # NeMo get_seq_len / HF ParakeetFeatureExtractor: n // 160 valid frames
+    assert P.n_frames(16000) == 100 and P.n_enc_frames(100) == 13
+    assert P.n_frames(480000) == 3000 and P.n_enc_frames(3000) == 375
+    assert P.n_frames(0) == 0 and P.n_enc_frames(0) == 0
+    assert P.n_frames(159) == 0 and P.n_frames(160) == 1 and P.n_enc_frames(1) == 1
 
 
 def test_weight_rounding_modes():
