@@ -1,0 +1,123 @@
+"""The app's real Whisper call at the app's model width: whisper_full with timestamps on and
+temperature fallback off, large-v3 dimensions (d 1280, 20 heads, 128 mels, 51866 tokens) in bf16,
+2 encoder + 2 decoder layers, for B = 1 and B = 4 and 8 / 20 / 45 s inputs, and beam search
+(beam 5) -- against the oracle's whisper_full restatement (oracle/whisper_full.py over the fp32 C
+model on identically bf16-rounded weights).
+
+Reference call: /root/reference/src-tauri/src/managers/transcription.rs:494-503 (whisper params
+with timestamps on: the transcribe-rs default) -> whisper_full.
+
+Bars (bf16 activations at every GEMM input vs the oracle's f32):
+  * tokens, timestamp ids and segments equal up to the oracle's first decision whose margin
+    (argmax gap, timestamp-mass rule gap, beam candidate gap) is below GAP_BF16;
+  * on that agreed prefix the chosen tokens' log-probabilities within PLOG_BF16;
+  * a case whose oracle's first decision is already under the bar compares nothing and fails
+    (the non-empty-prefix guard of test_gpu_full._compare).
+Measured values per case: gpurun_out/full_large_v3.json."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from oracle import whisper_full as W
+
+pytestmark = pytest.mark.gpu
+
+SEED = 1234
+SPEC = "synthetic:large-v3:enc=2:dec=2"
+GAP_BF16 = 0.1     # measured largest |logit error| of the 2+2 bf16 model: ~0.05
+PLOG_BF16 = 0.05   # measured max 0.027 (b4, 8 s)
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+_REC = {}
+
+
+@pytest.fixture(scope="module")
+def large():
+    from spittle_amd import WhisperEngine, WhisperModelParams
+    O.set_threads(16)
+    e = WhisperEngine(WhisperModelParams(dtype="bf16", max_batch=8, seed=SEED))
+    e.load_model(SPEC)
+    om = O.Model(O.dims_for("large-v3", 2, 2), SEED, O.W_BF16)
+    yield e, om
+    e.unload_model()
+    om.close()
+    os.makedirs(OUT, exist_ok=True)
+    json.dump(_REC, open(os.path.join(OUT, "full_large_v3.json"), "w"), indent=1)
+
+
+def _params(**kw):
+    from spittle_amd import WhisperInferenceParams
+    kw.setdefault("language", "en")
+    kw.setdefault("temperature_inc", 0.0)
+    return WhisperInferenceParams(**kw)
+
+
+def _audio(seconds, seed):
+    n = int(seconds * 16000)
+    return np.concatenate([O.synth_audio(seed + k) for k in range((n + 479999) // 480000)])[:n]
+
+
+def _check(name, r, om, x, p):
+    wins, segs, toks, kept = W.transcribe(om, x, p)
+    steps = [s for _, w in wins for s in w.steps]
+    gaps = [s.margin for s in steps]
+    k = next((i for i, g in enumerate(gaps) if g <= GAP_BF16), None)
+    got = list(r.tokens)
+    n = len(toks)
+    rec = {"oracle_tokens": n, "gpu_tokens": len(got), "oracle_windows": len(wins), "gpu_windows": r.n_windows,
+           "first_small_margin_step": k, "smallest_margin": float(min(gaps)) if gaps else None}
+    if k is None:
+        assert got == toks, name
+        assert [(int(round(s.start * 100)), int(round(s.end * 100)), s.text) for s in r.segments] == \
+               [(a, b, t) for a, b, t, _, _ in segs], name
+        m = n
+    else:
+        assert min(k, n) > 0, (name, "the oracle's first decision is already under the bar: nothing to compare")
+        m = min(k, n)
+        assert got[:m] == toks[:m], name
+    dplog = [abs(float(r.top1[i]) - kept[i].plog) for i in range(m)]
+    # the timestamp id (best timestamp token of a step) reaches the output only through a
+    # timestamp token, where it is that token; elsewhere its own near-ties are not decisions
+    beg = O.special_tokens(om.dims.n_vocab)["beg"]
+    tid_ts = all(int(r.top2[i]) == kept[i].tid for i in range(m) if toks[i] >= beg)
+    rec.update({"compared_tokens": m, "max_plog_diff": max(dplog) if dplog else 0.0,
+                "tids_equal_all_steps": all(int(r.top2[i]) == kept[i].tid for i in range(m)),
+                "tids_equal_at_timestamps": tid_ts, "exact": k is None, "whole_output_equal": got == toks})
+    _REC[name] = rec
+    assert max(dplog, default=0.0) < PLOG_BF16, (name, max(dplog))
+    assert tid_ts, name
+    return rec
+
+
+@pytest.mark.parametrize("seconds,seed", [(8, 160), (20, 161), (45, 162)])
+def test_large_v3_timestamps_b1(large, seconds, seed):
+    e, om = large
+    x = _audio(seconds, seed)
+    r = e.transcribe_samples(x, _params(max_new_tokens=32))
+    _check(f"b1_{seconds}s", r, om, x, W.Params(max_tokens=32))
+    assert r.n_windows >= (2 if seconds > 30 else 1)
+
+
+def test_large_v3_timestamps_b4(large):
+    """Four utterances of different lengths (so different seek paths) in one call: each against
+    its own oracle run."""
+    e, om = large
+    xs = [_audio(8, 170), _audio(20, 171), _audio(45, 172), _audio(12.5, 173)]
+    rs = e.transcribe_batch(xs, _params(max_new_tokens=32))
+    for i, (x, r) in enumerate(zip(xs, rs)):
+        _check(f"b4_{i}_{len(x) / 16000:g}s", r, om, x, W.Params(max_tokens=32))
+
+
+@pytest.mark.parametrize("seconds,seed", [(20, 191), (45, 206)])
+def test_large_v3_beam5(large, seconds, seed):
+    """Beam 5: the oracle's margin for a step is the smallest gap among the ranked candidates
+    (5th vs 6th included), which bf16 random-weight logits make small within a few steps; the
+    inputs are ones whose first steps are decided by more than GAP_BF16 (seeds chosen by scanning
+    180-211 with the oracle), so the compared prefix is 5 and 2 tokens; the whole output is
+    recorded ("whole_output_equal")."""
+    e, om = large
+    x = _audio(seconds, seed)
+    r = e.transcribe_samples(x, _params(beam_size=5, max_new_tokens=16))
+    _check(f"beam5_{seconds}s", r, om, x, W.Params(max_tokens=16, beam_size=5))
