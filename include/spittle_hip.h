@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 7
+#define SPT_ABI_VERSION 8
 
 typedef enum {
     SPT_OK = 0,
@@ -238,7 +238,8 @@ spt_status spt_debug_ggml_tokenize(const char* model_path, const char* text, int
 spt_status spt_debug_ggml_dequant(int32_t ggml_type, const void* src, int64_t n, float* dst);
 
 /* ================================================================================================
- * ABI 6: Parakeet-V3 (NeMo FastConformer-TDT), the app's other local engine.
+ * ABI 6: Parakeet-V3 (NeMo FastConformer-TDT), the app's other local engine;
+ * ABI 8: spt_parakeet_create takes the app's model directory (the int8 ONNX export) natively.
  *
  * In the reference TranscriptionManager owns a transcribe_rs ParakeetEngine through
  * LoadedEngine::Parakeet and calls (src-tauri/src/managers/transcription.rs):
@@ -311,9 +312,25 @@ typedef struct {
 
 void spt_parakeet_default_model_params(spt_pk_model_params* p);
 void spt_parakeet_default_infer_params(spt_pk_infer_params* p);
-/* spec: "synthetic:parakeet-tdt-0.6b-v3[:layers=N][:seed=S]" or "synthetic:parakeet-test-small[...]" */
+/* model_spec: the app's model directory (below; the weights are dequantised and placed, vocab.txt
+ * becomes the vocabulary), or "synthetic:parakeet-tdt-0.6b-v3[:layers=N][:seed=S]" /
+ * "synthetic:parakeet-test-small[...]" (seeded weights; real ones through spt_parakeet_set_tensor) */
 spt_status spt_parakeet_create(const char* model_spec, const spt_pk_model_params* params, spt_pk_ctx** out,
                                char* err, size_t errlen);
+
+/* The model directory the app downloads (parakeet-tdt-0.6b-v3-int8, the onnx-asr export that
+ * transcribe-rs reads: encoder-model[.int8].onnx, decoder_joint-model[.int8].onnx, vocab.txt;
+ * model_catalog.json:229-241) is also what spt_parakeet_create takes as model_spec -- this is the
+ * same loader without a device: parse, dequantise (int8 / uint8 + scale + zero point, per tensor or
+ * per channel), map onto the engine's tensor ids (NeMo layouts), infer the dimensions.
+ * info->reserved0 receives the number of dequantised initializers.  Host memory only. */
+typedef struct spt_pk_onnx spt_pk_onnx;
+spt_status spt_parakeet_onnx_open(const char* dir, spt_pk_onnx** out, spt_pk_model_info* info, char* err, size_t errlen);
+/* a tensor's f32 values (NeMo layout) by engine tensor id: its element count, or -1 */
+int64_t spt_parakeet_onnx_tensor(const spt_pk_onnx* h, int32_t tensor_id, const float** data);
+/* vocab.txt's piece for a token id (NULL past the vocabulary or without vocab.txt) */
+const char* spt_parakeet_onnx_piece(const spt_pk_onnx* h, int32_t token_id);
+void spt_parakeet_onnx_close(spt_pk_onnx* h);
 void spt_parakeet_destroy(spt_pk_ctx* ctx);
 const char* spt_parakeet_last_error(const spt_pk_ctx* ctx);
 spt_status spt_parakeet_info(const spt_pk_ctx* ctx, spt_pk_model_info* info);

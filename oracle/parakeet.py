@@ -64,6 +64,7 @@ def lib():
         L.po_encode.argtypes = [C.c_void_p, fp, C.c_int, fp]
         L.po_decode.argtypes = [C.c_void_p, fp, C.c_int, C.c_int, ip, ip, fp, fp, C.c_int]
         L.po_decode_gaps.argtypes = [C.c_void_p, fp, C.c_int, C.c_int, ip, ip, fp, fp, fp, C.c_int]
+        L.po_set_tensor.argtypes = [C.c_void_p, C.c_int, fp, C.c_int64]
         L.po_tensor.restype = C.c_int64
         L.po_tensor.argtypes = [C.c_void_p, C.c_int, C.POINTER(fp)]
         _lib = L
@@ -122,6 +123,11 @@ class Model:
         if n < 0:
             raise KeyError(tid)
         return np.ctypeslib.as_array(ptr, shape=(n,)).copy()
+
+    def set_tensor(self, tid: int, data: np.ndarray) -> None:
+        a = np.ascontiguousarray(data, dtype=np.float32).ravel()
+        if lib().po_set_tensor(self._p, int(tid), _f(a), a.size) != 0:
+            raise KeyError(tid)
 
     def encode(self, mel_: np.ndarray) -> np.ndarray:
         mel_ = np.ascontiguousarray(mel_, dtype=np.float32)

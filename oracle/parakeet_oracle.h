@@ -81,6 +81,8 @@ int po_decode_gaps(po_model* m, const float* enc, int T3, int max_symbols, int* 
                    float* top2, float* gmin, int cap);
 /* a weight tensor by id (contract with the engine): its element count, or -1 */
 int64_t po_tensor(po_model* m, int tid, const float** data);
+/* replace a weight tensor (the values a loaded model file holds); 0, or -1 on an unknown id / size */
+int po_set_tensor(po_model* m, int tid, const float* data, int64_t n);
 
 #ifdef __cplusplus
 }

@@ -226,6 +226,16 @@ int64_t po_tensor(po_model* m, int tid, const float** data) {
     return -1;
 }
 
+int po_set_tensor(po_model* m, int tid, const float* data, int64_t n) {
+    for (int i = 0; i < m->n_t; i++)
+        if (m->t[i].tid == tid) {
+            if (m->t[i].n != n) return -1;
+            memcpy(*m->t[i].slot, data, sizeof(float) * (size_t)n);
+            return 0;
+        }
+    return -1;
+}
+
 /* ------------------------------------------------------------------ preprocessor */
 /* valid frames: NeMo FilterbankFeatures.get_seq_len = (n + 2*256 - 512) // 160 (HF
  * feature_extraction_parakeet.py:263-265); the STFT's last centred frame is not one of them */

@@ -32,7 +32,8 @@ EXPORTS = [
     "spt_parakeet_set_tensor", "spt_parakeet_set_vocab", "spt_parakeet_transcribe", "spt_parakeet_transcribe_batch",
     "spt_parakeet_transcribe_batch_device", "spt_parakeet_result_free", "spt_parakeet_get_timings",
     "spt_parakeet_debug_mel", "spt_parakeet_debug_encode", "spt_parakeet_debug_decode", "spt_parakeet_debug_last_encoder",
-    "spt_parakeet_debug_weight_checksum",
+    "spt_parakeet_debug_weight_checksum", "spt_parakeet_onnx_open", "spt_parakeet_onnx_tensor",
+    "spt_parakeet_onnx_piece", "spt_parakeet_onnx_close",
     # ABI 7: capture-side resampler
     "spt_resampler_create", "spt_resampler_info", "spt_resample_output_len", "spt_resample",
     "spt_resampler_last_error", "spt_resampler_destroy",
@@ -171,6 +172,12 @@ def load():
     L.spt_parakeet_default_model_params.argtypes = [C.POINTER(PkModelParams)]
     L.spt_parakeet_default_infer_params.argtypes = [C.POINTER(PkInferParams)]
     L.spt_parakeet_create.argtypes = [C.c_char_p, C.POINTER(PkModelParams), C.POINTER(vp), C.c_char_p, C.c_size_t]
+    L.spt_parakeet_onnx_open.argtypes = [C.c_char_p, C.POINTER(vp), C.POINTER(PkModelInfo), C.c_char_p, C.c_size_t]
+    L.spt_parakeet_onnx_tensor.restype = C.c_int64
+    L.spt_parakeet_onnx_tensor.argtypes = [vp, C.c_int32, C.POINTER(C.POINTER(C.c_float))]
+    L.spt_parakeet_onnx_piece.restype = C.c_char_p
+    L.spt_parakeet_onnx_piece.argtypes = [vp, C.c_int32]
+    L.spt_parakeet_onnx_close.argtypes = [vp]
     L.spt_parakeet_destroy.argtypes = [vp]
     L.spt_parakeet_last_error.argtypes = [vp]
     L.spt_parakeet_last_error.restype = C.c_char_p
@@ -206,7 +213,9 @@ def load():
     for fn in EXPORTS:
         if fn.startswith("spt_parakeet_") and fn not in ("spt_parakeet_default_model_params",
                                                           "spt_parakeet_default_infer_params", "spt_parakeet_destroy",
-                                                          "spt_parakeet_last_error", "spt_parakeet_result_free"):
+                                                          "spt_parakeet_last_error", "spt_parakeet_result_free",
+                                                          "spt_parakeet_onnx_tensor", "spt_parakeet_onnx_piece",
+                                                          "spt_parakeet_onnx_close"):
             getattr(L, fn).restype = C.c_int
     for fn in ("spt_weights_arena", "spt_weights_commit", "spt_ctx_create_replicas", "spt_transcribe_batch_replicas",
                "spt_weights_export", "spt_weights_import", "spt_ctx_info", "spt_transcribe", "spt_transcribe_batch", "spt_transcribe_batch_device",

@@ -335,7 +335,7 @@ spt_status run_windows(spt_ctx* c, std::vector<Window>& win, size_t n_utt, const
 
 extern "C" {
 
-const char* spt_version(void) { return "spittle_amd 0.8.0 (gfx950, ABI 7)"; }
+const char* spt_version(void) { return "spittle_amd 0.9.0 (gfx950, ABI 8)"; }
 
 const char* spt_language_code(int32_t lang_id) { return spt::lang_code(lang_id); }
 

@@ -18,11 +18,16 @@
 #include "common.h"
 #include "kernels.h"
 #include "parakeet.h"
+#include "pk_onnx.h"
 
 struct spt_pk_ctx {
     std::unique_ptr<spt::ParakeetEngine> eng;
     std::vector<std::string> pieces;
     std::string spec, err;
+};
+
+struct spt_pk_onnx {  // a parsed model directory (host memory only)
+    spt::PkOnnxModel m;
 };
 
 namespace {
@@ -211,9 +216,27 @@ spt_status spt_parakeet_create(const char* model_spec, const spt_pk_model_params
     spt::PkDims dm;
     uint64_t seed = mp.seed;
     std::string perr;
-    if (!spt::parse_parakeet_spec(model_spec, &dm, &seed, &perr)) {
-        set_err(err, errlen, std::string("unsupported Parakeet model spec '") + model_spec +
-                                 "': use a synthetic spec and load real weights with spt_parakeet_set_tensor");
+    // the app's model directory (catalog parakeet-tdt-0.6b-v3-int8: the onnx-asr export), parsed on
+    // the host before any device work; or a synthetic spec
+    std::unique_ptr<spt::PkOnnxModel> onnx;
+    if (spt::is_parakeet_onnx_dir(model_spec)) {
+        onnx.reset(new (std::nothrow) spt::PkOnnxModel());
+        if (!onnx) return SPT_ERR_OOM;
+        try {
+            if (!spt::load_parakeet_onnx(model_spec, onnx.get(), &perr)) {
+                set_err(err, errlen, perr);
+                return SPT_ERR_LOAD;
+            }
+        } catch (const std::exception& e) {  // std::bad_alloc on absurd shapes
+            set_err(err, errlen, std::string("loading ") + model_spec + ": " + e.what());
+            return SPT_ERR_LOAD;
+        }
+        dm = onnx->dims;
+        mp.flags |= SPT_PK_WEIGHTS_EMPTY;
+    } else if (!spt::parse_parakeet_spec(model_spec, &dm, &seed, &perr)) {
+        set_err(err, errlen, std::string("unsupported Parakeet model '") + model_spec +
+                                 "': expected the model directory (encoder-model[.int8].onnx, decoder_joint-model[.int8].onnx, "
+                                 "vocab.txt) or a synthetic spec");
         return SPT_ERR_LOAD;
     }
     if (!perr.empty()) {
@@ -237,6 +260,16 @@ spt_status spt_parakeet_create(const char* model_spec, const spt_pk_model_params
         const int dt = mp.dtype == SPT_DTYPE_F16 ? spt::DT_F16 : mp.dtype == SPT_DTYPE_BF16 ? spt::DT_BF16 : spt::DT_F32;
         c->eng.reset(new spt::ParakeetEngine(dm, dt, mp.device, mp.max_batch, max_samples, seed,
                                              !(mp.flags & SPT_PK_WEIGHTS_EMPTY)));
+        if (onnx) {
+            for (int tid : c->eng->tensor_ids())
+                if (!onnx->tensors.count(tid))
+                    throw std::runtime_error(std::string(model_spec) + ": no tensor for " + spt::pk_tensor_name(tid));
+            for (auto& kv : onnx->tensors) {  // host copies freed as they land
+                c->eng->set_tensor(kv.first, kv.second.data(), (int64_t)kv.second.size());
+                std::vector<float>().swap(kv.second);
+            }
+            c->pieces = onnx->pieces;
+        }
     } catch (const std::exception& e) {
         set_err(err, errlen, e.what());
         const spt_status s = classify(e);
@@ -249,6 +282,56 @@ spt_status spt_parakeet_create(const char* model_spec, const spt_pk_model_params
 }
 
 void spt_parakeet_destroy(spt_pk_ctx* ctx) { delete ctx; }
+
+spt_status spt_parakeet_onnx_open(const char* dir, spt_pk_onnx** out, spt_pk_model_info* info, char* err,
+                                  size_t errlen) {
+    if (!dir || !out) {
+        set_err(err, errlen, "null argument");
+        return SPT_ERR_INVALID_ARG;
+    }
+    *out = nullptr;
+    if (!spt::is_parakeet_onnx_dir(dir)) {
+        set_err(err, errlen, std::string(dir) + ": not a Parakeet model directory (no encoder-model[.int8].onnx)");
+        return SPT_ERR_LOAD;
+    }
+    std::unique_ptr<spt_pk_onnx> h(new (std::nothrow) spt_pk_onnx());
+    if (!h) return SPT_ERR_OOM;
+    std::string e;
+    try {
+        if (!spt::load_parakeet_onnx(dir, &h->m, &e)) {
+            set_err(err, errlen, e);
+            return SPT_ERR_LOAD;
+        }
+    } catch (const std::exception& x) {
+        set_err(err, errlen, std::string("loading ") + dir + ": " + x.what());
+        return SPT_ERR_LOAD;
+    }
+    if (info) {
+        memset(info, 0, sizeof(*info));
+        const spt::PkDims& d = h->m.dims;
+        info->n_mels = d.n_mels; info->d = d.d; info->n_layers = d.n_layers; info->n_heads = d.n_heads; info->ff = d.ff;
+        info->sub_ch = d.sub_ch; info->conv_k = d.conv_k; info->pred = d.pred; info->n_vocab = d.n_vocab;
+        info->n_dur = d.n_dur;
+        info->reserved0 = h->m.n_quantized;
+    }
+    *out = h.release();
+    return SPT_OK;
+}
+
+int64_t spt_parakeet_onnx_tensor(const spt_pk_onnx* h, int32_t tensor_id, const float** data) {
+    if (!h || !data) return -1;
+    auto it = h->m.tensors.find(tensor_id);
+    if (it == h->m.tensors.end()) return -1;
+    *data = it->second.data();
+    return (int64_t)it->second.size();
+}
+
+const char* spt_parakeet_onnx_piece(const spt_pk_onnx* h, int32_t token_id) {
+    if (!h || token_id < 0 || (size_t)token_id >= h->m.pieces.size()) return nullptr;
+    return h->m.pieces[token_id].c_str();
+}
+
+void spt_parakeet_onnx_close(spt_pk_onnx* h) { delete h; }
 
 const char* spt_parakeet_last_error(const spt_pk_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 

@@ -96,7 +96,7 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     esz_ = dt_ == DT_BF16 ? 2 : 4;
     cp_ = ((dm_.n_mels + 63) / 64) * 64;
     if ((3 * cp_ * esz_) % 128) cp_ = ((dm_.n_mels + 127) / 128) * 128;
-    if (const char* g = getenv("SPT_DECODE_GROUPS")) n_groups_ = std::max(1, std::min(2, atoi(g)));
+    if (const char* g = getenv("SPT_DECODE_GROUPS")) n_groups_ = std::max(1, std::min(4, atoi(g)));
     if (const char* v = getenv("SPT_FUSED_QKV")) fused_qkv_ = atoi(v) != 0;
     if (const char* v = getenv("SPT_XATTN_SPLIT")) xsplit_ = std::max(1, std::min(4, atoi(v)));
     // cross-attention key split: fixed per engine (never per batch).  The fc2 K split (2; r1

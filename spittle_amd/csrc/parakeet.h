@@ -56,6 +56,11 @@ public:
     // canonical NeMo layout) -- the path real checkpoints take
     void set_tensor(int tid, const float* host, int64_t n);
     bool has_tensor(int tid) const { return table_.count(tid) != 0; }
+    std::vector<int> tensor_ids() const {
+        std::vector<int> v;
+        for (auto& kv : table_) v.push_back(kv.first);
+        return v;
+    }
     int64_t tensor_numel(int tid) const;
 
     // B utterances, pcm_dev + b * stride (device); n[b] <= max_samples

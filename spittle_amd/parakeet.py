@@ -10,10 +10,11 @@ transcription.rs uses it):
   * ``unload_model()``                                       (transcription.rs:175-208)
   * ``TranscriptionResult { text, segments }``; the app uses ``.text`` (transcription.rs:537-546)
 
-Model sources: ``"synthetic:parakeet-tdt-0.6b-v3[:layers=N][:seed=S]"`` (seeded weights, the
-benchmark), or a NeMo ``.nemo`` checkpoint (a tar holding model_config.yaml, model_weights.ckpt
-and the tokenizer), mapped tensor by tensor onto the engine (load_nemo).  The app's catalog
-model is the ONNX int8 export of the same network; ONNX graphs are not parsed here.
+Model sources: the app's model directory -- the catalog's parakeet-tdt-0.6b-v3-int8, the int8 ONNX
+export transcribe-rs reads (encoder-model.int8.onnx, decoder_joint-model.int8.onnx, vocab.txt) --
+parsed, dequantised and placed by the native loader inside spt_parakeet_create (spittle_amd/csrc/
+pk_onnx.cpp; no Python on that path); ``"synthetic:parakeet-tdt-0.6b-v3[:layers=N][:seed=S]"``
+(seeded weights, the benchmark); or a NeMo ``.nemo`` checkpoint (load_nemo, tensor by tensor).
 Everything below the boundary runs on the GPU (libspittle_hip.so); there is no CPU path.
 """
 from __future__ import annotations
@@ -48,8 +49,8 @@ class ParakeetModelParams:
 
     @staticmethod
     def int8() -> "ParakeetModelParams":
-        """The app's choice (transcription.rs:281).  The int8 ONNX export's quantisation is not
-        reproduced; the network runs with an fp16 encoder."""
+        """The app's choice (transcription.rs:281): the int8 export's weights are dequantised at load
+        and the network runs with an fp16 encoder."""
         return ParakeetModelParams()
 
     @staticmethod
@@ -90,12 +91,14 @@ class ParakeetEngine:
         params = params or ParakeetModelParams.int8()
         self.unload_model()
         path = str(path)
-        if path.startswith("synthetic:"):
+        if path.startswith("synthetic:") or is_onnx_dir(path):
+            # the app's model directory (the int8 ONNX export) is parsed natively by spt_parakeet_create
             self._create(path, params, empty=False)
             return
         nemo = _find_nemo(path)
         if nemo is None:
-            raise TranscriptionError(L.SPT_ERR_LOAD, f"{path}: no .nemo checkpoint (ONNX exports are not supported)")
+            raise TranscriptionError(L.SPT_ERR_LOAD, f"{path}: neither an ONNX model directory "
+                                                     "(encoder-model[.int8].onnx) nor a .nemo checkpoint")
         load_nemo(self, nemo, params)
 
     def load_model(self, path: str) -> None:
@@ -292,6 +295,51 @@ def nemo_key_map(n_layers: int) -> Dict[str, int]:
         m[nm + ".weight"] = i
         m[nm + ".bias"] = i + 1
     return m
+
+
+def is_onnx_dir(path: str) -> bool:
+    """The layout of the catalog's parakeet-tdt-0.6b-v3-int8 directory (onnx-asr export)."""
+    return os.path.isdir(path) and any(os.path.isfile(os.path.join(path, f))
+                                       for f in ("encoder-model.int8.onnx", "encoder-model.onnx"))
+
+
+class OnnxModelDir:
+    """The native model-directory loader without a device (spt_parakeet_onnx_*): dimensions,
+    dequantised tensors by engine id, vocabulary -- what spt_parakeet_create places."""
+
+    def __init__(self, path: str):
+        self._lib = L.load()
+        self._h = C.c_void_p()
+        self.info = L.PkModelInfo()
+        err = C.create_string_buffer(512)
+        st = self._lib.spt_parakeet_onnx_open(str(path).encode(), C.byref(self._h), C.byref(self.info), err, 512)
+        if st != L.SPT_OK:
+            raise TranscriptionError(st, err.value.decode())
+        self.n_quantized = self.info.reserved0
+
+    def dims(self) -> Dict[str, int]:
+        return {k: getattr(self.info, k) for k in ("n_mels", "d", "n_layers", "n_heads", "ff", "sub_ch", "conv_k",
+                                                    "pred", "n_vocab", "n_dur")}
+
+    def tensor(self, tid: int) -> Optional[np.ndarray]:
+        p = C.POINTER(C.c_float)()
+        n = self._lib.spt_parakeet_onnx_tensor(self._h, int(tid), C.byref(p))
+        return None if n < 0 else np.ctypeslib.as_array(p, shape=(n,)).copy()
+
+    def piece(self, i: int) -> Optional[str]:
+        s = self._lib.spt_parakeet_onnx_piece(self._h, int(i))
+        return None if s is None else s.decode()
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.spt_parakeet_onnx_close(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def _find_nemo(path: str) -> Optional[str]:

@@ -5,7 +5,13 @@
  *                       -> read text / segments -> spt_result_free    (transcription.rs:494-503)
  *   unload_model        spt_ctx_destroy                               (transcription.rs:175-208)
  * then the same again (the idle watcher unloads, the next dictation reloads), and the error
- * paths the binding maps to Err(..).  Exit 0 = every step behaved. */
+ * paths the binding maps to Err(..).  With a third argument, the Parakeet sequence of
+ * HipParakeetEngine on that model directory (the catalog's int8 ONNX export layout):
+ *   load_model_with_params(&path, ParakeetModelParams::int8())  spt_parakeet_create(dir)
+ *                                                                (transcription.rs:278-297)
+ *   transcribe_samples(.., Segment)   spt_parakeet_transcribe    (transcription.rs:505-513)
+ * (with --link-only: the host-only loader, spt_parakeet_onnx_open, no device).
+ * Exit 0 = every step behaved. */
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -110,6 +116,31 @@ static int resampler_session(void) {
     return 0;
 }
 
+/* HipParakeetEngine: load the model directory, transcribe with Segment timestamps, read, free */
+static int parakeet_session(const char* dir, const float* pcm, size_t n) {
+    spt_pk_model_params mp;
+    spt_parakeet_default_model_params(&mp); /* ParakeetModelParams::int8(): fp16 encoder */
+    mp.max_batch = 2;
+    mp.max_seconds = 8.0f;
+    spt_pk_ctx* ctx = NULL;
+    char err[512] = {0};
+    spt_status st = spt_parakeet_create(dir, &mp, &ctx, err, sizeof err);
+    if (st != SPT_OK) fprintf(stderr, "parakeet create: %s\n", err);
+    CHECK(st == SPT_OK && ctx, "spt_parakeet_create(model directory)");
+    spt_pk_infer_params ip;
+    spt_parakeet_default_infer_params(&ip);
+    CHECK(ip.timestamp_granularity == SPT_PK_TS_SEGMENT, "Segment granularity by default");
+    spt_pk_result* r = NULL;
+    st = spt_parakeet_transcribe(ctx, pcm, n, &ip, &r);
+    if (st != SPT_OK) fprintf(stderr, "parakeet transcribe: %s\n", spt_parakeet_last_error(ctx));
+    CHECK(st == SPT_OK && r && r->text, "spt_parakeet_transcribe");
+    for (int i = 0; i < r->n_segments; ++i) CHECK(r->segments[i].end > r->segments[i].start, "segment times");
+    printf("parakeet: %d tokens, %d segments, text \"%.60s\"\n", r->n_tokens, r->n_segments, r->text);
+    spt_parakeet_result_free(r);
+    spt_parakeet_destroy(ctx);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     const char* spec = argc > 1 ? argv[1] : "synthetic:tiny";
     printf("%s\n", spt_version());
@@ -117,7 +148,19 @@ int main(int argc, char** argv) {
     char err[256];
     CHECK(spt_ctx_create("/nonexistent/ggml-base.bin", NULL, &ctx, err, sizeof err) == SPT_ERR_LOAD && !ctx,
           "missing model file");
-    if (argc > 2 && strcmp(argv[2], "--link-only") == 0) return 0;
+    if (argc > 2 && strcmp(argv[2], "--link-only") == 0) {
+        if (argc > 3) { /* the model-directory loader needs no device */
+            spt_pk_onnx* h = NULL;
+            spt_pk_model_info info;
+            spt_status st = spt_parakeet_onnx_open(argv[3], &h, &info, err, sizeof err);
+            if (st != SPT_OK) fprintf(stderr, "onnx open: %s\n", err);
+            CHECK(st == SPT_OK && h, "spt_parakeet_onnx_open");
+            printf("parakeet dir: d %d, layers %d, heads %d, vocab %d, %d dequantised\n", info.d, info.n_layers,
+                   info.n_heads, info.n_vocab, info.reserved0);
+            spt_parakeet_onnx_close(h);
+        }
+        return 0;
+    }
     const size_t n = 16000 * 6;
     float* pcm = (float*)malloc(n * sizeof(float));
     for (size_t i = 0; i < n; ++i)
@@ -126,6 +169,7 @@ int main(int argc, char** argv) {
     int rc = one_session(spec, pcm, n);
     if (!rc) rc = one_session(spec, pcm, n); /* unload, then load again */
     if (!rc) rc = resampler_session();
+    if (!rc && argc > 3) rc = parakeet_session(argv[3], pcm, n);
     free(pcm);
     if (!rc) printf("capi_smoke ok\n");
     return rc;

@@ -20,16 +20,29 @@ def _build(tmp_path):
     return exe
 
 
+def _model_dir(tmp_path):
+    """the catalog's parakeet-tdt-0.6b-v3-int8 layout (tests/onnx_parakeet.py), test-small dims"""
+    from oracle import parakeet as P
+    from tests import onnx_parakeet
+    d = P.dims_for("test-small")
+    path = str(tmp_path / "parakeet-tdt-0.6b-v3-int8")
+    onnx_parakeet.write_dir(path, P.Model(d, seed=3), d, quant="int8")
+    return path
+
+
 def test_c_program_compiles_and_links(tmp_path):
     exe = _build(tmp_path)
-    r = subprocess.run([exe, "synthetic:tiny", "--link-only"], capture_output=True, text=True, timeout=60)
+    r = subprocess.run([exe, "synthetic:tiny", "--link-only", _model_dir(tmp_path)], capture_output=True, text=True,
+                       timeout=60)
     assert r.returncode == 0, r.stderr
-    assert "ABI 7" in r.stdout
+    assert "ABI 8" in r.stdout
+    assert "parakeet dir: d 256, layers 2, heads 4, vocab 1024" in r.stdout
 
 
 @pytest.mark.gpu
 def test_c_program_runs_the_binding_sequence(tmp_path):
     exe = _build(tmp_path)
-    r = subprocess.run([exe, "synthetic:tiny"], capture_output=True, text=True, timeout=240)
+    r = subprocess.run([exe, "synthetic:tiny", "--run", _model_dir(tmp_path)], capture_output=True, text=True,
+                       timeout=240)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "capi_smoke ok" in r.stdout
+    assert "parakeet: " in r.stdout and "capi_smoke ok" in r.stdout

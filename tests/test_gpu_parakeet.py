@@ -294,6 +294,39 @@ def test_f32_engine_matches_hf_fixtures(name, cfg, spec):
     om.close()
 
 
+def test_onnx_model_dir_end_to_end(tmp_path):
+    """The app's own call on the catalog's model directory layout (parakeet-tdt-0.6b-v3-int8: int8
+    ONNX export + vocab.txt; /root/reference/src-tauri/src/managers/transcription.rs:278-297,
+    505-513): ParakeetEngine.load_model_with_params(dir) -> spt_parakeet_create parses, dequantises
+    and places every tensor natively.  The f32 engine against the oracle holding the same
+    dequantised weights: tokens and frames equal (decision margins over F32_GAP), text from
+    vocab.txt; the app's int8() params (fp16 encoder) load and run too."""
+    from spittle_amd import ParakeetEngine, ParakeetModelParams
+    from spittle_amd.parakeet import OnnxModelDir
+    from tests import onnx_parakeet
+    d = P.dims_for("test-small")
+    om = P.Model(d, seed=SEED)
+    path = str(tmp_path / "parakeet-tdt-0.6b-v3-int8")
+    exp = onnx_parakeet.write_dir(path, om, d, quant="int8")
+    h = OnnxModelDir(path)
+    for tid in exp:
+        om.set_tensor(tid, h.tensor(tid))
+    h.close()
+    e = ParakeetEngine()
+    e.load_model_with_params(path, ParakeetModelParams(dtype="f32", max_batch=2, max_seconds=8.0))
+    assert e.info()["n_layers"] == 2 and e.info()["n_vocab"] == d.n_vocab
+    pcm = synth_audio(40, 16000 * 3 + 500)
+    r = e.transcribe_samples(pcm, _tok_params())
+    i, n_or, gap = _agree(r, om, om.encode(P.mel(pcm)), F32_GAP)
+    assert len(r.tokens) > 0
+    assert r.text == "".join(onnx_parakeet.vocab_piece(t) for t in r.tokens).replace("▁", " ").strip()
+    e.unload_model()
+    e.load_model_with_params(path, ParakeetModelParams.int8())
+    r16 = e.transcribe_samples(pcm)
+    assert r16.text and len(r16.tokens) > 0
+    e.unload_model()
+
+
 def test_c5_streaming_b64_full_size():
     """BASELINE config 5 at the bench's own shape: parakeet-tdt-0.6b-v3 (24 layers, d 1024), fp16
     encoder, 64 concurrent 1 s windows in one pass (832 encoder rows: the tile-128/256 GEMMs),
