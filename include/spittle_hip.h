@@ -385,6 +385,53 @@ spt_status spt_resample(spt_resampler* r, const float* pcm, size_t n_samples, fl
 const char* spt_resampler_last_error(const spt_resampler* r);
 void spt_resampler_destroy(spt_resampler* r);
 
+/* ================================================================================================
+ * ABI 8: the capture-side voice-activity gate.  The recorder's consumer thread
+ * pushes every 480-sample (30 ms) frame from the FrameResampler through
+ *   SmoothedVad::new(Box::new(SileroVad::new("resources/models/silero_vad_v4.onnx", 0.3)), 15, 15, 2)
+ * (src-tauri/src/managers/audio.rs:132-134, 295-307) and appends what it returns as Speech to the
+ * recording (audio_toolkit/audio/recorder.rs:284-301); Cmd::Start resets the smoothing (:343-349).
+ *
+ *   spt_vad_create(model_path, params)  = SileroVad::new + SmoothedVad::new  (the model file the app
+ *                                         ships is read natively: ONNX graph, 16 kHz branch)
+ *   spt_vad_push(pcm, n)                = push_frame for each 480-sample frame in order (a trailing
+ *                                         partial frame is kept as Speech, like the recorder's
+ *                                         unwrap_or); result: the kept samples, each frame's speech
+ *                                         probability and VadFrame kind (0 Noise, 1 Speech(frame),
+ *                                         2 Speech(prefill + frame))
+ *   spt_vad_reset(v, 0)                 = SmoothedVad::reset (the Silero LSTM state carries, as in the
+ *                                         app); reset_model_state = 1 also zeroes it (a new SileroVad)
+ *
+ * The network runs on the device: every frame's convolutional front end at once, then the
+ * two-layer LSTM recurrence over the frames in one workgroup (its state kept between calls).
+ * ============================================================================================== */
+typedef struct spt_vad spt_vad;
+typedef struct {
+    float threshold;          /* speech when prob > threshold (0.3) */
+    int32_t prefill_frames;   /* 15 */
+    int32_t hangover_frames;  /* 15 */
+    int32_t onset_frames;     /* 2 */
+    int32_t device;
+    int32_t reserved0;
+} spt_vad_params;
+typedef struct {
+    float* samples;           /* the kept audio (Speech frames, prefill at onsets), n_samples long */
+    size_t n_samples;
+    float* prob;              /* per whole frame: Silero's speech probability */
+    uint8_t* kind;            /* per frame (a trailing partial frame included): 0 Noise, 1 Speech, 2 onset */
+    int32_t n_frames;
+    int32_t reserved0;
+    double device_ms;         /* front end + recurrence on the device */
+} spt_vad_result;
+void spt_vad_default_params(spt_vad_params* p);
+spt_status spt_vad_create(const char* model_path, const spt_vad_params* params, spt_vad** out, char* err,
+                          size_t errlen);
+spt_status spt_vad_push(spt_vad* v, const float* pcm, size_t n_samples, spt_vad_result** out);
+void spt_vad_result_free(spt_vad_result* r);
+spt_status spt_vad_reset(spt_vad* v, int32_t reset_model_state);
+const char* spt_vad_last_error(const spt_vad* v);
+void spt_vad_destroy(spt_vad* v);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,4 +1,4 @@
-//! Raw bindings to `include/spittle_hip.h` (ABI 6), the C boundary of the MI355X-native Whisper
+//! Raw bindings to `include/spittle_hip.h` (ABI 8), the C boundary of the MI355X-native Whisper
 //! and Parakeet-V3 backend.  One item per declaration of the header, same names, same layouts (x86-64 SysV; the
 //! layouts are checked field by field against gcc by tests/test_capi.py).  Safe wrappers live in
 //! the `spittle-hip` crate.
@@ -308,6 +308,69 @@ extern "C" {
     ) -> spt_status;
     pub fn spt_resampler_last_error(r: *const spt_resampler) -> *const c_char;
     pub fn spt_resampler_destroy(r: *mut spt_resampler);
+
+    // ---- ABI 8: the app's Parakeet model directory without a device (spt_parakeet_create also
+    // takes the directory itself)
+    pub fn spt_parakeet_onnx_open(
+        dir: *const c_char,
+        out: *mut *mut spt_pk_onnx,
+        info: *mut spt_pk_model_info,
+        err: *mut c_char,
+        errlen: usize,
+    ) -> spt_status;
+    pub fn spt_parakeet_onnx_tensor(h: *const spt_pk_onnx, tensor_id: i32, data: *mut *const f32) -> i64;
+    pub fn spt_parakeet_onnx_piece(h: *const spt_pk_onnx, token_id: i32) -> *const c_char;
+    pub fn spt_parakeet_onnx_close(h: *mut spt_pk_onnx);
+    pub fn spt_parakeet_debug_last_encoder(ctx: *mut spt_pk_ctx, b: i32, out: *mut f32, t3: *mut i32) -> spt_status;
+
+    // ---- ABI 8: voice-activity gate (audio_toolkit/vad: SmoothedVad over SileroVad)
+    pub fn spt_vad_default_params(p: *mut spt_vad_params);
+    pub fn spt_vad_create(
+        model_path: *const c_char,
+        params: *const spt_vad_params,
+        out: *mut *mut spt_vad,
+        err: *mut c_char,
+        errlen: usize,
+    ) -> spt_status;
+    pub fn spt_vad_push(v: *mut spt_vad, pcm: *const f32, n_samples: usize, out: *mut *mut spt_vad_result) -> spt_status;
+    pub fn spt_vad_result_free(r: *mut spt_vad_result);
+    pub fn spt_vad_reset(v: *mut spt_vad, reset_model_state: i32) -> spt_status;
+    pub fn spt_vad_last_error(v: *const spt_vad) -> *const c_char;
+    pub fn spt_vad_destroy(v: *mut spt_vad);
+}
+
+/// Opaque parsed Parakeet model directory (ABI 8).
+#[repr(C)]
+pub struct spt_pk_onnx {
+    _private: [u8; 0],
+}
+
+/// Opaque voice-activity gate (ABI 8).
+#[repr(C)]
+pub struct spt_vad {
+    _private: [u8; 0],
+}
+
+#[repr(C)]
+#[derive(Clone, Copy, Debug)]
+pub struct spt_vad_params {
+    pub threshold: f32,
+    pub prefill_frames: i32,
+    pub hangover_frames: i32,
+    pub onset_frames: i32,
+    pub device: i32,
+    pub reserved0: i32,
+}
+
+#[repr(C)]
+pub struct spt_vad_result {
+    pub samples: *mut f32,
+    pub n_samples: usize,
+    pub prob: *mut f32,
+    pub kind: *mut u8,
+    pub n_frames: i32,
+    pub reserved0: i32,
+    pub device_ms: f64,
 }
 
 /// Opaque capture-side resampler context (ABI 7).

@@ -1,5 +1,6 @@
 //! `HipWhisperEngine` and `HipParakeetEngine`: the `transcribe_rs::TranscriptionEngine` surfaces
-//! Spittle binds to, backed by the MI355X-native library (`libspittle_hip.so`, C ABI 7), plus `HipFrameResampler`.
+//! Spittle binds to, backed by the MI355X-native library (`libspittle_hip.so`, C ABI 8), plus `HipFrameResampler` and
+//! `HipSmoothedVad` (the capture-side resampler and voice-activity gate).
 //!
 //! What it replaces in the app (/root/reference/src-tauri/src/managers/transcription.rs):
 //!
@@ -514,5 +515,80 @@ impl Drop for HipFrameResampler {
     fn drop(&mut self) {
         // SAFETY: created by spt_resampler_create, destroyed once
         unsafe { sys::spt_resampler_destroy(self.r) };
+    }
+}
+
+/// The capture-side voice-activity gate (ABI 8): `SmoothedVad::new(Box::new(SileroVad::new(path,
+/// 0.3)), 15, 15, 2)` of /root/reference/src-tauri/src/managers/audio.rs:132-134 in one object,
+/// the Silero network on the device.  `push_frame` has the app's `VoiceActivityDetector` shape
+/// (audio_toolkit/vad/mod.rs); the app-side adapter is three lines.
+pub struct HipSmoothedVad {
+    v: *mut sys::spt_vad,
+    last: Vec<f32>,
+}
+
+/// `VadFrame` of audio_toolkit/vad/mod.rs
+pub enum HipVadFrame<'a> {
+    Speech(&'a [f32]),
+    Noise,
+}
+
+// SAFETY: the context selects its device on every call and holds no thread-local state
+unsafe impl Send for HipSmoothedVad {}
+
+impl HipSmoothedVad {
+    pub fn new<P: AsRef<Path>>(model_path: P, threshold: f32, prefill: usize, hangover: usize, onset: usize,
+                               device: i32) -> Result<Self, Box<dyn Error>> {
+        let path = CString::new(model_path.as_ref().to_string_lossy().as_bytes())?;
+        let mut p = sys::spt_vad_params { threshold, prefill_frames: prefill as i32, hangover_frames: hangover as i32,
+                                          onset_frames: onset as i32, device, reserved0: 0 };
+        if !(0.0..=1.0).contains(&threshold) {
+            return Err("threshold must be between 0.0 and 1.0".into());
+        }
+        let mut v = std::ptr::null_mut();
+        let mut err = vec![0 as c_char; 512];
+        // SAFETY: every pointer is valid for the call
+        let st = unsafe { sys::spt_vad_create(path.as_ptr(), &mut p, &mut v, err.as_mut_ptr(), err.len()) };
+        if st != sys::SPT_OK {
+            // SAFETY: the library NUL-terminates the message inside the buffer
+            let msg = unsafe { CStr::from_ptr(err.as_ptr()) }.to_string_lossy().into_owned();
+            return Err(status_error("vad", st, msg));
+        }
+        Ok(Self { v, last: Vec::new() })
+    }
+
+    /// One 30 ms frame (or a whole recorded stream, frame after frame): the kept samples.
+    pub fn push_frame<'a>(&'a mut self, frame: &'a [f32]) -> Result<HipVadFrame<'a>, Box<dyn Error>> {
+        let mut r = std::ptr::null_mut();
+        // SAFETY: the frame outlives the call; the result is library-owned and freed below
+        let st = unsafe { sys::spt_vad_push(self.v, frame.as_ptr(), frame.len(), &mut r) };
+        if st != sys::SPT_OK {
+            // SAFETY: the message lives in the context until its next call
+            let msg = unsafe { CStr::from_ptr(sys::spt_vad_last_error(self.v)) }.to_string_lossy().into_owned();
+            return Err(status_error("vad push", st, msg));
+        }
+        // SAFETY: r is a valid result until spt_vad_result_free
+        let (kept, speech) = unsafe {
+            let res = &*r;
+            let kept = if res.n_samples > 0 { std::slice::from_raw_parts(res.samples, res.n_samples).to_vec() } else { Vec::new() };
+            (kept, res.n_frames > 0 && *res.kind != 0)
+        };
+        // SAFETY: freed once
+        unsafe { sys::spt_vad_result_free(r) };
+        self.last = kept;
+        Ok(if speech { HipVadFrame::Speech(&self.last) } else { HipVadFrame::Noise })
+    }
+
+    /// `SmoothedVad::reset` (the Silero state carries over, as in the app)
+    pub fn reset(&mut self) {
+        // SAFETY: a live context
+        unsafe { sys::spt_vad_reset(self.v, 0) };
+    }
+}
+
+impl Drop for HipSmoothedVad {
+    fn drop(&mut self) {
+        // SAFETY: created by spt_vad_create, destroyed once
+        unsafe { sys::spt_vad_destroy(self.v) };
     }
 }

@@ -37,6 +37,9 @@ EXPORTS = [
     # ABI 7: capture-side resampler
     "spt_resampler_create", "spt_resampler_info", "spt_resample_output_len", "spt_resample",
     "spt_resampler_last_error", "spt_resampler_destroy",
+    # ABI 8: voice-activity gate
+    "spt_vad_default_params", "spt_vad_create", "spt_vad_push", "spt_vad_result_free", "spt_vad_reset",
+    "spt_vad_last_error", "spt_vad_destroy",
 ]
 SPT_PK_WEIGHTS_EMPTY = 1
 SPT_PK_TS_TOKEN, SPT_PK_TS_WORD, SPT_PK_TS_SEGMENT = 0, 1, 2
@@ -113,6 +116,17 @@ class PkModelInfo(C.Structure):
 class PkTimings(C.Structure):
     _fields_ = [(n, C.c_double) for n in ("mel_ms", "encoder_ms", "decode_ms", "total_ms", "h2d_ms")] + \
                [(n, C.c_int32) for n in ("n_steps", "batch", "enc_frames", "reserved0")]
+
+
+class VadParams(C.Structure):
+    _fields_ = [("threshold", C.c_float), ("prefill_frames", C.c_int32), ("hangover_frames", C.c_int32),
+                ("onset_frames", C.c_int32), ("device", C.c_int32), ("reserved0", C.c_int32)]
+
+
+class VadResult(C.Structure):
+    _fields_ = [("samples", C.POINTER(C.c_float)), ("n_samples", C.c_size_t), ("prob", C.POINTER(C.c_float)),
+                ("kind", C.POINTER(C.c_uint8)), ("n_frames", C.c_int32), ("reserved0", C.c_int32),
+                ("device_ms", C.c_double)]
 
 
 _lib = None
@@ -210,6 +224,20 @@ def load():
     L.spt_resampler_last_error.restype = C.c_char_p
     L.spt_resampler_destroy.argtypes = [vp]
     L.spt_resampler_destroy.restype = None
+    L.spt_vad_default_params.argtypes = [C.POINTER(VadParams)]
+    L.spt_vad_default_params.restype = None
+    L.spt_vad_create.argtypes = [C.c_char_p, C.POINTER(VadParams), C.POINTER(vp), C.c_char_p, C.c_size_t]
+    L.spt_vad_create.restype = C.c_int
+    L.spt_vad_push.argtypes = [vp, fp, C.c_size_t, C.POINTER(C.POINTER(VadResult))]
+    L.spt_vad_push.restype = C.c_int
+    L.spt_vad_result_free.argtypes = [C.POINTER(VadResult)]
+    L.spt_vad_result_free.restype = None
+    L.spt_vad_reset.argtypes = [vp, C.c_int32]
+    L.spt_vad_reset.restype = C.c_int
+    L.spt_vad_last_error.argtypes = [vp]
+    L.spt_vad_last_error.restype = C.c_char_p
+    L.spt_vad_destroy.argtypes = [vp]
+    L.spt_vad_destroy.restype = None
     for fn in EXPORTS:
         if fn.startswith("spt_parakeet_") and fn not in ("spt_parakeet_default_model_params",
                                                           "spt_parakeet_default_infer_params", "spt_parakeet_destroy",
