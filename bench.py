@@ -275,6 +275,9 @@ def parakeet_bench(device: int, steps: int, warmup: int, with_cpu: bool) -> dict
                                "encoder_roofline": {"bound": "mfma", "flops_per_call": flops, "achieved": round(tf, 1),
                                                     "peak": MFMA_PEAK_F16_TFS, "unit": "TFLOP/s",
                                                     "frac": round(tf / MFMA_PEAK_F16_TFS, 4)}}
+    if only == "stream64":
+        e.unload_model()
+        return out
     med, tot, res, ph = run(w1[:1])
     out["streaming_1s_b1_latency_ms"] = {"median": round(med * 1e3, 3),
                                          "phases_ms": {k: round(v, 3) for k, v in ph.items() if k.endswith("_ms")},

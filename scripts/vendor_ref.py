@@ -20,7 +20,23 @@ def tm(fn, it=20):
     return s.elapsed_time(e) * 1e3 / it  # us
 
 
+import sys
+
 dev = "cuda"
+if "--parakeet" in sys.argv:
+    # Parakeet-V3 encoder GEMMs in f16 at the C5 streaming pass (64 x 13 frames) and offline (8 x 375)
+    for M in (832, 3000):
+        for name, N, K in [("ff1", 4096, 1024), ("qkv", 3072, 1024), ("pw1", 2048, 1024), ("out", 1024, 1024),
+                           ("ff2", 1024, 4096)]:
+            a = torch.randn(M, K, device=dev, dtype=torch.float16)
+            w = torch.randn(N, K, device=dev, dtype=torch.float16)
+            b = torch.randn(N, device=dev, dtype=torch.float16)
+            us = tm(lambda: F.linear(a, w, b))
+            fl = 2.0 * M * N * K
+            print(json.dumps({"op": f"hipblaslt_linear_pk_{name}", "M": M, "N": N, "K": K, "us": round(us, 2),
+                              "TFLOP/s": round(fl / us / 1e6, 1), "frac_of_2500": round(fl / us / 1e6 / 2500, 3)}),
+                  flush=True)
+    sys.exit(0)
 M, d = 8 * 1500, 1280
 for name, N, K in [("qkv", 3 * d, d), ("out", d, d), ("fc1", 4 * d, d), ("fc2", d, 4 * d), ("cross_kv", 64 * d, d)]:
     a = torch.randn(M, K, device=dev, dtype=torch.bfloat16)

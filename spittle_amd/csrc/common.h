@@ -100,4 +100,9 @@ __device__ inline float wave_max(float v) {
 
 __host__ __device__ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) for the calling thread's current device, once
+// per (kernel, device): the attribute is per device, and replica threads drive several devices
+// from one process (r2 advisor finding).  Thread-safe.  Call outside stream capture.
+void ensure_lds_attr(const void* kernel, int bytes);
+
 }  // namespace spt

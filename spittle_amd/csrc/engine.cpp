@@ -117,6 +117,7 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     }
     try {
         gemv_prepare(dt_);
+        gemm_prepare();  // > 64 KiB LDS attributes on this device, before any capture
         alloc_weights();
         if (external_weights) {
             // filled later by import_weights; clear it so a premature use reads zeros, not garbage

@@ -456,10 +456,9 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
 }
 
 template <typename T, int MODE, int ASRC, int RG, int NWV, int CT, int MAXJ, bool EXACT = false>
-void gemv_attr() {
+void gemv_attr() {  // per kernel and device (ensure_lds_attr)
     const int red = NWV * RG * 64 * (int)sizeof(f32x4);
-    HIP_CHECK(hipFuncSetAttribute((const void*)gemv_kernel<T, MODE, ASRC, RG, NWV, CT, MAXJ, EXACT>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, GV_LDS_BYTES + red));
+    ensure_lds_attr((const void*)gemv_kernel<T, MODE, ASRC, RG, NWV, CT, MAXJ, EXACT>, GV_LDS_BYTES + red);
 }
 
 template <typename T, int MODE, int ASRC, int RG, int NWV, int CT, int MAXJ, bool EXACT = false>

@@ -25,8 +25,11 @@
 #include "kernels.h"
 
 #include <algorithm>
-#include <type_traits>
 #include <cstdlib>
+#include <mutex>
+#include <set>
+#include <tuple>
+#include <type_traits>
 
 namespace spt {
 
@@ -84,9 +87,13 @@ __device__ __forceinline__ void epi_store(const GemmArgs& g, int bz, int row, co
     }
 }
 
-template <typename T, int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BM * SLAB];  // [buf][A|W][128 rows][128 B]
+// ST-slot LDS ring (ST x 32 KiB, dynamic for ST > 2): ST - 1 K-slabs in flight while one is
+// computed.  The 16-slab GEMMs of a Parakeet streaming pass (M = 832, K = 1024) and Whisper's
+// smaller shapes give about one workgroup per CU and no other wave to cover a slab's load
+// latency; with two slots every k-step waited for its own DMA round trip.
+template <typename T, int EPI, int ST>
+__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256, 1) put the accumulators in AGPRs + ~90 copies per k-step
+    extern __shared__ __attribute__((aligned(16))) char smem[];  // [slot][A|W][128 rows][128 B]
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 1, wn = wid & 1;
     const int nnt = g.N / BN;
@@ -94,7 +101,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
     const int nwg = gridDim.x, bid = blockIdx.x;
     const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-    const int tm = wg / nnt, tn = wg - tm * nnt;
+    const int nmt = (g.M + BM - 1) / BM;
+    const int tm = g.nmajor ? wg % nmt : wg / nnt, tn = g.nmajor ? wg / nmt : wg % nnt;
     const int m0 = tm * BM, n0 = tn * BN;
     const int bz = blockIdx.z;
     const int Kc = g.K / g.ksplit;  // this workgroup's K range: [blockIdx.y * Kc, + Kc)
@@ -133,12 +141,21 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
     const int nkt = Kc * (int)sizeof(T) / SLAB;
     const int fr = lane & 15, fq = lane >> 4;
 
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    // prologue: slabs 0 .. ST - 2.  Every iteration issues exactly one slab (past the end: the last
+    // slab again, into a free slot), so each wave's vmcnt counts the same instructions everywhere.
+#pragma unroll
+    for (int p = 0; p < ST - 1; ++p) stage(p, min(p, nkt - 1));
     for (int kt = 0; kt < nkt; ++kt) {
-        const int cur = kt & 1;
-        if (kt + 1 < nkt) stage(cur ^ 1, kt + 1);
+        const int cur = kt % ST;
+        // slab kt landed (8 DMA instructions per slab and wave; ST - 2 younger slabs may fly on),
+        // and every wave is done with slab kt - 1, whose slot the next issue overwrites
+        if constexpr (ST == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if constexpr (ST == 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        // a bare s_barrier: __syncthreads()'s release fence would make the compiler drain every
+        // in-flight slab (vmcnt(0)) in front of it
+        asm volatile("s_barrier" ::: "memory");
+        stage((kt + ST - 1) % ST, min(kt + ST - 1, nkt - 1));
         const SPT_LDS char* la = lds_a(cur);
         const SPT_LDS char* lw = lds_w(cur);
         if constexpr (sizeof(T) == 2) {
@@ -186,9 +203,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s >> 2][s & 3], wf[j][s >> 2][s & 3],
                                                                           acc[i][j], 0, 0, 0);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing repeat slabs land before exit
 
     // ---------------------------------------------------------------- epilogue
 #pragma unroll
@@ -551,30 +567,84 @@ void launch_skinny(const GemmArgs& g, hipStream_t st) {
 
 template <int EPI, bool F16>
 void launch_256(const GemmArgs& g, int batch, hipStream_t st) {
-    static bool attr = false;  // > 64 KiB dynamic LDS: set once per kernel
     // staggered wave groups: bitwise-identical results, encoder 21.54 -> 21.28 ms (r2, two A/B pairs);
     // SPT_G2_STAGGER=0 restores the lock-step schedule
     static const bool stg = !getenv("SPT_G2_STAGGER") || atoi(getenv("SPT_G2_STAGGER")) != 0;
-    if (!attr) {
-        HIP_CHECK(hipFuncSetAttribute((const void*)gemm256_kernel<EPI, F16, false>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS_ALL));
-        HIP_CHECK(hipFuncSetAttribute((const void*)gemm256_kernel<EPI, F16, true>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS_ALL));
-        attr = true;
-    }
+    // > 64 KiB dynamic LDS: per kernel and device (gemm_prepare sets them before any capture)
+    ensure_lds_attr((const void*)gemm256_kernel<EPI, F16, false>, G2_LDS_ALL);
+    ensure_lds_attr((const void*)gemm256_kernel<EPI, F16, true>, G2_LDS_ALL);
     dim3 grid(cdiv(g.M, G2_BM) * (g.N / G2_BN), g.ksplit, batch);
     if (stg) hipLaunchKernelGGL((gemm256_kernel<EPI, F16, true>), grid, dim3(512), G2_LDS_ALL, st, g);
     else hipLaunchKernelGGL((gemm256_kernel<EPI, F16, false>), grid, dim3(512), G2_LDS_ALL, st, g);
     SPT_LAUNCH_CHECK();
 }
 
+constexpr int kNtStages = 4;  // deepest LDS ring of the 128 x 128 kernel (4 x 32 KiB; default depth: nt_stages)
+// default 2 slots: at the Parakeet streaming shapes (M = 832) the 3- and 4-slot rings measured no
+// faster (r3 exp_r3e / exp_r3g: the k-step is not DMA-latency bound); SPT_GEMM_NT_STAGES = 3 / 4
+int nt_stages() {
+    static const int s = getenv("SPT_GEMM_NT_STAGES") ? atoi(getenv("SPT_GEMM_NT_STAGES")) : 2;
+    return s == 3 || s == 4 ? s : 2;
+}
+
+template <typename T, int EPI, int ST>
+void launch_t_st(const GemmArgs& g0, int batch, hipStream_t st) {
+    static const int nmajor = getenv("SPT_GEMM_NT_RASTER") ? atoi(getenv("SPT_GEMM_NT_RASTER")) : 0;
+    GemmArgs g = g0;
+    g.nmajor = nmajor;
+    constexpr int lds = ST * 2 * BM * SLAB;
+    if (lds > 64 * 1024) ensure_lds_attr((const void*)gemm_nt_kernel<T, EPI, ST>, lds);
+    dim3 grid(cdiv(g.M, BM) * (g.N / BN), g.ksplit, batch);
+    hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, ST>), grid, dim3(256), lds, st, g);
+}
+
 template <typename T, int EPI>
 void launch_t(const GemmArgs& g, int batch, hipStream_t st) {
-    dim3 grid(cdiv(g.M, BM) * (g.N / BN), g.ksplit, batch);
-    hipLaunchKernelGGL((gemm_nt_kernel<T, EPI>), grid, dim3(256), 0, st, g);
+    switch (nt_stages()) {
+        case 2: launch_t_st<T, EPI, 2>(g, batch, st); break;
+        case 3: launch_t_st<T, EPI, 3>(g, batch, st); break;
+        default: launch_t_st<T, EPI, kNtStages>(g, batch, st); break;
+    }
+}
+
+template <int EPI>
+void prepare_epi() {
+    ensure_lds_attr((const void*)gemm256_kernel<EPI, false, false>, G2_LDS_ALL);
+    ensure_lds_attr((const void*)gemm256_kernel<EPI, false, true>, G2_LDS_ALL);
+    ensure_lds_attr((const void*)gemm256_kernel<EPI, true, false>, G2_LDS_ALL);
+    ensure_lds_attr((const void*)gemm256_kernel<EPI, true, true>, G2_LDS_ALL);
+    ensure_lds_attr((const void*)gemm_nt_kernel<bf16, EPI, 3>, 3 * 2 * BM * SLAB);
+    ensure_lds_attr((const void*)gemm_nt_kernel<f16, EPI, 3>, 3 * 2 * BM * SLAB);
+    ensure_lds_attr((const void*)gemm_nt_kernel<float, EPI, 3>, 3 * 2 * BM * SLAB);
+    ensure_lds_attr((const void*)gemm_nt_kernel<bf16, EPI, kNtStages>, kNtStages * 2 * BM * SLAB);
+    ensure_lds_attr((const void*)gemm_nt_kernel<f16, EPI, kNtStages>, kNtStages * 2 * BM * SLAB);
+    ensure_lds_attr((const void*)gemm_nt_kernel<float, EPI, kNtStages>, kNtStages * 2 * BM * SLAB);
 }
 
 }  // namespace
+
+void ensure_lds_attr(const void* kernel, int bytes) {
+    static std::mutex mu;
+    static std::set<std::tuple<const void*, int, int>> done;
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(mu);
+    if (done.count({kernel, dev, bytes})) return;
+    HIP_CHECK(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+    done.insert({kernel, dev, bytes});
+}
+
+void gemm_prepare() {
+    prepare_epi<EPI_BIAS>();
+    prepare_epi<EPI_BIAS_GELU>();
+    prepare_epi<EPI_BIAS_GELU_POS>();
+    prepare_epi<EPI_BIAS_RESID>();
+    prepare_epi<EPI_KVSPLIT>();
+    prepare_epi<EPI_BIAS_SWISH>();
+    prepare_epi<EPI_BIAS_RELU>();
+    prepare_epi<EPI_BIAS_F32>();
+    prepare_epi<EPI_PARTIAL>();
+}
 
 void gemm_nt(int dtype, int epi, const GemmArgs& g, int batch, hipStream_t st) { gemm_nt_variant(dtype, epi, g, batch, 0, st); }
 

@@ -69,8 +69,11 @@ template <> __device__ __forceinline__ void store4<f16>(f16* p, float a, float b
     *(h4*)p = h4{(f16)a, (f16)b, (f16)c, (f16)d};
 }
 
-// LayerNorm with the pending split-K product of a residual GEMM folded in first
-template <typename T, int NV>
+// LayerNorm with the pending split-K product of a residual GEMM folded in first.  KS > 0: the
+// slab count as a template constant, so every slab, residual and bias load of a row is issued
+// before the first add (a runtime slab loop waited on each load in turn: r3 profile, 10.5 us per
+// launch at M = 832, 2 TB/s); KS = 0 keeps the runtime loop for other split counts.
+template <typename T, int NV, int KS>
 __global__ __launch_bounds__(256) void ln_pend_kernel(float* __restrict__ x, int M, int d, const float* __restrict__ slab,
                                                       int ks, int64_t sst, const float* __restrict__ pbias, float alpha,
                                                       const float* __restrict__ w, const float* __restrict__ bb,
@@ -82,22 +85,51 @@ __global__ __launch_bounds__(256) void ln_pend_kernel(float* __restrict__ x, int
     float4* xr = (float4*)(x + (size_t)row * d);
     float4 v[NV];
     float s = 0.f;
+    if constexpr (KS > 0) {
+        float4 u[NV][KS], x0[NV], pb[NV];
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-        const int idx = lane + 64 * i;
-        if (idx < n4) {
-            float4 p = *(const float4*)(slab + (size_t)row * d + 4 * idx);
-            for (int q = 1; q < ks; ++q) {
-                const float4 u = *(const float4*)(slab + q * sst + (size_t)row * d + 4 * idx);
-                p.x += u.x; p.y += u.y; p.z += u.z; p.w += u.w;
+        for (int i = 0; i < NV; ++i) {
+            const int idx = min(lane + 64 * i, n4 - 1);
+#pragma unroll
+            for (int q = 0; q < KS; ++q) u[i][q] = *(const float4*)(slab + q * sst + (size_t)row * d + 4 * idx);
+            x0[i] = xr[idx];
+            pb[i] = ((const float4*)pbias)[idx];
+        }
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            float4 p = u[i][0];
+#pragma unroll
+            for (int q = 1; q < KS; ++q) {
+                p.x += u[i][q].x; p.y += u[i][q].y; p.z += u[i][q].z; p.w += u[i][q].w;
             }
-            const float4 pb = ((const float4*)pbias)[idx], x0 = xr[idx];
-            v[i] = make_float4(x0.x + alpha * (p.x + pb.x), x0.y + alpha * (p.y + pb.y), x0.z + alpha * (p.z + pb.z),
-                               x0.w + alpha * (p.w + pb.w));
-            if (write_x) xr[idx] = v[i];
-            s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
-        } else {
-            v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            const int idx = lane + 64 * i;
+            if (idx < n4) {
+                v[i] = make_float4(x0[i].x + alpha * (p.x + pb[i].x), x0[i].y + alpha * (p.y + pb[i].y),
+                                   x0[i].z + alpha * (p.z + pb[i].z), x0[i].w + alpha * (p.w + pb[i].w));
+                if (write_x) xr[idx] = v[i];
+                s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+            } else {
+                v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            const int idx = lane + 64 * i;
+            if (idx < n4) {
+                float4 p = *(const float4*)(slab + (size_t)row * d + 4 * idx);
+                for (int q = 1; q < ks; ++q) {
+                    const float4 u = *(const float4*)(slab + q * sst + (size_t)row * d + 4 * idx);
+                    p.x += u.x; p.y += u.y; p.z += u.z; p.w += u.w;
+                }
+                const float4 pb = ((const float4*)pbias)[idx], x0 = xr[idx];
+                v[i] = make_float4(x0.x + alpha * (p.x + pb.x), x0.y + alpha * (p.y + pb.y), x0.z + alpha * (p.z + pb.z),
+                                   x0.w + alpha * (p.w + pb.w));
+                if (write_x) xr[idx] = v[i];
+                s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+            } else {
+                v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
         }
     }
     const float mean = wave_sum(s) / (float)d;
@@ -125,17 +157,29 @@ __global__ __launch_bounds__(256) void ln_pend_kernel(float* __restrict__ x, int
     }
 }
 
+template <typename T, int NV>
+void ln_pend_nv(dim3 grid, float* x, int M, int d, const float* slab, int ks, int64_t sst, const float* pb, float alpha,
+                const float* w, const float* b, T* y, int wx, hipStream_t st) {
+    switch (ks) {
+        case 1: hipLaunchKernelGGL((ln_pend_kernel<T, NV, 1>), grid, dim3(256), 0, st, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx); break;
+        case 2: hipLaunchKernelGGL((ln_pend_kernel<T, NV, 2>), grid, dim3(256), 0, st, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx); break;
+        case 4: hipLaunchKernelGGL((ln_pend_kernel<T, NV, 4>), grid, dim3(256), 0, st, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx); break;
+        case 8: hipLaunchKernelGGL((ln_pend_kernel<T, NV, 8>), grid, dim3(256), 0, st, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx); break;
+        default: hipLaunchKernelGGL((ln_pend_kernel<T, NV, 0>), grid, dim3(256), 0, st, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx); break;
+    }
+}
+
 template <typename T>
 void ln_pend_dispatch(float* x, int M, int d, const float* slab, int ks, int64_t sst, const float* pb, float alpha,
                       const float* w, const float* b, T* y, int wx, hipStream_t st) {
     dim3 grid(cdiv(M, 4));
     switch (cdiv(d, 256)) {
-        case 1: hipLaunchKernelGGL((ln_pend_kernel<T, 1>), grid, dim3(256), 0, st, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx); break;
-        case 2: hipLaunchKernelGGL((ln_pend_kernel<T, 2>), grid, dim3(256), 0, st, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx); break;
-        case 3: hipLaunchKernelGGL((ln_pend_kernel<T, 3>), grid, dim3(256), 0, st, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx); break;
-        case 4: hipLaunchKernelGGL((ln_pend_kernel<T, 4>), grid, dim3(256), 0, st, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx); break;
-        case 5: hipLaunchKernelGGL((ln_pend_kernel<T, 5>), grid, dim3(256), 0, st, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx); break;
-        case 6: hipLaunchKernelGGL((ln_pend_kernel<T, 6>), grid, dim3(256), 0, st, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx); break;
+        case 1: ln_pend_nv<T, 1>(grid, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx, st); break;
+        case 2: ln_pend_nv<T, 2>(grid, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx, st); break;
+        case 3: ln_pend_nv<T, 3>(grid, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx, st); break;
+        case 4: ln_pend_nv<T, 4>(grid, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx, st); break;
+        case 5: ln_pend_nv<T, 5>(grid, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx, st); break;
+        case 6: ln_pend_nv<T, 6>(grid, x, M, d, slab, ks, sst, pb, alpha, w, b, y, wx, st); break;
         default: throw std::runtime_error("layernorm_pend: d too large");
     }
 }

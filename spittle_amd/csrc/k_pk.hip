@@ -759,8 +759,8 @@ __global__ __launch_bounds__(256) void joint_fin_kernel(PkFinArgs a) {
     const int P = a.P;
     if (ns.upd)
         for (int k = tid; k < P; k += 256) a.xemb[(size_t)b * P + k] = a.emb[(size_t)ns.tok * P + k];
-    const int t = min(ns.t, a.T3p - 1);
-    for (int k = tid; k < P; k += 256) a.fecur[(size_t)b * P + k] = a.fe[((size_t)b * a.T3p + t) * P + k];
+    const int t = min(ns.t, ns.t3p - 1);
+    for (int k = tid; k < P; k += 256) a.fecur[(size_t)b * P + k] = a.fe[((size_t)b * ns.t3p + t) * P + k];
 }
 
 // rows start at t = 0 with the blank symbol pending: zero states, the blank's (zero) embedding,
@@ -768,7 +768,7 @@ __global__ __launch_bounds__(256) void joint_fin_kernel(PkFinArgs a) {
 __global__ void state_init_kernel(PkState* st, int B, int V, float* h, float* c, int n, float* xemb, float* fecur,
                                   const float* fe, int T3p, int P, const int* __restrict__ lens) {
     const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i < B) st[i] = PkState{0, 0, 0, lens[i * 4 + 3] <= 0 ? 1 : 0, 1, V};  // no frames: nothing to decode
+    if (i < B) st[i] = PkState{0, 0, 0, lens[i * 4 + 3] <= 0 ? 1 : 0, 1, V, T3p};  // no frames: nothing to decode
     if (i < n) { h[i] = 0.0f; c[i] = 0.0f; }
     if (i < B * P) {
         const int b = i / P, k = i % P;
@@ -918,13 +918,10 @@ constexpr int kLstmDO = 16, kPredDO = 16, kJointDO = 64;
 // register-held wave-loads per lane and staged float4 per thread, sized for P <= 640
 constexpr int kNWL = 10, kSEL = 5, kNWP = 5, kSEP = 3, kNWJ = 20, kSEJ = 3;
 
-void pk_prepare() {
-    static bool done = false;  // > 64 KiB dynamic LDS: once per process, before any stream capture
-    if (done) return;
-    HIP_CHECK(hipFuncSetAttribute((const void*)dec_kernel<PKD_LSTM, kLstmDO, kNWL, kSEL>, hipFuncAttributeMaxDynamicSharedMemorySize, kDecSmemMax));
-    HIP_CHECK(hipFuncSetAttribute((const void*)dec_kernel<PKD_PRED, kPredDO, kNWP, kSEP>, hipFuncAttributeMaxDynamicSharedMemorySize, kDecSmemMax));
-    HIP_CHECK(hipFuncSetAttribute((const void*)dec_kernel<PKD_JOINT, kJointDO, kNWJ, kSEJ>, hipFuncAttributeMaxDynamicSharedMemorySize, kDecSmemMax));
-    done = true;
+void pk_prepare() {  // > 64 KiB dynamic LDS: per kernel and device, before any stream capture
+    ensure_lds_attr((const void*)dec_kernel<PKD_LSTM, kLstmDO, kNWL, kSEL>, kDecSmemMax);
+    ensure_lds_attr((const void*)dec_kernel<PKD_PRED, kPredDO, kNWP, kSEP>, kDecSmemMax);
+    ensure_lds_attr((const void*)dec_kernel<PKD_JOINT, kJointDO, kNWJ, kSEJ>, kDecSmemMax);
 }
 
 int pk_joint_tile() { return kJointDO; }

@@ -34,10 +34,14 @@ struct GemmArgs {
     int kv_B, kv_T, kv_H;                 // EPI_KVSPLIT: dest = the cross K/V cache (kv_offset)
     float alpha = 1.0f;                   // EPI_BIAS_RESID / EPI_BIAS_F32 scale
     int ksplit = 1; int64_t c_split = 0;  // EPI_PARTIAL: K split over grid.y, slab stride (elements)
+    int nmajor = 0;                       // 128 x 128 tile: raster tiles N-major (set by the launcher)
 };
 void gemm_nt(int dtype, int epi, const GemmArgs& g, int batch, hipStream_t st);
 // variant 0: automatic (bf16 N % 256 == 0 -> 256 x 256 tile); 1: 128 x 128 tile; 2: prefer 256 x 256;
 // 3: skinny (M <= 64, 16-bit dtypes: 16 columns per workgroup, the weight stream spread over the grid)
+// sets the > 64 KiB dynamic-LDS attribute of every GEMM kernel on the current device (engine
+// constructors call it before any stream capture; launches check it too)
+void gemm_prepare();
 void gemm_nt_variant(int dtype, int epi, const GemmArgs& g, int batch, int variant, hipStream_t st);
 
 // ------------------------------------------------------------------ weights (k_init.hip)

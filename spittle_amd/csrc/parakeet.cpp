@@ -131,6 +131,7 @@ ParakeetEngine::ParakeetEngine(const PkDims& dm, int dtype, int device, int max_
         ev_.resize(6);
         for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
         pk_prepare();
+        gemm_prepare();
         alloc_weights();
         alloc_workspace();
         upload_tables();
@@ -543,7 +544,7 @@ void ParakeetEngine::encode(int B, int Tp, int T1p, int T2p, int T3p) {
     }
 }
 
-void ParakeetEngine::enqueue_step(int B, int T3p, int max_symbols, int cap, int parity) {
+void ParakeetEngine::enqueue_step(int B, int max_symbols, int cap, int parity) {
     const int P = dm_.pred;
     const size_t BP = (size_t)B * P;
     auto hbuf = [&](float* base, int layer, int par) { return base + ((size_t)layer * 2 + par) * BP; };
@@ -569,20 +570,20 @@ void ParakeetEngine::enqueue_step(int B, int T3p, int max_symbols, int cap, int 
     f.part = jpart_; f.n_tiles = joint_tiles_; f.dur = dur_;
     f.V = dm_.n_vocab; f.n_dur = dm_.n_dur; f.max_symbols = max_symbols; f.B = B; f.cap = cap; f.lens = lens_;
     f.st = state_; f.out_tok = out_tok_; f.out_frame = out_frame_; f.out_t1 = out_t1_; f.out_t2 = out_t2_;
-    f.P = P; f.T3p = T3p; f.emb = emb_; f.fe = fe_; f.xemb = xemb_; f.fecur = fecur_;
+    f.P = P; f.emb = emb_; f.fe = fe_; f.xemb = xemb_; f.fecur = fecur_;
     pk_joint_fin(f, st_);
 }
 
 void ParakeetEngine::run_decode(int B, int T3p, int max_symbols, std::vector<PkUtt>* out) {
     const int P = dm_.pred;
     pk_state_init(state_, B, dm_.n_vocab, h_, c_, 4 * B * P, xemb_, fecur_, fe_, lens_, T3p, P, st_);
-    const GraphKey key{B, T3p, max_symbols};
+    const GraphKey key{B, max_symbols};  // the frame stride lives in the state rows
     auto it = graphs_.find(key);
     static const bool no_graph = getenv("SPT_NO_GRAPH") != nullptr;
     if (it == graphs_.end() && !no_graph) {
         hipGraph_t graph;
         HIP_CHECK(hipStreamBeginCapture(st_, hipStreamCaptureModeThreadLocal));
-        for (int s = 0; s < kStepsPerGraph; ++s) enqueue_step(B, T3p, max_symbols, cap_, s & 1);
+        for (int s = 0; s < kStepsPerGraph; ++s) enqueue_step(B, max_symbols, cap_, s & 1);
         HIP_CHECK(hipStreamEndCapture(st_, &graph));
         hipGraphExec_t exec;
         HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
@@ -594,7 +595,7 @@ void ParakeetEngine::run_decode(int B, int T3p, int max_symbols, std::vector<PkU
     hstate_.resize(B);
     int steps = 0;
     while (true) {
-        if (no_graph) for (int s = 0; s < kStepsPerGraph; ++s) enqueue_step(B, T3p, max_symbols, cap_, s & 1);
+        if (no_graph) for (int s = 0; s < kStepsPerGraph; ++s) enqueue_step(B, max_symbols, cap_, s & 1);
         else HIP_CHECK(hipGraphLaunch(it->second, st_));
         steps += kStepsPerGraph;
         HIP_CHECK(hipMemcpyAsync(hstate_.data(), state_, B * sizeof(PkState), hipMemcpyDeviceToHost, st_));

@@ -90,11 +90,10 @@ private:
         float *ln2_w, *ln2_b; void *ff2_w1; float* ff2_b1; void* ff2_w2; float* ff2_b2;
         float *lno_w, *lno_b;
     };
-    struct GraphKey {
-        int B, T3p, max_symbols;
+    struct GraphKey {  // decode-step graphs: shape-free in the utterance length (PkState::t3p)
+        int B, max_symbols;
         bool operator<(const GraphKey& o) const {
             if (B != o.B) return B < o.B;
-            if (T3p != o.T3p) return T3p < o.T3p;
             return max_symbols < o.max_symbols;
         }
     };
@@ -112,7 +111,7 @@ private:
     int gemm(int dt, int epi, const void* A, int lda, const void* W, int ldw, int M, int N, int K, const float* bias,
              void* Cp, int ldc, float alpha = 1.0f);
     void run_decode(int B, int T3p, int max_symbols, std::vector<PkUtt>* out);
-    void enqueue_step(int B, int T3p, int max_symbols, int cap, int parity);
+    void enqueue_step(int B, int max_symbols, int cap, int parity);
 
     PkDims dm_;
     int dt_, dev_, max_batch_, max_samples_;

@@ -49,6 +49,7 @@ void pk_place(int mode, int dtype, const float* src, int N, int K, void* dst, in
 // ---- TDT greedy decoding (f32 prediction network + joint)
 struct PkState {         // per row, device
     int t, at_t, n_out, done, upd, tok;
+    int t3p;  // this call's frame stride of fe (set by pk_state_init, so a captured step is shape-free)
 };
 // One decode step = LSTM layer 0, LSTM layer 1, prediction projection, joint, fin.  The LSTM
 // states ping-pong between two buffers per layer (a stage's workgroups read every unit of the
@@ -78,7 +79,7 @@ struct PkFinArgs {
     int V, n_dur, max_symbols, B, cap;
     const int* lens;                      // T3 per row at lens[b * 4 + 3]
     PkState* st;
-    int P, T3p;
+    int P;
     const float* emb; const float* fe;    // embedding [V+1][P]; encoder projection [B*T3p][P]
     float* xemb; float* fecur;            // out: next step's LSTM-0 input / current-frame row [B][P]
     int* out_tok; int* out_frame; float* out_t1; float* out_t2;  // [B][cap]

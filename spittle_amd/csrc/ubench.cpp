@@ -327,15 +327,15 @@ int main(int argc, char** argv) {
         return 0;
     }
     if (what == "gemm") {  // 128 x 128 vs 256 x 256 tile: timing and bitwise agreement
-        const int M = ai(2, 12000), N = ai(3, 5120), K = ai(4, 1280), epi = ai(5, 0), dt = ai(6, DT_BF16);
+        const int M = ai(2, 12000), N = ai(3, 5120), K = ai(4, 1280), epi = ai(5, 0), dt = ai(6, DT_BF16), ks = ai(7, 1);
         void* A = drand((size_t)M * K, dt, 1, -2);
         void* W = drand((size_t)N * K, dt, 2, -5);
         float* bias = frand(N, 3, -5);
-        const size_t cbytes = (size_t)M * N * 4;
+        const size_t cbytes = (size_t)ks * M * N * 4;
         void* C = dalloc(cbytes);
         GemmArgs g{};
         g.A = A; g.lda = K; g.W = W; g.ldw = K; g.M = M; g.N = N; g.K = K; g.bias = bias; g.C = C; g.ldc = N;
-        g.kv_B = M / 1500; g.kv_T = 1500; g.kv_H = 20;
+        g.kv_B = M / 1500; g.kv_T = 1500; g.kv_H = 20; g.ksplit = ks; g.c_split = (int64_t)M * N;
         if (epi == EPI_BIAS_GELU_POS) g.pos = frand((size_t)M * N, 4, 0);
         HIP_CHECK(hipDeviceSynchronize());  // inputs are generated on the null stream
         std::vector<char> ref(cbytes), out(cbytes);
@@ -360,8 +360,8 @@ int main(int argc, char** argv) {
             }
         }
         const double fl = 2.0 * M * N * K;
-        printf("gemm M=%d N=%d K=%d epi=%d dt=%d : 128-tile %.2f us %.1f TF/s | 256-tile %.2f us %.1f TF/s | bytes differing %zu\n",
-               M, N, K, epi, dt, us[1], fl / us[1] / 1e6, us[2], fl / us[2] / 1e6, diff);
+        printf("gemm M=%d N=%d K=%d ks=%d epi=%d dt=%d : 128-tile %.2f us %.1f TF/s | 256-tile %.2f us %.1f TF/s | bytes differing %zu\n",
+               M, N, K, ks, epi, dt, us[1], fl / us[1] / 1e6, us[2], fl / us[2] / 1e6, diff);
         return 0;
     }
     if (what == "layer" || what == "layer2") {

@@ -372,6 +372,10 @@ def load_nemo(engine: ParakeetEngine, path: str, params: ParakeetModelParams,
     with tarfile.open(path, "r:*") as tf:
         members = {os.path.basename(m.name): m for m in tf.getmembers() if m.isfile()}
         cfg = yaml.safe_load(tf.extractfile(members["model_config.yaml"]).read())
+        durs = cfg.get("model_defaults", {}).get("tdt_durations", [0, 1, 2, 3, 4])
+        if list(durs) != list(range(len(durs))):
+            # the device decoder advances by the duration head's argmax index (k_pk.hip joint_fin)
+            raise TranscriptionError(L.SPT_ERR_LOAD, f"{path}: tdt_durations {list(durs)} are not 0..{len(durs) - 1}")
         sd = torch.load(io.BytesIO(tf.extractfile(members["model_weights.ckpt"]).read()), map_location="cpu",
                         weights_only=True)
         tok = next((members[k] for k in members if k.endswith("tokenizer.model")), None)

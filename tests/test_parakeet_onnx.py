@@ -91,3 +91,24 @@ def test_loader_full_shape_dims(tmp_path):
     for tid in (1, 11, 1002, 1017, 1023, 1000 + 64 * 23 + 35, 90001, 90006, 90013):
         assert np.array_equal(h.tensor(tid), exp[tid]), tid
     h.close()
+
+
+def test_nemo_rejects_durations_other_than_range(tmp_path):
+    """load_nemo refuses a TDT checkpoint whose duration table is not 0..n-1 before it touches a
+    device: the decoder advances by the duration head's argmax index (k_pk.hip joint_fin)."""
+    import io
+    import tarfile
+
+    import yaml
+    from spittle_amd import ParakeetEngine, ParakeetModelParams, TranscriptionError
+    from spittle_amd.parakeet import load_nemo
+    cfg = {"encoder": {"d_model": 64, "n_layers": 1, "n_heads": 2}, "decoder": {"prednet": {"pred_hidden": 32}},
+           "joint": {"num_classes": 30}, "model_defaults": {"tdt_durations": [0, 1, 2, 4, 8]}}
+    path = str(tmp_path / "m.nemo")
+    with tarfile.open(path, "w") as tf:
+        for name, data in (("model_config.yaml", yaml.safe_dump(cfg).encode()), ("model_weights.ckpt", b"")):
+            ti = tarfile.TarInfo("./" + name)
+            ti.size = len(data)
+            tf.addfile(ti, io.BytesIO(data))
+    with pytest.raises(TranscriptionError, match="tdt_durations"):
+        load_nemo(ParakeetEngine(), path, ParakeetModelParams())
