@@ -111,8 +111,25 @@ def host_cpu() -> dict:
         allowed = len(os.sched_getaffinity(0))
     except AttributeError:
         allowed = os.cpu_count()
+    quota = None  # cgroup v2 CPU quota (the job's share of a shared host), in whole CPUs
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
     return {"model": model, "physical_cores": len(phys) or None, "logical_cpus": os.cpu_count(),
-            "affinity_cpus": allowed}
+            "affinity_cpus": allowed, "cgroup_cpu_quota": quota}
+
+
+def cpu_threads(cpu: dict) -> int:
+    """Threads for a CPU-baseline leg: every physical core this process may use, i.e.
+    min(affinity CPUs, physical cores, cgroup CPU quota); an explicit
+    SPT_CPU_THREADS overrides it."""
+    if os.environ.get("SPT_CPU_THREADS"):
+        return int(os.environ["SPT_CPU_THREADS"])
+    n = [v for v in (cpu["affinity_cpus"], cpu["physical_cores"], cpu["cgroup_cpu_quota"]) if v]
+    return max(1, min(n)) if n else 1
 
 
 def cpu_baseline(model_spec: str, decode_steps: int) -> dict:
@@ -123,7 +140,7 @@ def cpu_baseline(model_spec: str, decode_steps: int) -> dict:
     from oracle import oracle as O
     name = model_spec.split(":")[1]
     cpu = host_cpu()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(cpu["affinity_cpus"] or 1, 16)
+    threads = cpu_threads(cpu)
     O.set_threads(threads)
     dims = O.dims_for(name)
     m = O.Model(dims, 1234, O.W_F32)
@@ -140,6 +157,7 @@ def cpu_baseline(model_spec: str, decode_steps: int) -> dict:
     total = t3 - t0
     return {"value": round(CHUNK_S / total, 4), "unit": "audio-sec/wall-sec", "cores": threads, "kind": "port",
             "cpu_model": cpu["model"], "host_physical_cores": cpu["physical_cores"],
+            "affinity_cpus": cpu["affinity_cpus"], "cgroup_cpu_quota": cpu["cgroup_cpu_quota"],
             "sample": f"1 x 30 s chunk, {name} dims fp32, {threads} OpenMP threads: mel {t1 - t0:.2f}s + encoder "
                       f"{t2 - t1:.2f}s + cross-KV + {PROMPT_LEN}-token prompt pass + {decode_steps - 1} decoder passes "
                       f"{t3 - t2:.2f}s = {total:.1f}s per chunk (timed whole, no extrapolation)"}
@@ -300,7 +318,7 @@ def parakeet_bench(device: int, steps: int, warmup: int, with_cpu: bool) -> dict
     if with_cpu:
         from oracle import parakeet as PO
         cpu = host_cpu()
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(cpu["affinity_cpus"] or 1, 16)
+        threads = cpu_threads(cpu)
         PO.set_threads(threads)
         m = PO.Model(PO.dims_for("parakeet-tdt-0.6b-v3"), 1234, PO.W_F32)
         x = synth_audio(3100)[:16000 * 5]
@@ -310,7 +328,7 @@ def parakeet_bench(device: int, steps: int, warmup: int, with_cpu: bool) -> dict
         dt = time.perf_counter() - t0
         m.close()
         out["cpu_baseline"] = {"value": round(5.0 / dt, 3), "unit": "audio-sec/wall-sec", "cores": threads,
-                               "kind": "port", "cpu_model": cpu["model"],
+                               "kind": "port", "cpu_model": cpu["model"], "affinity_cpus": cpu["affinity_cpus"],
                                "sample": f"1 x 5 s utterance, parakeet-tdt-0.6b-v3 dims fp32, {threads} OpenMP threads, "
                                          f"mel + encoder + TDT greedy {dt:.2f}s (timed whole)"}
     return out
@@ -354,12 +372,27 @@ def resampler_bench(device: int, with_cpu: bool) -> dict:
     return out
 
 
-def app_latency(eng, dur_s=(5, 10, 30)) -> dict:
+def _stats_fields(eng, ms: float) -> dict:
+    """The call's engine runs and decoder passes (spt_get_call_stats) beside its wall time."""
+    cs = eng.call_stats()
+    n = max(1, cs["decoder_passes"])
+    return {"ms": round(ms, 2), "engine_calls": cs["engine_calls"], "decoder_passes": cs["decoder_passes"],
+            "device_ms": round(cs["device_ms"], 2), "encoder_ms": round(cs["encoder_ms"], 2),
+            "decode_ms": round(cs["decode_ms"], 2), "decode_ms_per_pass": round(cs["decode_ms"] / n, 4),
+            "host_ms": round(ms - cs["device_ms"], 2)}
+
+
+def app_latency(eng, info: dict, dtype: str, dur_s=(5, 10, 30)) -> dict:
     """The app's real call (transcription.rs:494-503): one utterance (B = 1), whisper_full with
     its default parameters (timestamps on, temperature fallback 0.2 / best_of 5), language
     "en", through spt_transcribe.  Random-init weights never emit EOT or confident tokens, so
     every window decodes to its token limit and falls back through every temperature: an
-    upper bound of the app's latency; the passes it took are reported with it."""
+    upper bound of the app's latency.  Each case reports its engine calls (one per window and
+    temperature), decoder passes and the device time behind them (spt_get_call_stats);
+    decode_ms_per_pass mixes 1-row greedy passes and 5-row (best_of) sampled passes.
+    `b1_greedy_pass` isolates the B = 1 pass: one 30 s window on the greedy fast path, its mean
+    decoder pass against the bytes that pass streams (every layer weight, the logits matrix, one
+    utterance's cross K/V and its self K/V at the mean position)."""
     from spittle_amd import WhisperInferenceParams
     from spittle_amd.synth import synth_audio
     out = {}
@@ -370,8 +403,8 @@ def app_latency(eng, dur_s=(5, 10, 30)) -> dict:
         t0 = time.perf_counter()
         r = eng.transcribe_samples(x, p)
         ms = (time.perf_counter() - t0) * 1e3
-        out[f"{s}s"] = {"ms": round(ms, 2), "windows": r.n_windows, "fallbacks": r.n_fallbacks,
-                        "tokens": len(r.tokens), "segments": len(r.segments)}
+        out[f"{s}s"] = dict(_stats_fields(eng, ms), windows=r.n_windows, fallbacks=r.n_fallbacks,
+                            tokens=len(r.tokens), segments=len(r.segments))
     # beam search (whisper.cpp's WHISPER_SAMPLING_BEAM_SEARCH, beam_size 5; one captured graph per
     # step, the candidate bookkeeping on the host), 10 s, no fallback
     pb = WhisperInferenceParams(language="en", beam_size=5, temperature_inc=0.0)
@@ -380,8 +413,22 @@ def app_latency(eng, dur_s=(5, 10, 30)) -> dict:
     t0 = time.perf_counter()
     r = eng.transcribe_samples(x, pb)
     ms = (time.perf_counter() - t0) * 1e3
-    out["10s_beam5"] = {"ms": round(ms, 2), "windows": r.n_windows, "tokens": len(r.tokens),
-                        "ms_per_token": round(ms / max(1, len(r.tokens)), 3)}
+    st = _stats_fields(eng, ms)
+    cs = eng.call_stats()
+    out["10s_beam5"] = dict(st, windows=r.n_windows, tokens=len(r.tokens), beam_steps=cs["beam_steps"],
+                            ms_per_decoder_step=round(ms / max(1, cs["decoder_passes"]), 3))
+    # the B = 1 decoder pass alone (fast path, 30 s, 128 steps)
+    pg = WhisperInferenceParams(language="en", no_timestamps=True, temperature_inc=0.0, ignore_eot=True,
+                                max_new_tokens=N_STEPS)
+    x = synth_audio(2030)
+    eng.transcribe_samples(x, pg)
+    t0 = time.perf_counter()
+    eng.transcribe_samples(x, pg)
+    ms = (time.perf_counter() - t0) * 1e3
+    roof = phase_rooflines(info, eng.timings(), 1, N_STEPS, dtype).get("decode_pass", {})
+    out["b1_greedy_pass"] = dict(_stats_fields(eng, ms), bytes_per_pass=roof.get("bytes_per_pass"),
+                                 ms_per_pass=roof.get("ms_per_pass"), achieved_GBs=roof.get("achieved"),
+                                 frac_of_hbm_peak=roof.get("frac"))
     return out
 
 
@@ -477,11 +524,16 @@ def main():
     dt_dev, med_dev, phases_dev = timed(step_dev)
     rank_ms = [None] * world
     if world > 1:
-        dist.all_gather_object(rank_ms, round(dt * 1e3 / args.steps, 3))
+        dist.all_gather_object(rank_ms, round(med * 1e3, 3))
+    # the median step; the slowest rank's median (weak scaling: every rank's
+    # step must finish), next to the mean over the barrier-bracketed region
+    med_max = max_over_ranks(med, device=dev)
+    med_dev_max = max_over_ranks(med_dev, device=dev)
 
-    audio_s = world * B * CHUNK_S * args.steps
-    value = audio_s / dt
-    ms_per_step = dt * 1000.0 / args.steps
+    audio_step = world * B * CHUNK_S
+    value = audio_step / med_max
+    value_mean = audio_step * args.steps / dt
+    ms_per_step = med_max * 1000.0
 
     roof = kernels = None
     cpu = app = None
@@ -489,7 +541,7 @@ def main():
         if not args.no_probe:
             roof, kernels = roofline(eng)
         if world == 1 and not args.no_app_latency:
-            app = app_latency(eng)
+            app = app_latency(eng, info, args.dtype)
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.model, args.decode_steps)
     rs = None
@@ -503,15 +555,16 @@ def main():
         out = {
             "metric": metric_for(args.model), "value": round(value, 3), "unit": "audio-sec/wall-sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-            "ms_per_step_median_rank0": round(med * 1e3, 3),
+            "value_stat": "median step (max over ranks)", "value_mean": round(value_mean, 3),
+            "ms_per_step_mean": round(dt * 1000.0 / args.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": f"synthetic (BASELINE.md §3 seeded 16 kHz signal; random-init {args.model.split(':', 1)[-1]} weights)",
             "config": {"workload": f"whisper-{args.model.split(':')[-1]} 30s chunks, batch {B}/GPU, greedy en, "
                                    f"{PROMPT_LEN}-token prompt + {args.decode_steps} decode steps, host PCM in, text out",
                        "model": args.model, "global_batch": world * B, "seq_len": 1500,
                        "decode_steps": args.decode_steps, "parallelism": f"replicas x{world} (utterance shards)"},
-            "value_device_resident": round(audio_s / dt_dev, 3),
-            "ms_per_step_device_resident": round(dt_dev * 1000.0 / args.steps, 3),
+            "value_device_resident": round(audio_step / med_dev_max, 3),
+            "ms_per_step_device_resident": round(med_dev_max * 1000.0, 3),
             "phases_ms": {k: round(v, 3) for k, v in phases.items() if k.endswith("_ms")},
             "phases_ms_device_resident": {k: round(v, 3) for k, v in phases_dev.items() if k.endswith("_ms")},
             "roofline": roof, "rooflines": phase_rooflines(info, phases, B, args.decode_steps, args.dtype),

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 8
+#define SPT_ABI_VERSION 9
 
 typedef enum {
     SPT_OK = 0,
@@ -173,6 +173,22 @@ const char* spt_token_to_str(const spt_ctx* ctx, int32_t id);
 
 spt_status spt_get_timings(const spt_ctx* ctx, spt_timings* t);
 
+/* ABI 9: everything the last spt_transcribe* call ran, summed.  spt_timings holds the last engine
+ * run only; a whisper_full call (the app's default parameters) runs one engine call per window
+ * batch and temperature, and beam search one decoder pass per step, so its latency reads per
+ * decoder pass from here: device_ms / decoder_passes bounds the pass time from above. */
+typedef struct {
+    int32_t engine_calls;     /* mel + encoder + cross K/V + decode runs */
+    int32_t decoder_passes;   /* every decoder pass: prompt passes, decode steps, beam steps */
+    int32_t beam_steps;       /* host-driven beam steps among them */
+    int32_t reserved0;
+    double device_ms;         /* device time of those runs and steps (HIP events) */
+    double encoder_ms;
+    double decode_ms;         /* decoder passes incl. prompt prefill and sampling */
+} spt_call_stats;
+
+spt_status spt_get_call_stats(const spt_ctx* ctx, spt_call_stats* s);
+
 /* Multi-GPU load: the weight arena is one device allocation whose layout is a
  * pure function of (model, dtype), spt_model_info.weight_bytes long.  Rank 0 loads the model
  * (file parse + device dequantisation) and exports the arena into a device buffer; the buffer
@@ -261,8 +277,10 @@ typedef struct {
     int32_t dtype;        /* SPT_DTYPE_F16 (default) or SPT_DTYPE_F32 (bf16 also accepted) */
     int32_t device;
     int32_t max_batch;    /* utterances (chunks) per device pass, <= 64 */
-    float max_seconds;    /* longest chunk one pass takes; longer utterances are cut into chunks of
-                             this length (a multiple of 80 ms) and their results concatenated */
+    float max_seconds;    /* workspace size: the longest utterance one pass takes before it grows.
+                             A longer recording grows the workspace to its length and is decoded
+                             whole (up to 20 min / 96 GiB of workspace); only past that is it cut
+                             into chunks (multiples of 80 ms) whose results are concatenated */
     uint64_t seed;        /* synthetic weights */
     uint32_t flags;       /* SPT_PK_WEIGHTS_EMPTY: zero weights, to be filled by set_tensor */
     int32_t reserved0;
@@ -354,7 +372,8 @@ spt_status spt_parakeet_get_timings(const spt_pk_ctx* ctx, spt_pk_timings* t);
 spt_status spt_parakeet_debug_mel(spt_pk_ctx* ctx, const float* pcm16k, size_t n_samples, float* out);
 spt_status spt_parakeet_debug_encode(spt_pk_ctx* ctx, const float* mel, int32_t T, float* out);
 /* the encoder output [T3][d] (f32) of batch row b of the last transcribe call (the production
- * path: graph-replayed or eager); out holds max_seconds' T3 rows; *T3 receives the row's count */
+ * path: graph-replayed or eager); out holds the T3 rows of spt_pk_model_info.max_samples (which grows
+ * with the longest recording decoded); *T3 receives the row's count */
 spt_status spt_parakeet_debug_last_encoder(spt_pk_ctx* ctx, int32_t b, float* out, int32_t* T3);
 /* TDT greedy decoding of a given encoder output [T3][d] (f32): the decoder alone */
 spt_status spt_parakeet_debug_decode(spt_pk_ctx* ctx, const float* enc, int32_t T3, int32_t max_symbols,

@@ -1,4 +1,4 @@
-//! Raw bindings to `include/spittle_hip.h` (ABI 8), the C boundary of the MI355X-native Whisper
+//! Raw bindings to `include/spittle_hip.h` (ABI 9), the C boundary of the MI355X-native Whisper
 //! and Parakeet-V3 backend.  One item per declaration of the header, same names, same layouts (x86-64 SysV; the
 //! layouts are checked field by field against gcc by tests/test_capi.py).  Safe wrappers live in
 //! the `spittle-hip` crate.
@@ -6,7 +6,7 @@
 
 use std::os::raw::{c_char, c_int, c_void};
 
-pub const SPT_ABI_VERSION: c_int = 7;
+pub const SPT_ABI_VERSION: c_int = 9;
 
 pub type spt_status = c_int;
 pub const SPT_OK: spt_status = 0;
@@ -107,6 +107,18 @@ pub struct spt_model_info {
 
 #[repr(C)]
 #[derive(Clone, Copy, Debug, Default)]
+pub struct spt_call_stats {
+    pub engine_calls: i32,
+    pub decoder_passes: i32,
+    pub beam_steps: i32,
+    pub reserved0: i32,
+    pub device_ms: f64,
+    pub encoder_ms: f64,
+    pub decode_ms: f64,
+}
+
+#[repr(C)]
+#[derive(Clone, Copy, Debug, Default)]
 pub struct spt_timings {
     pub mel_ms: f64,
     pub encoder_ms: f64,
@@ -185,6 +197,8 @@ extern "C" {
     pub fn spt_token_to_str(ctx: *const spt_ctx, id: i32) -> *const c_char;
 
     pub fn spt_get_timings(ctx: *const spt_ctx, t: *mut spt_timings) -> spt_status;
+    // ---- ABI 9: the whole last call (every window, fallback and beam step)
+    pub fn spt_get_call_stats(ctx: *const spt_ctx, s: *mut spt_call_stats) -> spt_status;
 
     pub fn spt_weights_export(ctx: *mut spt_ctx, dev_dst: *mut c_void, bytes: usize) -> spt_status;
     pub fn spt_weights_import(ctx: *mut spt_ctx, dev_src: *const c_void, bytes: usize) -> spt_status;

@@ -335,7 +335,7 @@ spt_status run_windows(spt_ctx* c, std::vector<Window>& win, size_t n_utt, const
 
 extern "C" {
 
-const char* spt_version(void) { return "spittle_amd 0.9.0 (gfx950, ABI 8)"; }
+const char* spt_version(void) { return "spittle_amd 0.9.0 (gfx950, ABI 9)"; }
 
 const char* spt_language_code(int32_t lang_id) { return spt::lang_code(lang_id); }
 
@@ -452,6 +452,7 @@ spt_status spt_transcribe_batch(spt_ctx* ctx, const float* const* pcm, const siz
     spt_infer_params dflt;
     spt_default_infer_params(&dflt);
     if (!params) params = &dflt;
+    ctx->eng->reset_call_stats();
     if (full_mode(params)) {
         for (size_t u = 0; u < batch; ++u) {
             out[u] = nullptr;
@@ -508,6 +509,7 @@ spt_status spt_transcribe_batch_device(spt_ctx* ctx, const float* pcm_dev, size_
     spt_infer_params dflt;
     spt_default_infer_params(&dflt);
     if (!params) params = &dflt;  // the defaults are whisper_full's (timestamps on): unsupported here
+    ctx->eng->reset_call_stats();
     if (full_mode(params))
         return fail(ctx, SPT_ERR_UNSUPPORTED,
                     "device windows take the no-timestamp greedy protocol (SPT_NO_TIMESTAMPS, temperature_inc 0)");
@@ -586,6 +588,15 @@ spt_status spt_get_timings(const spt_ctx* ctx, spt_timings* t) {
     const spt::Timings& m = ctx->eng->timings();
     t->mel_ms = m.mel_ms; t->encoder_ms = m.encoder_ms; t->cross_kv_ms = m.cross_kv_ms; t->decode_ms = m.decode_ms;
     t->total_ms = m.total_ms; t->h2d_ms = m.h2d_ms; t->n_decode_passes = m.n_decode_passes; t->batch = m.batch;
+    return SPT_OK;
+}
+
+spt_status spt_get_call_stats(const spt_ctx* ctx, spt_call_stats* s) {
+    if (!ctx || !s) return SPT_ERR_INVALID_ARG;
+    const spt::CallStats& c = ctx->eng->call_stats();
+    s->engine_calls = c.engine_calls; s->decoder_passes = c.decoder_passes; s->beam_steps = c.beam_steps;
+    s->reserved0 = 0;
+    s->device_ms = c.device_ms; s->encoder_ms = c.encoder_ms; s->decode_ms = c.decode_ms;
     return SPT_OK;
 }
 

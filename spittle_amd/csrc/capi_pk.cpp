@@ -3,8 +3,10 @@
 // Mirrors transcribe-rs' ParakeetEngine as Spittle drives it (/root/reference/src-tauri/src/
 // managers/transcription.rs: load_model_with_params 278-297, transcribe_samples with
 // TimestampGranularity::Segment 505-513, unload 175-208): status codes + message, borrowed PCM,
-// library-owned results.  Utterances longer than the context's max_seconds are cut into chunks
-// on 80 ms (encoder frame) boundaries, batched through the device together and concatenated.
+// library-owned results.  Like the reference engine, a recording is decoded whole in one pass:
+// an utterance longer than the context's max_seconds grows the workspace to its length (up to 20
+// minutes and kMaxGrowBytes of workspace); only past that limit, or when the device has no room,
+// is it cut into chunks on 80 ms (encoder frame) boundaries, batched and concatenated.
 #include <hip/hip_runtime.h>
 #include <string.h>
 
@@ -19,6 +21,10 @@
 #include "kernels.h"
 #include "parakeet.h"
 #include "pk_onnx.h"
+
+namespace {
+constexpr int64_t kMaxGrowBytes = 96ll << 30;  // workspace a long recording may grow to (of 288 GB HBM)
+}
 
 struct spt_pk_ctx {
     std::unique_ptr<spt::ParakeetEngine> eng;
@@ -391,6 +397,14 @@ spt_status spt_parakeet_transcribe_batch(spt_pk_ctx* ctx, const float* const* pc
         if (n_samples[u] > (size_t)INT32_MAX / 2) return fail(ctx, SPT_ERR_INVALID_ARG, "utterance too long");
     }
     spt::ParakeetEngine& e = *ctx->eng;
+    size_t longest = 0;
+    for (size_t u = 0; u < batch; ++u) longest = std::max(longest, n_samples[u]);
+    try {
+        if (longest > (size_t)e.max_samples() && longest <= 16000u * 1200u)
+            e.reserve_samples((int)longest, kMaxGrowBytes);  // false: the chunked fallback below
+    } catch (const std::exception& ex) {
+        return fail(ctx, classify(ex), ex.what());
+    }
     const int cs = e.max_samples();
     struct Chunk { size_t utt; int idx; const float* p; int n; };
     std::vector<Chunk> ch;
@@ -447,19 +461,23 @@ spt_status spt_parakeet_transcribe_batch_device(spt_pk_ctx* ctx, const float* pc
     if (!ctx || !out || !pcm_dev || !n_samples || batch == 0) return fail(ctx, SPT_ERR_INVALID_ARG, "null argument");
     spt::ParakeetEngine& e = *ctx->eng;
     if (batch > (size_t)e.max_batch()) return fail(ctx, SPT_ERR_INVALID_ARG, "batch exceeds max_batch");
-    if (stride < (size_t)e.max_samples()) return fail(ctx, SPT_ERR_INVALID_ARG, "device stride shorter than the chunk length");
     spt_pk_infer_params dp;
     spt_parakeet_default_infer_params(&dp);
     if (!params) params = &dp;
     spt_status s = check_params(ctx, params);
     if (s != SPT_OK) return s;
     std::vector<int> ns(batch);
+    size_t longest = 0;
     for (size_t b = 0; b < batch; ++b) {
         out[b] = nullptr;
-        if (n_samples[b] > (size_t)e.max_samples()) return fail(ctx, SPT_ERR_INVALID_ARG, "device chunk longer than max_seconds");
+        if (n_samples[b] > 16000u * 1200u) return fail(ctx, SPT_ERR_INVALID_ARG, "utterance longer than 20 minutes");
+        if (batch > 1 && n_samples[b] > stride) return fail(ctx, SPT_ERR_INVALID_ARG, "utterance longer than the device stride");
         ns[b] = (int)n_samples[b];
+        longest = std::max(longest, n_samples[b]);
     }
     try {
+        if (longest > (size_t)e.max_samples() && !e.reserve_samples((int)longest, kMaxGrowBytes))
+            return fail(ctx, SPT_ERR_OOM, "no device room to decode an utterance this long in one pass");
         std::vector<spt::PkUtt> res;
         e.transcribe_device(pcm_dev, (int64_t)stride, ns.data(), (int)batch, params->max_symbols, &res);
         for (size_t b = 0; b < batch; ++b) {

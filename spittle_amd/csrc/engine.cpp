@@ -105,7 +105,7 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     // a kernel template constant.
     select();
     HIP_CHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
-    ev_.resize(8);
+    ev_.resize(10);  // 0-5 phases, 6-7 PCM staging, 8-9 a beam step
     for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
     // a decoder pass stages at most max_rows_ rows in its LayerNorm GEMVs' LDS images; a batch
     // above that is decoded as several groups (each sized for the whole batch, re-sliced per call)
@@ -1105,6 +1105,11 @@ void Engine::transcribe_device(const float* pcm_dev, int64_t stride, const int* 
     HIP_CHECK(hipEventElapsedTime(&ms, ev_[0], ev_[5])); tm_.total_ms = ms;
     tm_.h2d_ms = h2d;
     tm_.batch = B;
+    cs_.engine_calls++;
+    cs_.decoder_passes += tm_.n_decode_passes;
+    cs_.device_ms += tm_.total_ms;
+    cs_.encoder_ms += tm_.encoder_ms;
+    cs_.decode_ms += tm_.decode_ms;
 }
 
 void Engine::stage_pcm(const float* const* pcm, const int* n, int B) {
@@ -1197,6 +1202,7 @@ void Engine::beam_next(const int* src, const int* tokens, const int* rowstate, i
         enqueue_head(g, 1, beam_rq_, beam_rq_.n_steps, x, suppress_, (beam_rq_.flags & 1u) != 0);
     };
     static const bool no_graph = getenv("SPT_NO_GRAPH") != nullptr;
+    HIP_CHECK(hipEventRecord(ev_[8], g.st));
     if (no_graph) {
         beam_pass();
     } else {
@@ -1215,7 +1221,14 @@ void Engine::beam_next(const int* src, const int* tokens, const int* rowstate, i
         }
         HIP_CHECK(hipGraphLaunch(it->second, g.st));
     }
-    read_cands(B, out);
+    HIP_CHECK(hipEventRecord(ev_[9], g.st));
+    read_cands(B, out);  // synchronises g.st
+    float ms = 0.0f;
+    HIP_CHECK(hipEventElapsedTime(&ms, ev_[8], ev_[9]));
+    cs_.beam_steps++;
+    cs_.decoder_passes++;
+    cs_.device_ms += ms;
+    cs_.decode_ms += ms;
 }
 
 // ----------------------------------------------------------------------------- debug hooks

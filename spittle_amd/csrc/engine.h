@@ -56,6 +56,13 @@ struct Timings {
     int n_decode_passes = 0, batch = 0;
 };
 
+// everything one C-ABI call ran (a whisper_full call: every window batch, temperature fallback
+// and beam step), summed; reset by the C ABI at the start of each spt_transcribe* call
+struct CallStats {
+    int engine_calls = 0, decoder_passes = 0, beam_steps = 0;
+    double device_ms = 0, encoder_ms = 0, decode_ms = 0;
+};
+
 class Engine {
 public:
     // src == nullptr: synthetic weights from `seed`; else the weights, mel filters of a ggml file
@@ -86,6 +93,8 @@ public:
     void commit_weights();
     int64_t workspace_bytes() const { return abytes_; }
     const Timings& timings() const { return tm_; }
+    const CallStats& call_stats() const { return cs_; }
+    void reset_call_stats() { cs_ = CallStats(); }
 
     // pcm_dev: B windows of <= 480000 samples at pcm_dev + b * stride (device memory)
     // tokens/top1/top2: host [B][n_steps]
@@ -240,6 +249,7 @@ private:
     void read_cands(int B, BeamCands* out);
 
     Timings tm_;
+    CallStats cs_;
 };
 
 // model dimensions of a ggml file's hparams; false + *err if the engine cannot run it

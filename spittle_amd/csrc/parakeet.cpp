@@ -116,15 +116,11 @@ ParakeetEngine::ParakeetEngine(const PkDims& dm, int dtype, int device, int max_
     F1_ = halve(dm_.n_mels);
     F2_ = halve(F1_);
     F3_ = halve(F2_);
-    Tmax_ = max_samples / PK_HOP;
-    T1max_ = halve(Tmax_);
-    T2max_ = halve(T1max_);
-    T3max_ = halve(T2max_);
+    set_frame_limits();
     const int P = dm_.pred;
     P_pad_ = round_up(P, 64);
     joint_pad_ = round_up(dm_.n_vocab + 1 + dm_.n_dur, 64);
     joint_tiles_ = joint_pad_ / pk_joint_tile();
-    cap_ = T3max_ * kMaxSymbols + 1;
     select();
     try {
         HIP_CHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
@@ -323,6 +319,48 @@ void ParakeetEngine::set_tensor(int tid, const float* host, int64_t n) {
     HIP_CHECK(hipMemcpyAsync(scratch_, host, (size_t)n * 4, hipMemcpyHostToDevice, st_));
     place(t, scratch_);
     HIP_CHECK(hipStreamSynchronize(st_));
+}
+
+void ParakeetEngine::set_frame_limits() {
+    Tmax_ = max_samples_ / PK_HOP;
+    T1max_ = halve(Tmax_);
+    T2max_ = halve(T1max_);
+    T3max_ = halve(T2max_);
+    cap_ = T3max_ * kMaxSymbols + 1;
+}
+
+bool ParakeetEngine::reserve_samples(int n, int64_t max_bytes) {
+    if (n <= max_samples_) return true;
+    if (n > 16000 * 1200) return false;
+    // grow by at least a quarter (a dictation session's recordings lengthen a little at a time),
+    // in whole 80 ms encoder frames
+    int64_t want = std::max<int64_t>(n, (int64_t)max_samples_ + max_samples_ / 4);
+    want = std::min<int64_t>(round_up((int)std::min<int64_t>(want, 16000 * 1200), 1280), 16000 * 1200);
+    // the workspace is linear in max_samples up to a few fixed-size buffers: project its size
+    const double per = (double)abytes_ / max_samples_;
+    if (per * want > (double)max_bytes) return false;
+    select();
+    HIP_CHECK(hipStreamSynchronize(st_));
+    for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
+    graphs_.clear();
+    for (auto& kv : enc_graphs_) (void)hipGraphExecDestroy(kv.second);
+    enc_graphs_.clear();
+    enc_seen_.clear();
+    const int old = max_samples_;
+    HIP_CHECK(hipFree(aarena_));
+    aarena_ = nullptr;
+    max_samples_ = (int)want;
+    set_frame_limits();
+    try {
+        alloc_workspace();
+    } catch (const std::exception&) {  // no room: back to the old size (just freed, so it fits)
+        max_samples_ = old;
+        set_frame_limits();
+        alloc_workspace();
+        return false;
+    }
+    HIP_CHECK(hipStreamSynchronize(st_));
+    return true;
 }
 
 void ParakeetEngine::alloc_workspace() {
@@ -630,7 +668,9 @@ void ParakeetEngine::transcribe_device(const float* pcm_dev, int64_t stride, con
                                        std::vector<PkUtt>* out) {
     if (B < 1 || B > max_batch_) throw std::runtime_error("batch must be in [1, max_batch]");
     if (max_symbols < 1 || max_symbols > kMaxSymbols) throw std::runtime_error("max_symbols must be in [1, 16]");
-    if (stride < max_samples_ && B > 1) throw std::runtime_error("device stride shorter than max_samples");
+    if (B > 1)
+        for (int b = 0; b < B; ++b)
+            if (stride < n[b]) throw std::runtime_error("device stride shorter than an utterance");
     select();
     std::vector<int> lens;
     int Tp, T1p, T2p, T3p;

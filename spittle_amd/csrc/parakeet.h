@@ -48,6 +48,11 @@ public:
     int dtype() const { return dt_; }
     int max_batch() const { return max_batch_; }
     int max_samples() const { return max_samples_; }
+    // grow the workspace so one pass takes utterances of n samples (the app decodes a whole
+    // recording in one pass: transcription.rs:505-513); graphs captured on the old workspace are
+    // dropped.  Returns false, with the old workspace kept, if the larger one does not fit in
+    // max_bytes (or in device memory).
+    bool reserve_samples(int n, int64_t max_bytes);
     int64_t weight_bytes() const { return wbytes_; }
     int64_t workspace_bytes() const { return abytes_; }
     const PkTimings& timings() const { return tm_; }
@@ -102,6 +107,7 @@ private:
     void release();
     void alloc_weights();
     void alloc_workspace();
+    void set_frame_limits();  // Tmax_ .. T3max_, cap_ from max_samples_
     void upload_tables();
     void place(const TSpec& t, const float* src_dev);
     void frame_counts(const int* n, int B, std::vector<int>* lens, int* Tp, int* T1p, int* T2p, int* T3p) const;

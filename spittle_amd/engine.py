@@ -258,6 +258,13 @@ class WhisperEngine:
         self._check(self._lib.spt_get_timings(self._ctx, C.byref(t)))
         return {k: getattr(t, k) for k, _ in t._fields_}
 
+    def call_stats(self) -> dict:
+        """What the last transcribe* call ran in total (engine calls, decoder passes, device ms)."""
+        self._need()
+        t = L.CallStats()
+        self._check(self._lib.spt_get_call_stats(self._ctx, C.byref(t)))
+        return {k: getattr(t, k) for k, _ in t._fields_ if k != "reserved0"}
+
     def debug_mel(self, samples) -> np.ndarray:
         self._need()
         x = np.ascontiguousarray(np.asarray(samples, np.float32).reshape(-1))

@@ -134,19 +134,25 @@ def test_fp16_batch_is_bitwise_invariant(small16):
         assert list(rs.tokens) == list(rbi.tokens) and np.array_equal(rs.top1, rbi.top1)
 
 
-def test_long_utterance_is_chunked():
+def test_long_utterance_is_decoded_whole():
+    """A recording longer than the context's max_seconds is decoded in one pass (the reference's
+    ParakeetEngine::transcribe_samples takes the whole buffer): the workspace grows to its length,
+    and the result equals the oracle run on the whole recording, not on chunks of it."""
     e = _engine("synthetic:parakeet-test-small", "f32", max_seconds=2.0, max_batch=2)
     om = P.Model(P.dims_for("test-small"), seed=SEED)
     pcm = synth_audio(9, 16000 * 5 + 500)
+    short = synth_audio(10, 16000 * 1)
+    r0 = e.transcribe_samples(short, _tok_params())  # graphs and buffers of the small workspace
     r = e.transcribe_samples(pcm, _tok_params())
-    assert r.n_chunks == 3
-    toks, frames = [], []
-    for c in range(3):
-        chunk = pcm[c * 32000:(c + 1) * 32000]
-        t, f, _, _ = om.decode(om.encode(P.mel(chunk)))
-        toks += list(t)
-        frames += [x + c * 25 for x in f]  # 2 s = 25 encoder frames of 80 ms
-    assert list(r.tokens) == toks and list(r.frames) == frames
+    assert r.n_chunks == 1
+    assert e.info()["max_samples"] >= pcm.size
+    t, f, _, _ = om.decode(om.encode(P.mel(pcm)))
+    assert list(r.tokens) == list(t) and list(r.frames) == list(f)
+    # after growing: the short utterance again, and both together in one batch
+    r1 = e.transcribe_samples(short, _tok_params())
+    assert list(r1.tokens) == list(r0.tokens) and list(r1.frames) == list(r0.frames)
+    rb = e.transcribe_batch([short, pcm], _tok_params())
+    assert list(rb[0].tokens) == list(r0.tokens) and list(rb[1].tokens) == list(r.tokens)
     e.unload_model()
 
 
