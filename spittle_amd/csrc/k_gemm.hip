@@ -439,6 +439,24 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     for (int j = 0; j < 4; ++j) bv[j] = g.bias ? g.bias[n0 + wc * 64 + 16 * j + fr] : 0.0f;
 #pragma unroll
     for (int pass = 0; pass < 128 / PR; ++pass) {
+        const int ch = lane % CPR, rsub = lane / CPR;
+        // the residual / positional operand of the f32 epilogues, loaded for the whole pass before
+        // the LDS staging and any store.  Read inside the store loop, each load waited behind the
+        // previous iteration's store to a possibly aliasing address: one dependent round trip per
+        // row group (r3 ubench: the residual epilogue cost 16 us per 256 x 256 tile)
+        constexpr bool YIN = EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU_POS;
+        float4 ypre[YIN ? PR / RPI : 1];
+        if constexpr (YIN) {
+#pragma unroll
+            for (int it = 0; it < PR / RPI; ++it) {
+                const int row = min(m0 + wr * 128 + pass * PR + it * RPI + rsub, g.M - 1);
+                const int col = n0 + wc * 64 + ch * (16 / ESZ);
+                if constexpr (EPI == EPI_BIAS_RESID)
+                    ypre[it] = *(const float4*)((const float*)g.C + (size_t)bz * g.sC + (size_t)row * g.ldc + col);
+                else
+                    ypre[it] = *(const float4*)(g.pos + (size_t)row * g.N + col);
+            }
+        }
 #pragma unroll
         for (int ii = 0; ii < PR / 16; ++ii) {
             const int i = pass * (PR / 16) + ii;
@@ -459,7 +477,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
         __builtin_amdgcn_wave_barrier();
-        const int ch = lane % CPR, rsub = lane / CPR;
 #pragma unroll
         for (int it = 0; it < PR / RPI; ++it) {
             const int rl = it * RPI + rsub;
@@ -481,9 +498,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
                 float* cp = (float*)g.C + (size_t)bz * g.sC + (size_t)row * g.ldc + col;
                 float4 o = *(const float4*)&v;
                 float4 y;
-                if constexpr (EPI == EPI_BIAS_RESID) y = *(const float4*)cp;
-                else if constexpr (EPI == EPI_BIAS_F32) y = make_float4(0.f, 0.f, 0.f, 0.f);
-                else y = *(const float4*)(g.pos + (size_t)row * g.N + col);
+                if constexpr (YIN) y = ypre[it];
+                else y = make_float4(0.f, 0.f, 0.f, 0.f);
                 o.x += y.x; o.y += y.y; o.z += y.z; o.w += y.w;
                 *(float4*)cp = o;
             }
