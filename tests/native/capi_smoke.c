@@ -141,6 +141,43 @@ static int parakeet_session(const char* dir, const float* pcm, size_t n) {
     return 0;
 }
 
+/* HipSmoothedVad (rust/spittle-hip): SileroVad::new(path, 0.3) + SmoothedVad::new(.., 15, 15, 2),
+ * push_frame per 30 ms frame, reset, destroy (audio.rs:132-134, recorder.rs:284-301) */
+static int vad_session(const char* model_path) {
+    spt_vad_params p;
+    spt_vad_default_params(&p);
+    CHECK(p.threshold == 0.3f && p.prefill_frames == 15 && p.hangover_frames == 15 && p.onset_frames == 2,
+          "SmoothedVad defaults of the app");
+    spt_vad* v = NULL;
+    char err[256] = {0};
+    spt_status st = spt_vad_create(model_path, &p, &v, err, sizeof err);
+    if (st != SPT_OK) fprintf(stderr, "vad create: %s\n", err);
+    CHECK(st == SPT_OK && v, "spt_vad_create");
+    float frame[480];
+    size_t kept = 0;
+    int speech = 0;
+    for (int f = 0; f < 100; ++f) { /* 3 s: 1 s silence, 1 s voiced tone bursts, 1 s silence */
+        for (int i = 0; i < 480; ++i) {
+            const float t = (float)(f * 480 + i) / 16000.0f;
+            const int voiced = f >= 33 && f < 66;
+            frame[i] = voiced ? 0.3f * sinf(2.0f * 3.14159265f * 180.0f * t) * (0.6f + 0.4f * sinf(2.0f * 3.14159265f * 4.0f * t))
+                              : 0.0f;
+        }
+        spt_vad_result* r = NULL;
+        CHECK(spt_vad_push(v, frame, 480, &r) == SPT_OK && r, spt_vad_last_error(v));
+        CHECK(r->n_frames == 1 && r->prob[0] >= 0.0f && r->prob[0] <= 1.0f, "one frame, a probability");
+        CHECK(r->n_samples == 0 || r->n_samples % 480 == 0, "whole frames kept");
+        kept += r->n_samples;
+        speech += r->kind[0] != 0;
+        spt_vad_result_free(r);
+    }
+    printf("vad: %d speech frames, %zu samples kept\n", speech, kept);
+    CHECK(spt_vad_reset(v, 0) == SPT_OK, "reset");
+    spt_vad_destroy(v);
+    CHECK(spt_vad_create("/nonexistent/silero_vad_v4.onnx", &p, &v, err, sizeof err) != SPT_OK && !v, "missing model");
+    return 0;
+}
+
 int main(int argc, char** argv) {
     const char* spec = argc > 1 ? argv[1] : "synthetic:tiny";
     printf("%s\n", spt_version());
@@ -170,6 +207,7 @@ int main(int argc, char** argv) {
     if (!rc) rc = one_session(spec, pcm, n); /* unload, then load again */
     if (!rc) rc = resampler_session();
     if (!rc && argc > 3) rc = parakeet_session(argv[3], pcm, n);
+    if (!rc && argc > 4) rc = vad_session(argv[4]);
     free(pcm);
     if (!rc) printf("capi_smoke ok\n");
     return rc;

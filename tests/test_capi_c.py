@@ -1,7 +1,8 @@
 """The C boundary as a C program sees it (tests/native/capi_smoke.c): the header compiles as
 C11 with -Wall -Werror, the program links against libspittle_hip.so, and -- on a GPU -- it runs
 the exact sequence the Rust binding performs (rust/spittle-hip: create -> transcribe -> read
--> free -> destroy, twice, plus the error paths)."""
+-> free -> destroy, twice, plus the error paths; the resampler, the Parakeet model directory and
+the voice-activity gate sessions)."""
 import os
 import subprocess
 
@@ -42,7 +43,8 @@ def test_c_program_compiles_and_links(tmp_path):
 @pytest.mark.gpu
 def test_c_program_runs_the_binding_sequence(tmp_path):
     exe = _build(tmp_path)
-    r = subprocess.run([exe, "synthetic:tiny", "--run", _model_dir(tmp_path)], capture_output=True, text=True,
-                       timeout=240)
+    vad_model = os.path.join(ROOT, "tests", "golden", "silero_vad_v4.onnx")
+    r = subprocess.run([exe, "synthetic:tiny", "--run", _model_dir(tmp_path), vad_model], capture_output=True,
+                       text=True, timeout=240)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "parakeet: " in r.stdout and "capi_smoke ok" in r.stdout
+    assert "parakeet: " in r.stdout and "vad: " in r.stdout and "capi_smoke ok" in r.stdout
