@@ -142,7 +142,7 @@ void spt_default_infer_params(spt_infer_params* p);
 
 /* model_spec: "synthetic:<tiny.en|tiny|base|small|medium|large-v3>[:enc=N][:dec=N][:seed=S]"
  * or the path of a whisper.cpp ggml model file (the catalog's ggml-*.bin; tensor types f32,
- * f16, q4_0, q4_1, q5_0, q5_1, q8_0; dequantised once at load into the engine dtype).
+ * f16, q4_0, q4_1, q5_0, q5_1, q8_0, q4_K, q5_K, q6_K; dequantised once at load into the engine dtype).
  * Replaces WhisperEngine::load_model(&path) (transcribe-rs; src-tauri/src/managers/
  * transcription.rs:261-276); bad files fail with SPT_ERR_LOAD and a message. */
 spt_status spt_ctx_create(const char* model_spec, const spt_model_params* params, spt_ctx** out,

@@ -443,16 +443,25 @@ __global__ __launch_bounds__(256) void conv_module_kernel(const T* __restrict__ 
     T* ob = out + (size_t)b * Tp * d;
     const int i = (blockIdx.z * 256 + threadIdx.x) * CM_V;  // first of this thread's 4 channels
     if (i >= d) return;
+    // every frame's pair is loaded unconditionally (a clamped row) and masked after: a load under a
+    // per-frame condition is branched around, and hipcc then waits for each one before the next
+    // (one dependent round trip per frame)
+    V4 xv[CM_TT + K - 1], gv[CM_TT + K - 1];
+#pragma unroll
+    for (int f = 0; f < CM_TT + K - 1; ++f) {
+        const int tt = min(max(t0 - K / 2 + f, 0), Tp - 1);
+        xv[f] = *(const V4*)(ab + (size_t)tt * 2 * d + i);
+        gv[f] = *(const V4*)(ab + (size_t)tt * 2 * d + d + i);
+    }
     float g[CM_TT + K - 1][CM_V];
 #pragma unroll
     for (int f = 0; f < CM_TT + K - 1; ++f) {
         const int tt = t0 - K / 2 + f;
+        const bool valid = tt >= 0 && tt < T3;
 #pragma unroll
-        for (int c = 0; c < CM_V; ++c) g[f][c] = 0.0f;
-        if (tt >= 0 && tt < T3) {
-            const V4 x = *(const V4*)(ab + (size_t)tt * 2 * d + i), gate = *(const V4*)(ab + (size_t)tt * 2 * d + d + i);
-#pragma unroll
-            for (int c = 0; c < CM_V; ++c) g[f][c] = to_f<T>((T)x[c]) * sigmoidf_(to_f<T>((T)gate[c]));  // GLU
+        for (int c = 0; c < CM_V; ++c) {
+            const float v = to_f<T>((T)xv[f][c]) * sigmoidf_(to_f<T>((T)gv[f][c]));  // GLU
+            g[f][c] = valid ? v : 0.0f;
         }
     }
     float wk[CM_V][K], bs[CM_V], bt[CM_V], bias[CM_V];
