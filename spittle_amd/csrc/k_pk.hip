@@ -518,8 +518,9 @@ __global__ void place_subperm_kernel(const float* __restrict__ s, int N, int C, 
 // ---------------------------------------------------------------- TDT greedy step
 // One kernel per stage of a decode step, 512 threads = 8 K-groups.  A workgroup owns DO outputs;
 // a lane loads a float4 of W^T (4 consecutive outputs of one k row; a wave-load covers
-// 256 / DO k rows x DO outputs = 1 KB), the x rows of up to 16 utterances sit in LDS as [k][16]
-// (broadcast float4 reads), so each lane carries 4 outputs x 16 rows of accumulators.  Every
+// 256 / DO k rows x DO outputs = 1 KB), the x rows of one row group (DR = 8
+// utterances; the groups spread over grid.y) sit in LDS as [k][XP] (broadcast float4 reads), so
+// each lane carries 4 outputs x 8 rows of accumulators.  Every
 // lane's weight loads for its K-group slice are issued together (8 per batch), the k rows of a
 // wave fold by xor shuffles and the 8 K-groups through LDS; the epilogue is the stage's own: the
 // LSTM cell (gate-interleaved W^T: a workgroup's 16 outputs are the i, f, g, o rows of 4 units),
@@ -558,10 +559,12 @@ __global__ __launch_bounds__(512) void dec_kernel(PkDecArgs a) {
         for (int u = 0; u < NWM; ++u)
             w[u] = u < NW ? *(const float4*)(wcol + (size_t)u * KS * DO) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    for (int rg = 0; rg < a.B; rg += DR) {
+    // this row group's staged x rows; a workgroup walks the row groups blockIdx.y, + gridDim.y, ..
+    // and issues the next group's rows as soon as the current ones sit in LDS, so they fly under
+    // the current group's products and reductions
+    const int K4 = a.K / 4, NE = K4 * DR, rstep = DR * gridDim.y;
+    auto load_x = [&](int rg, float4* v, float4* v2) {
         const int R = min(DR, a.B - rg);
-        const int K4 = a.K / 4, NE = K4 * DR;
-        float4 v[SE];
 #pragma unroll
         for (int u = 0; u < SE; ++u) {
             const int idx = min(tid + 512 * u, NE - 1);
@@ -572,22 +575,34 @@ __global__ __launch_bounds__(512) void dec_kernel(PkDecArgs a) {
                 v[u] = *(const float4*)(k < P ? lo : hi);
             } else if constexpr (MODE == PKD_PRED) {
                 v[u] = *(const float4*)(a.xin + (size_t)b * P + k);
-            } else {
-                const float4 e = *(const float4*)(a.fe + (size_t)b * P + k);  // the row's current frame
-                const float4 g = *(const float4*)(a.gp + (size_t)b * P + k);
-                v[u] = make_float4(fmaxf(e.x + g.x, 0.f), fmaxf(e.y + g.y, 0.f), fmaxf(e.z + g.z, 0.f),
-                                   fmaxf(e.w + g.w, 0.f));  // ReLU(enc + pred)
+            } else {  // joint input ReLU(enc + pred), formed at the LDS store (a prefetch must not wait)
+                v[u] = *(const float4*)(a.fe + (size_t)b * P + k);  // the row's current frame
+                v2[u] = *(const float4*)(a.gp + (size_t)b * P + k);
             }
         }
+    };
+    float4 v[SE], v2[MODE == PKD_JOINT ? SE : 1];
+    if (blockIdx.y * DR < a.B) load_x(blockIdx.y * DR, v, v2);
+    // consume the weight registers here: at their first use inside the loop hipcc would wait with
+    // vmcnt(0), which also drains the next row group's rows issued just before the products
+#pragma unroll
+    for (int u = 0; u < NWM; ++u) asm volatile("" ::"v"(w[u].x), "v"(w[u].y), "v"(w[u].z), "v"(w[u].w));
+    for (int rg = blockIdx.y * DR; rg < a.B; rg += rstep) {
+        const int R = min(DR, a.B - rg);
         // epilogue operands
-        float eb[4] = {0.f, 0.f, 0.f, 0.f}, eh = 0.f, ec = 0.f;
+        // (the two LSTM biases are added only at their use: an add here would wait on the loads
+        // in front of the LDS hand-off)
+        float eb[4] = {0.f, 0.f, 0.f, 0.f}, eb1[4] = {0.f, 0.f, 0.f, 0.f}, eh = 0.f, ec = 0.f;
         int eupd = 0;
         if constexpr (MODE == PKD_LSTM) {
             if (tid < DR * NU) {
                 const int jj = tid % NU, r = min(tid / NU, R - 1), j = blockIdx.x * NU + jj;
                 const size_t o = (size_t)(rg + r) * P + j;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) eb[q] = a.b0[q * P + j] + a.b1[q * P + j];
+                for (int q = 0; q < 4; ++q) {
+                    eb[q] = a.b0[q * P + j];
+                    eb1[q] = a.b1[q * P + j];
+                }
                 eh = a.h_in[o];
                 ec = a.c_in[o];
                 eupd = a.st[rg + r].upd;
@@ -608,13 +623,18 @@ __global__ __launch_bounds__(512) void dec_kernel(PkDecArgs a) {
             if (idx < NE) {
                 const int k = 4 * (idx / DR), r = idx % DR;
                 const bool ok = r < R;
-                xs[(k + 0) * XP + r] = ok ? v[u].x : 0.f;
-                xs[(k + 1) * XP + r] = ok ? v[u].y : 0.f;
-                xs[(k + 2) * XP + r] = ok ? v[u].z : 0.f;
-                xs[(k + 3) * XP + r] = ok ? v[u].w : 0.f;
+                float4 x = v[u];
+                if constexpr (MODE == PKD_JOINT)
+                    x = make_float4(fmaxf(x.x + v2[u].x, 0.f), fmaxf(x.y + v2[u].y, 0.f), fmaxf(x.z + v2[u].z, 0.f),
+                                    fmaxf(x.w + v2[u].w, 0.f));
+                xs[(k + 0) * XP + r] = ok ? x.x : 0.f;
+                xs[(k + 1) * XP + r] = ok ? x.y : 0.f;
+                xs[(k + 2) * XP + r] = ok ? x.z : 0.f;
+                xs[(k + 3) * XP + r] = ok ? x.w : 0.f;
             }
         }
         lds_sync();
+        if (rg + rstep < a.B) load_x(rg + rstep, v, v2);
         float acc[4][DR];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -668,8 +688,9 @@ __global__ __launch_bounds__(512) void dec_kernel(PkDecArgs a) {
                     const int j = blockIdx.x * NU + jj;
                     float g[4];
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) g[q] = eb[q] + red[(size_t)r * DO + q * NU + jj];
+                    for (int q = 0; q < 4; ++q) g[q] = (eb[q] + eb1[q]) + red[(size_t)r * DO + q * NU + jj];
                     float h = eh, c = ec;
+                    asm volatile("" : "+v"(eupd));  // keeps the flag test here, not at its load
                     if (eupd) {
                         c = sig_(g[1]) * c + sig_(g[0]) * tanhf(g[2]);
                         h = sig_(g[3]) * tanhf(c);
@@ -682,6 +703,7 @@ __global__ __launch_bounds__(512) void dec_kernel(PkDecArgs a) {
         } else if constexpr (MODE == PKD_PRED) {
             if (tid < DR * DO) {
                 const int r = tid / DO, o = tid % DO, n = n0 + o;
+                asm volatile("" : "+v"(eupd));
                 if (r < R && n < a.N && eupd) a.gp[(size_t)(rg + r) * P + n] = eb[0] + red[(size_t)r * DO + o];
             }
         } else {
@@ -926,6 +948,7 @@ constexpr int kDecSmemMax = 159 * 1024;  // dynamic LDS bound (the kernel's stat
 constexpr int kLstmDO = 16, kPredDO = 16, kJointDO = 64;
 // register-held wave-loads per lane and staged float4 per thread, sized for P <= 640
 constexpr int kNWL = 10, kSEL = 5, kNWP = 5, kSEP = 3, kNWJ = 20, kSEJ = 3;
+constexpr int kDecRowsWg = 2 * DR;  // utterances per decode workgroup (two row groups)
 
 void pk_prepare() {  // > 64 KiB dynamic LDS: per kernel and device, before any stream capture
     ensure_lds_attr((const void*)dec_kernel<PKD_LSTM, kLstmDO, kNWL, kSEL>, kDecSmemMax);
@@ -944,12 +967,17 @@ void pk_decode_stage(int mode, const PkDecArgs& a, hipStream_t s) {
         throw std::runtime_error("pk_decode_stage: bad shape");
     const size_t smem = ((size_t)a.K * XP + (size_t)DG * DR * DO) * 4;
     if (smem > (size_t)kDecSmemMax) throw std::runtime_error("pk_decode_stage: K too large for the LDS row stage");
-    const int grid = mode == PKD_LSTM ? a.P / (DO / 4) : a.ld / DO;
+    // row groups (DR utterances each) spread over grid.y, kDecRowsWg utterances per workgroup: one
+    // workgroup row running all 8 groups of a batch of 64 in turn took 50 us per LSTM stage (10 at
+    // B = 8), 16 per workgroup 39, 8 per workgroup the same (every workgroup re-reads its weight
+    // slice) and 32 slower (r3 exp_r3r: the stages are bound by rounds of workgroups, about one
+    // 512-thread workgroup per CU at a time, not by the passes)
+    const dim3 grid(mode == PKD_LSTM ? a.P / (DO / 4) : a.ld / DO, cdiv(a.B, kDecRowsWg));
     pk_prepare();
     switch (mode) {
-        case PKD_LSTM: hipLaunchKernelGGL((dec_kernel<PKD_LSTM, kLstmDO, kNWL, kSEL>), dim3(grid), dim3(512), smem, s, a); break;
-        case PKD_PRED: hipLaunchKernelGGL((dec_kernel<PKD_PRED, kPredDO, kNWP, kSEP>), dim3(grid), dim3(512), smem, s, a); break;
-        case PKD_JOINT: hipLaunchKernelGGL((dec_kernel<PKD_JOINT, kJointDO, kNWJ, kSEJ>), dim3(grid), dim3(512), smem, s, a); break;
+        case PKD_LSTM: hipLaunchKernelGGL((dec_kernel<PKD_LSTM, kLstmDO, kNWL, kSEL>), grid, dim3(512), smem, s, a); break;
+        case PKD_PRED: hipLaunchKernelGGL((dec_kernel<PKD_PRED, kPredDO, kNWP, kSEP>), grid, dim3(512), smem, s, a); break;
+        case PKD_JOINT: hipLaunchKernelGGL((dec_kernel<PKD_JOINT, kJointDO, kNWJ, kSEJ>), grid, dim3(512), smem, s, a); break;
         default: throw std::runtime_error("pk_decode_stage: bad mode");
     }
     SPT_LAUNCH_CHECK();
