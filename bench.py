@@ -237,19 +237,55 @@ def phase_rooflines(info: dict, phases: dict, B: int, decode_steps: int, dtype: 
     return out
 
 
-def parakeet_encoder_flops(info: dict, T: int) -> int:
-    """Algorithmic FLOPs of one utterance's Parakeet encoder pass at T mel frames (SURVEY §8d
-    style): subsampling convolutions + linear, the per-layer GEMMs (two half-FFNs, q/k/v/out,
-    the convolution module's pointwise pair), the relative-position projection, attention
-    (q.k, q.p and p.v over the T3 x T3 pairs), and the joint's encoder projection."""
+def parakeet_stage_work(info: dict, T: int, B: int) -> dict:
+    """Algorithmic work of one Parakeet encoder pass over B utterances of T mel frames, per stage
+    class of spt_parakeet_profile_encoder (SURVEY §8d style): (work, kind) with kind "f16"
+    (MFMA flops), "f32" (f32 MFMA flops) or "hbm" (bytes).  Subsampling convolutions + linear;
+    the relative-position projection once per pass (every layer's linear_pos over the 2 T3 - 1
+    shared positions); the two half-FFNs, q/k/v/out and the convolution module's pointwise pair
+    over the T3 frames; attention's q.k, q.p and p.v over the T3 x T3 pairs; the depthwise stage
+    as its GLU input read + output write (f16); the LayerNorms as the residual rows they read and
+    write: five per layer, four of them folding one pending f32 product and three writing x back
+    (the split-K slabs beyond one product are the implementation's, not counted)."""
     h = lambda t: (t - 1) // 2 + 1
     d, ff, C, L, P, K = info["d"], info["ff"], info["sub_ch"], info["n_layers"], info["pred"], info["conv_k"]
     T1, T2, T3 = h(T), h(h(T)), h(h(h(T)))
     F1, F2, F3 = h(info["n_mels"]), h(h(info["n_mels"])), h(h(h(info["n_mels"])))
+    rows = B * T3
     sub = 2 * 9 * C * T1 * F1 + 2 * 9 * C * (T2 * F2 + T3 * F3) + 2 * C * C * (T2 * F2 + T3 * F3) + 2 * C * F3 * d * T3
-    layer = T3 * (2 * 2 * 2 * d * ff + 2 * 4 * d * d + 2 * 3 * d * d + 2 * d * K) + 6 * T3 * T3 * d
-    pos = 2 * (2 * T3 - 1) * d * d * L
-    return int(sub + L * layer + pos + 2 * T3 * d * P)
+    return {"subsampling": (B * sub, "f16"),
+            "pos": (2 * (2 * T3 - 1) * d * d * L, "f16"),
+            "layernorm": (rows * L * 60 * d, "hbm"),
+            "ffn": (rows * L * 8 * d * ff, "f16"),
+            "qkv_out": (rows * L * 8 * d * d, "f16"),
+            "attn": (B * L * 6 * T3 * T3 * d, "f16"),
+            "conv_pw": (rows * L * 6 * d * d, "f16"),
+            "conv_dw": (rows * L * 6 * d, "hbm"),
+            "joint_enc": (rows * 2 * d * P, "f32")}
+
+
+def parakeet_encoder_flops(info: dict, T: int, B: int) -> int:
+    """Algorithmic FLOPs of one Parakeet encoder pass over B utterances of T mel frames: the MFMA
+    stages of parakeet_stage_work (the depthwise convolution's 2 K flops per element aside)."""
+    return int(sum(w for w, k in parakeet_stage_work(info, T, B).values() if k != "hbm"))
+
+
+def parakeet_kernels(e, info: dict, T: int, B: int, iters: int = 3) -> dict:
+    """Per-stage rooflines of the last call's encoder pass: spt_parakeet_profile_encoder re-runs it
+    eagerly (same buffers, bitwise the same output) with a HIP event after every stage; ms per
+    pass per stage class vs that stage's algorithmic work (parakeet_stage_work)."""
+    ms = e.profile_encoder(iters)
+    out = {}
+    for k, (w, kind) in parakeet_stage_work(info, T, B).items():
+        t = ms[k]
+        if kind == "hbm":
+            ach, peak, unit = w / (t * 1e-3) / 1e9 if t > 0 else 0.0, HBM_PEAK_GBS, "GB/s"
+        else:
+            ach, peak, unit = w / (t * 1e-3) / 1e12 if t > 0 else 0.0, (FP32_PEAK_TFS if kind == "f32" else MFMA_PEAK_F16_TFS), "TFLOP/s"
+        out[k] = {"ms": round(t, 4), "work": int(w), "bound": "hbm" if kind == "hbm" else "mfma", "achieved": round(ach, 1),
+                  "peak": peak, "unit": unit, "frac": round(ach / peak, 4)}
+    out["sum_ms"] = round(sum(ms.values()), 4)
+    return out
 
 
 def parakeet_bench(device: int, steps: int, warmup: int, with_cpu: bool) -> dict:
@@ -285,14 +321,15 @@ def parakeet_bench(device: int, steps: int, warmup: int, with_cpu: bool) -> dict
     if only == "offline":
         w1 = w1[:1]
     med, tot, res, ph = run(w1)
-    flops = 64 * parakeet_encoder_flops(info, 16000 // 160)
+    flops = parakeet_encoder_flops(info, 16000 // 160, len(w1))
     tf = flops / (ph["encoder_ms"] * 1e-3) / 1e12
     out["streaming_1s_b64"] = {"rtfx": round(64 * steps / tot, 2), "ms_per_pass_median": round(med * 1e3, 3),
                                "phases_ms": {k: round(v, 3) for k, v in ph.items() if k.endswith("_ms")},
                                "decode_steps": ph["n_steps"], "tokens_first_window": len(res[0].tokens),
                                "encoder_roofline": {"bound": "mfma", "flops_per_call": flops, "achieved": round(tf, 1),
                                                     "peak": MFMA_PEAK_F16_TFS, "unit": "TFLOP/s",
-                                                    "frac": round(tf / MFMA_PEAK_F16_TFS, 4)}}
+                                                    "frac": round(tf / MFMA_PEAK_F16_TFS, 4)},
+                               "kernels": parakeet_kernels(e, info, 16000 // 160, len(w1))}
     if only == "stream64":
         e.unload_model()
         return out
@@ -304,14 +341,15 @@ def parakeet_bench(device: int, steps: int, warmup: int, with_cpu: bool) -> dict
     if only == "stream":
         w30 = [w30[0][:16000]]
     med, tot, res, ph = run(w30)
-    flops = 8 * parakeet_encoder_flops(info, 480000 // 160)
+    flops = parakeet_encoder_flops(info, 480000 // 160, len(w30))
     tf = flops / (ph["encoder_ms"] * 1e-3) / 1e12
     out["offline_30s_b8"] = {"rtfx": round(8 * 30.0 * steps / tot, 2), "ms_per_pass_median": round(med * 1e3, 3),
                              "phases_ms": {k: round(v, 3) for k, v in ph.items() if k.endswith("_ms")},
                              "decode_steps": ph["n_steps"], "tokens_first_chunk": len(res[0].tokens),
                              "encoder_roofline": {"bound": "mfma", "flops_per_call": flops, "achieved": round(tf, 1),
                                                   "peak": MFMA_PEAK_F16_TFS, "unit": "TFLOP/s",
-                                                  "frac": round(tf / MFMA_PEAK_F16_TFS, 4)}}
+                                                  "frac": round(tf / MFMA_PEAK_F16_TFS, 4)},
+                             "kernels": parakeet_kernels(e, info, 480000 // 160, len(w30))}
     out["vs_published_cpu_rtfx"] = {"published": PK_PUBLISHED_RTFX, "source": "README.md:151 (i5 CPU, ONNX int8)",
                                     "streaming_ratio": round(out["streaming_1s_b64"]["rtfx"] / PK_PUBLISHED_RTFX, 1)}
     e.unload_model()

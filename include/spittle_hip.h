@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 9
+#define SPT_ABI_VERSION 10
 
 typedef enum {
     SPT_OK = 0,
@@ -367,6 +367,23 @@ spt_status spt_parakeet_transcribe_batch_device(spt_pk_ctx* ctx, const float* pc
                                                 const spt_pk_infer_params* params, spt_pk_result** out);
 void spt_parakeet_result_free(spt_pk_result* r);
 spt_status spt_parakeet_get_timings(const spt_pk_ctx* ctx, spt_pk_timings* t);
+/* ABI 10: encoder stage profile (measurement).  Re-runs the last call's encoder pass `iters` times
+ * eagerly, on the same buffers and shape (bitwise the same output), with a HIP event on the engine
+ * stream after every stage's launches; ms[c] = mean time per pass spent in stage class c.
+ * n >= SPT_PK_STAGE_COUNT. */
+typedef enum {
+    SPT_PK_STAGE_SUBSAMPLING = 0, /* conv stem: conv0, two depthwise + pointwise stages, linear */
+    SPT_PK_STAGE_POS = 1,         /* relative positions + every layer's linear_pos (one GEMM) */
+    SPT_PK_STAGE_LAYERNORM = 2,   /* 5 LayerNorms per layer (pending split-K products folded in) */
+    SPT_PK_STAGE_FFN = 3,         /* both half-FFNs' GEMMs (SiLU up-projection, split-K down) */
+    SPT_PK_STAGE_QKV_OUT = 4,     /* attention q/k/v and output GEMMs */
+    SPT_PK_STAGE_ATTN = 5,        /* relative-position attention */
+    SPT_PK_STAGE_CONV_PW = 6,     /* convolution module pointwise GEMMs */
+    SPT_PK_STAGE_CONV_DW = 7,     /* GLU + depthwise conv + BatchNorm + SiLU */
+    SPT_PK_STAGE_JOINT_ENC = 8,   /* the joint's encoder projection */
+    SPT_PK_STAGE_COUNT = 9
+} spt_pk_stage;
+spt_status spt_parakeet_profile_encoder(spt_pk_ctx* ctx, int32_t iters, double* ms, int32_t n);
 /* test hooks: normalised log-mel [n_mels][max(1, n / 160)] (n / 160 valid frames, NeMo get_seq_len); encoder output [T3][d] of a mel
  * [n_mels][T]; sum|w| and sum w of a tensor as stored (transposed tensors: SPT_ERR_UNSUPPORTED) */
 spt_status spt_parakeet_debug_mel(spt_pk_ctx* ctx, const float* pcm16k, size_t n_samples, float* out);

@@ -1,4 +1,4 @@
-//! Raw bindings to `include/spittle_hip.h` (ABI 9), the C boundary of the MI355X-native Whisper
+//! Raw bindings to `include/spittle_hip.h` (ABI 10), the C boundary of the MI355X-native Whisper
 //! and Parakeet-V3 backend.  One item per declaration of the header, same names, same layouts (x86-64 SysV; the
 //! layouts are checked field by field against gcc by tests/test_capi.py).  Safe wrappers live in
 //! the `spittle-hip` crate.
@@ -6,7 +6,8 @@
 
 use std::os::raw::{c_char, c_int, c_void};
 
-pub const SPT_ABI_VERSION: c_int = 9;
+pub const SPT_ABI_VERSION: c_int = 10;
+pub const SPT_PK_STAGE_COUNT: c_int = 9;
 
 pub type spt_status = c_int;
 pub const SPT_OK: spt_status = 0;
@@ -288,6 +289,8 @@ extern "C" {
     ) -> spt_status;
     pub fn spt_parakeet_result_free(r: *mut spt_pk_result);
     pub fn spt_parakeet_get_timings(ctx: *const spt_pk_ctx, t: *mut spt_pk_timings) -> spt_status;
+    // ---- ABI 10: encoder stage profile (ms[SPT_PK_STAGE_COUNT], spt_pk_stage order)
+    pub fn spt_parakeet_profile_encoder(ctx: *mut spt_pk_ctx, iters: i32, ms: *mut f64, n: i32) -> spt_status;
     pub fn spt_parakeet_debug_mel(ctx: *mut spt_pk_ctx, pcm16k: *const f32, n_samples: usize, out: *mut f32) -> spt_status;
     pub fn spt_parakeet_debug_encode(ctx: *mut spt_pk_ctx, mel: *const f32, t: i32, out: *mut f32) -> spt_status;
     pub fn spt_parakeet_debug_last_encoder(ctx: *mut spt_pk_ctx, b: i32, out: *mut f32, t3: *mut i32) -> spt_status;

@@ -40,10 +40,14 @@ EXPORTS = [
     # ABI 8: voice-activity gate
     "spt_vad_default_params", "spt_vad_create", "spt_vad_push", "spt_vad_result_free", "spt_vad_reset",
     "spt_vad_last_error", "spt_vad_destroy",
+    # ABI 10: Parakeet encoder stage profile
+    "spt_parakeet_profile_encoder",
 ]
 SPT_PK_WEIGHTS_EMPTY = 1
 SPT_PK_TS_TOKEN, SPT_PK_TS_WORD, SPT_PK_TS_SEGMENT = 0, 1, 2
 SPT_MODEL_WEIGHTS_EXTERNAL = 1
+# spt_pk_stage: encoder stage classes of spt_parakeet_profile_encoder, in order
+PK_STAGES = ("subsampling", "pos", "layernorm", "ffn", "qkv_out", "attn", "conv_pw", "conv_dw", "joint_enc")
 PROBES = {"dec_cross_attn": 0, "dec_self_attn": 1, "dec_logits": 2, "dec_fc1": 3, "enc_fc1_gemm": 4,
           "enc_attn": 5}
 
@@ -212,6 +216,7 @@ def load():
                                                        C.POINTER(PkInferParams), PR]
     L.spt_parakeet_result_free.argtypes = [C.POINTER(PkResult)]
     L.spt_parakeet_get_timings.argtypes = [vp, C.POINTER(PkTimings)]
+    L.spt_parakeet_profile_encoder.argtypes = [vp, C.c_int32, C.POINTER(C.c_double), C.c_int32]
     L.spt_parakeet_debug_mel.argtypes = [vp, fp, C.c_size_t, fp]
     L.spt_parakeet_debug_encode.argtypes = [vp, fp, C.c_int32, fp]
     L.spt_parakeet_debug_decode.argtypes = [vp, fp, C.c_int32, C.c_int32, PR]

@@ -335,7 +335,7 @@ spt_status run_windows(spt_ctx* c, std::vector<Window>& win, size_t n_utt, const
 
 extern "C" {
 
-const char* spt_version(void) { return "spittle_amd 0.9.0 (gfx950, ABI 9)"; }
+const char* spt_version(void) { return "spittle_amd 0.10.0 (gfx950, ABI 10)"; }
 
 const char* spt_language_code(int32_t lang_id) { return spt::lang_code(lang_id); }
 

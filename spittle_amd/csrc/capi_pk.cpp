@@ -514,6 +514,17 @@ spt_status spt_parakeet_get_timings(const spt_pk_ctx* ctx, spt_pk_timings* t) {
     return SPT_OK;
 }
 
+spt_status spt_parakeet_profile_encoder(spt_pk_ctx* ctx, int32_t iters, double* ms, int32_t n) {
+    static_assert(SPT_PK_STAGE_COUNT == spt::PK_ST_COUNT, "stage classes");
+    if (!ctx || !ms || n < SPT_PK_STAGE_COUNT) return fail(ctx, SPT_ERR_INVALID_ARG, "null argument or n too small");
+    try {
+        ctx->eng->profile_encoder(iters, ms);
+        return SPT_OK;
+    } catch (const std::exception& e) {
+        return fail(ctx, classify(e), e.what());
+    }
+}
+
 spt_status spt_parakeet_debug_mel(spt_pk_ctx* ctx, const float* pcm16k, size_t n_samples, float* out) {
     if (!ctx || !out || (n_samples && !pcm16k)) return fail(ctx, SPT_ERR_INVALID_ARG, "null argument");
     if (n_samples > (size_t)ctx->eng->max_samples()) return fail(ctx, SPT_ERR_INVALID_ARG, "longer than max_seconds");

@@ -155,7 +155,9 @@ void ParakeetEngine::release() {
     for (auto& kv : enc_graphs_) (void)hipGraphExecDestroy(kv.second);
     enc_graphs_.clear();
     for (auto& e : ev_) if (e) (void)hipEventDestroy(e);
+    for (auto& e : prof_ev_) if (e) (void)hipEventDestroy(e);
     ev_.clear();
+    prof_ev_.clear();
     if (warena_) (void)hipFree(warena_);
     if (aarena_) (void)hipFree(aarena_);
     if (scratch_) (void)hipFree(scratch_);
@@ -521,38 +523,54 @@ void ParakeetEngine::run_encoder(int B, int Tp, int T1p, int T2p, int T3p) {
     float* x2 = x_ + (int64_t)max_batch_ * T3max_ * d;
     const int M = B * T3p;
     gemm(dt_, EPI_BIAS_F32, y3_, F3_ * C, sub_w_, F3_ * C, M, d, F3_ * C, sub_b_, x, d, sqrtf((float)d));
+    mark(PK_ST_SUB);
     // ---- relative positions, projected for every layer at once
     pk_relpos(dt_, T3p, d, pe_, st_);
     gemm(dt_, EPI_BIAS, pe_, d, pos_w_, d, 2 * T3p - 1, Ln * d, d, nullptr, pp_, Ln * d);
+    mark(PK_ST_POS);
     const int64_t sst = (int64_t)M * d;
     int ks;
     for (int l = 0; l < Ln; ++l) {
         const Layer& y = L_[l];
         // 1/2 FFN; its product stays pending in the slabs until the next LayerNorm
         layernorm(dt_, x, M, d, y.ln1_w, y.ln1_b, xn_, st_);
+        mark(PK_ST_LN);
         gemm(dt_, EPI_BIAS_SWISH, xn_, d, y.ff1_w1, d, M, ff, d, y.ff1_b1, ffh_, ff);
         ks = gemm(dt_, EPI_PARTIAL, ffh_, ff, y.ff1_w2, ff, M, d, ff, nullptr, slab_, d);
+        mark(PK_ST_FFN);
         // rel-pos MHSA
         layernorm_pend(dt_, x, M, d, slab_, ks, sst, y.ff1_b2, 0.5f, y.lna_w, y.lna_b, xn_, true, st_);
+        mark(PK_ST_LN);
         gemm(dt_, EPI_BIAS, xn_, d, y.qkv_w, d, M, 3 * d, d, y.qkv_b, qkv_, 3 * d);
+        mark(PK_ST_QKVO);
         pk_rel_attn(dt_, qkv_, (const char*)pp_ + (size_t)l * d * esz_, Ln * d, y.pos_u, y.pos_v, lens_, B, T3p, H, dk,
                     ctx_, st_);
+        mark(PK_ST_ATTN);
         ks = gemm(dt_, EPI_PARTIAL, ctx_, d, y.o_w, d, M, d, d, nullptr, slab_, d);
+        mark(PK_ST_QKVO);
         // convolution module
         layernorm_pend(dt_, x, M, d, slab_, ks, sst, y.o_b, 1.0f, y.lnc_w, y.lnc_b, xn_, true, st_);
+        mark(PK_ST_LN);
         gemm(dt_, EPI_BIAS, xn_, d, y.pw1_w, d, M, 2 * d, d, y.pw1_b, glu_, 2 * d);
+        mark(PK_ST_CONV_PW);
         pk_conv_module(dt_, glu_, lens_, B, T3p, d, dm_.conv_k, y.dw_w, y.dw_b, y.bn_g, y.bn_b, y.bn_m, y.bn_v, cv_, st_);
+        mark(PK_ST_CONV_DW);
         ks = gemm(dt_, EPI_PARTIAL, cv_, d, y.pw2_w, d, M, d, d, nullptr, slab_, d);
+        mark(PK_ST_CONV_PW);
         // 1/2 FFN
         layernorm_pend(dt_, x, M, d, slab_, ks, sst, y.pw2_b, 1.0f, y.ln2_w, y.ln2_b, xn_, true, st_);
+        mark(PK_ST_LN);
         gemm(dt_, EPI_BIAS_SWISH, xn_, d, y.ff2_w1, d, M, ff, d, y.ff2_b1, ffh_, ff);
         ks = gemm(dt_, EPI_PARTIAL, ffh_, ff, y.ff2_w2, ff, M, d, ff, nullptr, slab_, d);
+        mark(PK_ST_FFN);
         // LayerNorm out (f32) of x + the pending 1/2 FFN into the other residual buffer
         layernorm_pend(DT_F32, x, M, d, slab_, ks, sst, y.ff2_b2, 0.5f, y.lno_w, y.lno_b, x2, false, st_);
+        mark(PK_ST_LN);
         std::swap(x, x2);
     }
     // the joint's encoder projection of every frame (f32)
     gemm(DT_F32, EPI_BIAS, x, d, jenc_w_, d, M, dm_.pred, d, jenc_b_, fe_, dm_.pred);
+    mark(PK_ST_JOINT);
     enc_out_ = x;
 }
 
@@ -580,6 +598,49 @@ void ParakeetEngine::encode(int B, int Tp, int T1p, int T2p, int T3p) {
     } else {
         run_encoder(B, Tp, T1p, T2p, T3p);
     }
+}
+
+void ParakeetEngine::mark(int cls) {
+    if (!prof_on_) return;
+    const size_t i = prof_cls_.size();
+    if (i >= prof_ev_.size()) throw std::runtime_error("profile_encoder: event pool exhausted");
+    HIP_CHECK(hipEventRecord(prof_ev_[i], st_));
+    prof_cls_.push_back(cls);
+}
+
+void ParakeetEngine::profile_encoder(int iters, double ms[PK_ST_COUNT]) {
+    select();
+    const int B = last_dims_[0];
+    if (B < 1) throw std::runtime_error("profile_encoder needs a completed transcription call first");
+    if (iters < 1 || iters > 1000) throw std::runtime_error("iters out of range");
+    const size_t need = (size_t)14 * dm_.n_layers + 8;  // 13 marks per layer
+    while (prof_ev_.size() < need) {
+        hipEvent_t e;
+        HIP_CHECK(hipEventCreate(&e));
+        prof_ev_.push_back(e);
+    }
+    for (int c = 0; c < PK_ST_COUNT; ++c) ms[c] = 0.0;
+    for (int it = 0; it < iters; ++it) {
+        prof_cls_.clear();
+        prof_on_ = true;
+        HIP_CHECK(hipEventRecord(ev_[0], st_));
+        try {
+            run_encoder(B, last_dims_[1], last_dims_[2], last_dims_[3], last_dims_[4]);
+        } catch (...) {
+            prof_on_ = false;
+            throw;
+        }
+        prof_on_ = false;
+        HIP_CHECK(hipStreamSynchronize(st_));
+        hipEvent_t prev = ev_[0];
+        for (size_t i = 0; i < prof_cls_.size(); ++i) {
+            float t = 0.f;
+            HIP_CHECK(hipEventElapsedTime(&t, prev, prof_ev_[i]));
+            ms[prof_cls_[i]] += t;
+            prev = prof_ev_[i];
+        }
+    }
+    for (int c = 0; c < PK_ST_COUNT; ++c) ms[c] /= iters;
 }
 
 void ParakeetEngine::enqueue_step(int B, int max_symbols, int cap, int parity) {
@@ -677,6 +738,7 @@ void ParakeetEngine::transcribe_device(const float* pcm_dev, int64_t stride, con
     frame_counts(n, B, &lens, &Tp, &T1p, &T2p, &T3p);
     last_lens_ = lens;
     last_T3p_ = T3p;
+    last_dims_[0] = B; last_dims_[1] = Tp; last_dims_[2] = T1p; last_dims_[3] = T2p; last_dims_[4] = T3p;
     HIP_CHECK(hipEventRecord(ev_[0], st_));
     HIP_CHECK(hipMemcpyAsync(nsamp_, n, B * 4, hipMemcpyHostToDevice, st_));
     HIP_CHECK(hipMemcpyAsync(lens_, lens.data(), lens.size() * 4, hipMemcpyHostToDevice, st_));

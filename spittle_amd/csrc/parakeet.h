@@ -30,6 +30,10 @@ struct PkUtt {                  // one utterance's TDT greedy output
     std::vector<float> top1, top2;  // the token's joint logit and the runner-up's
 };
 
+// encoder stage classes of profile_encoder (spt_pk_stage in include/spittle_hip.h)
+enum { PK_ST_SUB = 0, PK_ST_POS, PK_ST_LN, PK_ST_FFN, PK_ST_QKVO, PK_ST_ATTN, PK_ST_CONV_PW, PK_ST_CONV_DW,
+       PK_ST_JOINT, PK_ST_COUNT };
+
 struct PkTimings {
     double mel_ms = 0, encoder_ms = 0, decode_ms = 0, total_ms = 0, h2d_ms = 0;
     int n_steps = 0, batch = 0, enc_frames = 0;
@@ -79,6 +83,10 @@ public:
     void debug_decode(const float* enc_host, int T3, int max_symbols, PkUtt* out);
     // the encoder output rows [T3][d] (f32) of batch row b of the last transcribe call; returns T3
     int debug_last_encoder(int b, float* out_host);
+    // measurement: re-run the last call's encoder pass `iters` times eagerly (same buffers and
+    // shape, bitwise the same output) with a HIP event after every launch; ms[c] = mean time per
+    // pass spent in stage class c (PK_ST_*)
+    void profile_encoder(int iters, double ms[PK_ST_COUNT]);
     bool debug_weight_checksum(int tid, double* out2);
 
 private:
@@ -152,6 +160,11 @@ private:
     float *frames_ = nullptr, *spec_ = nullptr, *mel_ = nullptr;
     void *y1_ = nullptr, *y2a_ = nullptr, *y2_ = nullptr, *y3a_ = nullptr, *y3_ = nullptr;
     float* x_ = nullptr;
+    void mark(int cls);           // profile_encoder: event after the launch(es) of stage class cls
+    std::vector<hipEvent_t> prof_ev_;
+    std::vector<int> prof_cls_;
+    bool prof_on_ = false;
+    int last_dims_[5] = {0, 0, 0, 0, 0};  // the last call's B, Tp, T1p, T2p, T3p
     std::vector<int> last_lens_;  // the last transcribe call's per-row lengths {T, T1, T2, T3}
     int last_T3p_ = 0;
     float* enc_out_ = nullptr;  // the residual buffer holding the last call's encoder output

@@ -166,6 +166,13 @@ class ParakeetEngine:
         _check(self._lib, self._ctx, self._lib.spt_parakeet_get_timings(self._need(), C.byref(t)))
         return {k: getattr(t, k) for k, _ in L.PkTimings._fields_}
 
+    def profile_encoder(self, iters: int = 5) -> Dict[str, float]:
+        """ms per pass in each encoder stage class (L.PK_STAGES) of the last call's shape, re-run
+        eagerly with a HIP event after every stage (spt_parakeet_profile_encoder)."""
+        ms = (C.c_double * len(L.PK_STAGES))()
+        _check(self._lib, self._ctx, self._lib.spt_parakeet_profile_encoder(self._need(), int(iters), ms, len(ms)))
+        return {k: ms[i] for i, k in enumerate(L.PK_STAGES)}
+
     def debug_mel(self, pcm) -> np.ndarray:
         a = np.ascontiguousarray(np.asarray(pcm, dtype=np.float32).ravel())
         out = np.empty((self.info()["n_mels"], max(1, a.size // 160)), np.float32)  # n // 160 valid frames (NeMo get_seq_len)

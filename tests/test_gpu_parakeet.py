@@ -193,6 +193,22 @@ def test_errors(small32):
     assert r.n_chunks == 0 and r.text == ""
 
 
+def test_profile_encoder_is_measurement_only(small16):
+    """spt_parakeet_profile_encoder (the bench's per-stage rooflines) re-runs the last call's
+    encoder pass eagerly with an event after every stage: each stage class gets time, and the
+    re-run leaves the last call's encoder output bitwise as it was."""
+    from spittle_amd import _lib as L
+    e, _ = small16
+    pcms = [synth_audio(40 + i, 16000) for i in range(3)]
+    e.transcribe_batch(pcms, _tok_params())
+    before = [e.debug_last_encoder(b) for b in range(3)]
+    st = e.profile_encoder(3)
+    assert list(st) == list(L.PK_STAGES)
+    assert all(v > 0 for v in st.values()), st
+    for b, a in enumerate(before):
+        assert np.array_equal(a, e.debug_last_encoder(b))
+
+
 def test_encoder_f16_close_to_oracle(small16):
     e, om = small16
     mel = P.mel(synth_audio(3, 16000 * 3))
