@@ -559,6 +559,7 @@ void enc_attention(int dtype, const void* qkv, int B, int T, int H, void* out, h
         dim3 g(cdiv(T, 256), H, B);
         if (sum == 1) hipLaunchKernelGGL(attn_bf16_q64_kernel<1>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
         else if (sum == 2) hipLaunchKernelGGL(attn_bf16_q64_kernel<2>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
+        else if (sum == 3 && swz == 3) hipLaunchKernelGGL((attn_bf16_q64_kernel<3, 3>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
         else if (sum == 3) hipLaunchKernelGGL(attn_bf16_q64_kernel<3>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
         else if (swz == 0) hipLaunchKernelGGL((attn_bf16_q64_kernel<0, 0>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
         else if (swz == 1) hipLaunchKernelGGL((attn_bf16_q64_kernel<0, 1>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
