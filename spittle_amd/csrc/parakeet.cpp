@@ -476,15 +476,21 @@ void ParakeetEngine::run_mel(const float* pcm_dev, int64_t stride, int B, int Tp
 
 // GEMM tile choice: the 256 x 256 tile whenever at least ~96 of its workgroups are in flight
 // (its MFMA efficiency beats the 128 x 128 tile's even with part of the chip idle), else the
-// 128 x 128 tile.  Residual products (EPI_PARTIAL, N = d) also split K over grid.y toward ~192
-// (256-tile) or ~512 (128-tile) workgroups; their f32 slabs are summed, with the bias and the
-// 1/2 FFN scale, by the LayerNorm that reads the residual next.  Returns the split used.
+// 128 x 128 tile, or the 64 x 128 tile where the 128 x 128 one would leave CUs without a second
+// workgroup (the C5 shape, M = 832: two waves per SIMD cover each other's LDS reads and slab
+// waits; r3 exp_r3v / exp_r3w: 19-35 % faster than either larger tile there, bitwise equal).
+// Residual products (EPI_PARTIAL, N = d) also split K over grid.y toward ~192 (256-tile) or ~512
+// (128-tile) workgroups, the 64-row tile keeping >= 8 K-steps per split; their f32 slabs are
+// summed, with the bias and the 1/2 FFN scale, by the LayerNorm that reads the residual next.
+// Returns the split used.
 int ParakeetEngine::gemm(int dt, int epi, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
                          const float* bias, void* Cp, int ldc, float alpha) {
-    // SPT_GEMM_T256 / SPT_NO_SKINNY: read per call so tests can pin each variant (eager calls only:
-    // a captured encoder graph keeps the variants it was captured with)
+    // SPT_GEMM_T256 / SPT_GEMM_T64 / SPT_NO_SKINNY: read per call so tests can pin each variant
+    // (eager calls only: a captured encoder graph keeps the variants it was captured with)
     const char* t256e = getenv("SPT_GEMM_T256");
     const int t256 = t256e ? atoi(t256e) : 96;
+    const char* t64e = getenv("SPT_GEMM_T64");
+    const bool t64_ok = !(t64e && atoi(t64e) == 0);
     const bool no_skinny = getenv("SPT_NO_SKINNY") != nullptr;
     int variant = 1, ks = 1;
     if (dt != DT_F32 && M <= 64 && N % 16 == 0 && K % 128 == 0 && !no_skinny) {
@@ -492,16 +498,20 @@ int ParakeetEngine::gemm(int dt, int epi, const void* A, int lda, const void* W,
         variant = 3;
         if (epi == EPI_PARTIAL)
             while (ks < 8 && (N / 16) * ks < 256 && K % (2 * ks) == 0 && (K / (2 * ks)) % 128 == 0) ks *= 2;
-    } else if (dt != DT_F32 && N % 256 == 0 && K % 64 == 0) {
+    } else if (dt != DT_F32 && N % 256 == 0 && K % 64 == 0 && !(t64_ok && (int64_t)cdiv(M, 256) * (N / 256) < 32)) {
         const int64_t t = (int64_t)cdiv(M, 256) * (N / 256);
         int k2 = 1;
         if (epi == EPI_PARTIAL)
             while (k2 < 8 && t * k2 < 192 && K % (2 * k2) == 0 && (K / (2 * k2)) % 64 == 0 && K / (2 * k2) >= 256) k2 *= 2;
         if (t * k2 >= t256) { variant = 2; ks = k2; }
     }
+    if (variant == 1 && dt != DT_F32 && M > 64 && (int64_t)cdiv(M, 128) * (N / 128) < 256 && t64_ok) variant = 4;
     if (variant == 1 && epi == EPI_PARTIAL) {
         const int64_t t = (int64_t)cdiv(M, 128) * (N / 128);
         while (ks < 8 && t * ks * 2 <= 512 && K % (2 * ks) == 0 && (K / (2 * ks)) % 64 == 0) ks *= 2;
+    } else if (variant == 4 && epi == EPI_PARTIAL) {
+        const int64_t t = (int64_t)cdiv(M, 64) * (N / 128);
+        while (ks < 8 && t * ks * 2 <= 512 && K % (2 * ks) == 0 && K / (2 * ks) >= 512 && (K / (2 * ks)) % 64 == 0) ks *= 2;
     }
     GemmArgs g{};
     g.A = A; g.lda = lda; g.W = W; g.ldw = ldw; g.M = M; g.N = N; g.K = K; g.bias = bias;

@@ -333,20 +333,25 @@ int main(int argc, char** argv) {
         float* bias = frand(N, 3, -5);
         const size_t cbytes = (size_t)ks * M * N * 4;
         void* C = dalloc(cbytes);
+        float* C0 = frand(cbytes / 4, 5, 0);  // the residual operand of EPI_BIAS_RESID (C += alpha * v)
         GemmArgs g{};
+        g.alpha = 1.0f;
         g.A = A; g.lda = K; g.W = W; g.ldw = K; g.M = M; g.N = N; g.K = K; g.bias = bias; g.C = C; g.ldc = N;
         g.kv_B = M / 1500; g.kv_T = 1500; g.kv_H = 20; g.ksplit = ks; g.c_split = (int64_t)M * N;
         if (epi == EPI_BIAS_GELU_POS) g.pos = frand((size_t)M * N, 4, 0);
         HIP_CHECK(hipDeviceSynchronize());  // inputs are generated on the null stream
         std::vector<char> ref(cbytes), out(cbytes);
-        double us[3] = {0, 0, 0};
-        for (int v = 1; v <= 2; ++v) {
-            HIP_CHECK(hipMemsetAsync(C, 0, cbytes, st));
+        double us[5] = {0, 0, 0, 0, 0};
+        std::vector<char> out64(cbytes);
+        for (int v : {1, 2, 4}) {
+            HIP_CHECK(hipMemcpyAsync(C, C0, cbytes, hipMemcpyDeviceToDevice, st));
             gemm_nt_variant(dt, epi, g, 1, v, st);
             HIP_CHECK(hipStreamSynchronize(st));
-            HIP_CHECK(hipMemcpy(v == 1 ? ref.data() : out.data(), C, cbytes, hipMemcpyDeviceToHost));
+            HIP_CHECK(hipMemcpy(v == 1 ? ref.data() : v == 2 ? out.data() : out64.data(), C, cbytes, hipMemcpyDeviceToHost));
             us[v] = time_us(st, 20, [&] { gemm_nt_variant(dt, epi, g, 1, v, st); });
         }
+        size_t diff64 = 0;
+        for (size_t i = 0; i < cbytes; ++i) diff64 += ref[i] != out64[i];
         size_t diff = 0, shown = 0;
         for (size_t i = 0; i < cbytes; ++i) {
             if (ref[i] == out[i]) continue;
@@ -360,8 +365,9 @@ int main(int argc, char** argv) {
             }
         }
         const double fl = 2.0 * M * N * K;
-        printf("gemm M=%d N=%d K=%d ks=%d epi=%d dt=%d : 128-tile %.2f us %.1f TF/s | 256-tile %.2f us %.1f TF/s | bytes differing %zu\n",
-               M, N, K, ks, epi, dt, us[1], fl / us[1] / 1e6, us[2], fl / us[2] / 1e6, diff);
+        printf("gemm M=%d N=%d K=%d ks=%d epi=%d dt=%d : 128-tile %.2f us %.1f TF/s | 256-tile %.2f us %.1f TF/s | bytes differing %zu"
+               " | 64x128 %.2f us %.1f TF/s, bytes differing from 128-tile %zu\n",
+               M, N, K, ks, epi, dt, us[1], fl / us[1] / 1e6, us[2], fl / us[2] / 1e6, diff, us[4], fl / us[4] / 1e6, diff64);
         return 0;
     }
     if (what == "layer" || what == "layer2") {
