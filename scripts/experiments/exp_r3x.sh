@@ -1,4 +1,4 @@
-# r3 s2: 64 x 128 tile for small-M GEMMs (Parakeet C5 incl. residual products; Whisper single-window
+# r3 s2: small-M GEMM tiles (64 x 128, then 64 x 64; Parakeet C5 incl. residual products; Whisper single-window
 # encoder through the automatic tile choice): ubench shapes, the whole GPU suite, the Parakeet lines
 # with and without the tile (SPT_GEMM_T64=0), and the default bench line (app-call latency included)
 export TMPDIR=/tmp

@@ -95,36 +95,40 @@ __device__ __forceinline__ void epi_store(const GemmArgs& g, int bz, int row, co
 // computed.  The 16-slab GEMMs of a Parakeet streaming pass (M = 832, K = 1024) and Whisper's
 // smaller shapes give about one workgroup per CU and no other wave to cover a slab's load
 // latency; with two slots every k-step waited for its own DMA round trip.
-// BMT = 64 halves the tile's rows (each wave 32 x 64 of C): at M = 832 a 128-row tile gives at most
-// one workgroup per CU, so one wave per SIMD with every LDS read and DMA wait of a k-step exposed.
-template <typename T, int EPI, int ST, int BMT = BM>
+// BMT = 64 halves the tile's rows (each wave 32 x 64 of C), BNT = 64 its columns: at M = 832 a
+// 128 x 128 tile gives at most one workgroup per CU, so one wave per SIMD with every LDS read and
+// DMA wait of a k-step exposed.  Every C element is the same MFMA chain in every tile shape.
+template <typename T, int EPI, int ST, int BMT = BM, int BNT = BN>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256, 1) put the accumulators in AGPRs + ~90 copies per k-step
-    static_assert(BMT == 64 || BMT == 128, "tile rows");
+    static_assert((BMT == 64 || BMT == 128) && (BNT == 64 || BNT == 128), "tile shape");
+    static_assert(ST == 2 || (BMT == 128 && BNT == 128), "deeper rings: 128 x 128 only");
     constexpr int MI = BMT / 32;      // 16-row A fragments per wave
+    constexpr int NJ = BNT / 32;      // 16-column W fragments per wave
     constexpr int PA = BMT / 32;      // A pieces (8 rows x 128 B) a wave stages per slab
-    extern __shared__ __attribute__((aligned(16))) char smem[];  // [slot][A BMT rows | W 128 rows][128 B]
+    constexpr int PW = BNT / 32;      // W pieces
+    extern __shared__ __attribute__((aligned(16))) char smem[];  // [slot][A BMT rows | W BNT rows][128 B]
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 1, wn = wid & 1;
-    const int nnt = g.N / BN;
+    const int nnt = g.N / BNT;
     // bijective XCD-aware remap of the linear tile id
     const int nwg = gridDim.x, bid = blockIdx.x;
     const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     const int nmt = (g.M + BMT - 1) / BMT;
     const int tm = g.nmajor ? wg % nmt : wg / nnt, tn = g.nmajor ? wg / nmt : wg % nnt;
-    const int m0 = tm * BMT, n0 = tn * BN;
+    const int m0 = tm * BMT, n0 = tn * BNT;
     const int bz = blockIdx.z;
     const int Kc = g.K / g.ksplit;  // this workgroup's K range: [blockIdx.y * Kc, + Kc)
     const T* A = (const T*)g.A + (size_t)bz * g.sA + (size_t)blockIdx.y * Kc;
     const T* W = (const T*)g.W + (size_t)blockIdx.y * Kc;
 
-    // per-lane source pointers for the PA A pieces and 4 W pieces this wave stages
+    // per-lane source pointers for the PA A pieces and PW W pieces this wave stages
     const char* srcA[PA];
-    const char* srcW[4];
+    const char* srcW[PW];
     const int prow = lane >> 3, pch = lane & 7;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int rt = (wid * 4 + i) * 8 + prow;
+    for (int i = 0; i < PW; ++i) {
+        const int rt = (wid * PW + i) * 8 + prow;
         const int c = pch ^ swz(rt);
         srcW[i] = (const char*)(W + (size_t)(n0 + rt) * g.ldw) + c * 16;
     }
@@ -134,22 +138,22 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256,
         const int ra = min(m0 + rt, g.M - 1);
         srcA[i] = (const char*)(A + (size_t)ra * g.lda) + (pch ^ swz(rt)) * 16;
     }
-    auto lds_a = [&](int buf) -> SPT_LDS char* { return (SPT_LDS char*)smem + buf * (BMT + BN) * SLAB; };
-    auto lds_w = [&](int buf) -> SPT_LDS char* { return (SPT_LDS char*)smem + buf * (BMT + BN) * SLAB + BMT * SLAB; };
+    auto lds_a = [&](int buf) -> SPT_LDS char* { return (SPT_LDS char*)smem + buf * (BMT + BNT) * SLAB; };
+    auto lds_w = [&](int buf) -> SPT_LDS char* { return (SPT_LDS char*)smem + buf * (BMT + BNT) * SLAB + BMT * SLAB; };
     auto stage = [&](int buf, int kt) {
         const size_t koff = (size_t)kt * SLAB;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             if (i < PA) glds16(srcA[i] + koff, lds_a(buf) + (wid * PA + i) * 1024);
-            glds16(srcW[i] + koff, lds_w(buf) + (wid * 4 + i) * 1024);
+            if (i < PW) glds16(srcW[i] + koff, lds_w(buf) + (wid * PW + i) * 1024);
         }
     };
 
-    f32x4 acc[MI][4];
+    f32x4 acc[MI][NJ];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int nkt = Kc * (int)sizeof(T) / SLAB;
     const int fr = lane & 15, fq = lane >> 4;
@@ -160,13 +164,11 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256,
     for (int p = 0; p < ST - 1; ++p) stage(p, min(p, nkt - 1));
     for (int kt = 0; kt < nkt; ++kt) {
         const int cur = kt % ST;
-        // slab kt landed (PA + 4 DMA instructions per slab and wave; ST - 2 younger slabs may fly
-        // on), and every wave is done with slab kt - 1, whose slot the next issue overwrites
+        // slab kt landed (8 DMA instructions per slab and wave; ST - 2 younger slabs may fly on),
+        // and every wave is done with slab kt - 1, whose slot the next issue overwrites
         if constexpr (ST == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else if constexpr (ST == 3 && PA == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if constexpr (ST == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else if constexpr (PA == 4) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        else if constexpr (ST == 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
         // a bare s_barrier: __syncthreads()'s release fence would make the compiler drain every
         // in-flight slab (vmcnt(0)) in front of it
         asm volatile("s_barrier" ::: "memory");
@@ -176,11 +178,11 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256,
         if constexpr (sizeof(T) == 2) {
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
-                bf16x8 af[MI], wf[4];
+                bf16x8 af[MI], wf[NJ];
                 const int c = 4 * s + fq;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int rw = wn * 64 + 16 * i + fr;
+                for (int i = 0; i < NJ; ++i) {
+                    const int rw = wn * (BNT / 2) + 16 * i + fr;
                     wf[i] = *(const SPT_LDS bf16x8*)(lw + rw * SLAB + ((c ^ swz(rw)) << 4));
                 }
 #pragma unroll
@@ -191,7 +193,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256,
 #pragma unroll
                 for (int i = 0; i < MI; ++i)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
+                    for (int j = 0; j < NJ; ++j) {
                         if constexpr (TypeTag<T>::id == 2)
                             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, af[i]),
                                                                                __builtin_bit_cast(f16x8, wf[j]), acc[i][j], 0, 0, 0);
@@ -200,14 +202,14 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256,
                     }
             }
         } else {
-            f32x4 af[MI][2], wf[4][2];
+            f32x4 af[MI][2], wf[NJ][2];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int rw = wn * 64 + 16 * i + fr;
+                const int rw = wn * (BNT / 2) + 16 * i + fr;
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const int c = 2 * fq + h;
-                    wf[i][h] = *(const SPT_LDS f32x4*)(lw + rw * SLAB + ((c ^ swz(rw)) << 4));
+                    if (i < NJ) wf[i][h] = *(const SPT_LDS f32x4*)(lw + rw * SLAB + ((c ^ swz(rw)) << 4));
                     if (i < MI) {
                         const int ra = wm * (BMT / 2) + 16 * i + fr;
                         af[i][h] = *(const SPT_LDS f32x4*)(la + ra * SLAB + ((c ^ swz(ra)) << 4));
@@ -219,7 +221,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256,
 #pragma unroll
                 for (int i = 0; i < MI; ++i)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
+                    for (int j = 0; j < NJ; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s >> 2][s & 3], wf[j][s >> 2][s & 3],
                                                                           acc[i][j], 0, 0, 0);
         }
@@ -228,8 +230,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256,
 
     // ---------------------------------------------------------------- epilogue
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const EpiCol ec = epi_col<EPI>(g, n0 + wn * 64 + 16 * j + fr);
+    for (int j = 0; j < NJ; ++j) {
+        const EpiCol ec = epi_col<EPI>(g, n0 + wn * (BNT / 2) + 16 * j + fr);
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -634,18 +636,19 @@ void launch_t_st(const GemmArgs& g0, int batch, hipStream_t st) {
     hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, ST>), grid, dim3(256), lds, st, g);
 }
 
-template <typename T, int EPI>
-void launch_t64(const GemmArgs& g0, int batch, hipStream_t st) {  // 64 x 128 tile, 2-slot ring (48 KiB)
+template <typename T, int EPI, int BMT, int BNT>
+void launch_small(const GemmArgs& g0, int batch, hipStream_t st) {  // 64 x 128 / 64 x 64 tile, 2-slot ring
     static const int nmajor = getenv("SPT_GEMM_NT_RASTER") ? atoi(getenv("SPT_GEMM_NT_RASTER")) : 0;
     GemmArgs g = g0;
     g.nmajor = nmajor;
-    dim3 grid(cdiv(g.M, 64) * (g.N / BN), g.ksplit, batch);
-    hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, 2, 64>), grid, dim3(256), 2 * (64 + BN) * SLAB, st, g);
+    dim3 grid(cdiv(g.M, BMT) * (g.N / BNT), g.ksplit, batch);
+    hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, 2, BMT, BNT>), grid, dim3(256), 2 * (BMT + BNT) * SLAB, st, g);
 }
 
 template <typename T, int EPI>
 void launch_t(const GemmArgs& g, int batch, int variant, hipStream_t st) {
-    if (variant == 4) return launch_t64<T, EPI>(g, batch, st);
+    if (variant == 4) return launch_small<T, EPI, 64, 128>(g, batch, st);
+    if (variant == 5) return launch_small<T, EPI, 64, 64>(g, batch, st);
     switch (nt_stages()) {
         case 2: launch_t_st<T, EPI, 2>(g, batch, st); break;
         case 3: launch_t_st<T, EPI, 3>(g, batch, st); break;
@@ -698,7 +701,7 @@ void gemm_nt_variant(int dtype, int epi, const GemmArgs& g, int batch, int varia
     const int esz = dtype == DT_F32 ? 4 : 2;
     if (g.ksplit < 1 || g.K % g.ksplit || (g.ksplit > 1 && epi != EPI_PARTIAL))
         throw std::runtime_error("gemm_nt: split-K needs EPI_PARTIAL and K % ksplit == 0");
-    if (variant != 3 && (g.N % BN != 0 || (g.K / g.ksplit * esz) % SLAB != 0 || g.M <= 0))
+    if (variant != 3 && (g.N % (variant == 5 ? 64 : BN) != 0 || (g.K / g.ksplit * esz) % SLAB != 0 || g.M <= 0))
         throw std::runtime_error("gemm_nt: unsupported shape M=" + std::to_string(g.M) + " N=" +
                                  std::to_string(g.N) + " K=" + std::to_string(g.K));
 #define SPT_GEMM_CASES(T)                                                          \
@@ -746,11 +749,13 @@ void gemm_nt_variant(int dtype, int epi, const GemmArgs& g, int batch, int varia
     static const bool force128 = getenv("SPT_GEMM128") != nullptr;  // A/B switch for measurements
     if (variant == 0 && !force128 && dtype != DT_F32) {
         // automatic: the 256 x 256 tile from ~96 workgroups up; below that (a single Whisper
-        // window, M = 1500: 30 workgroups for the N = 1280 products) the 128 x 128 tile, or the
-        // 64 x 128 one while 128-row tiles would not fill the CUs once (all three bitwise equal)
+        // window, M = 1500: 30 workgroups for the N = 1280 products) the 128 x 128 tile, or while
+        // 128-row tiles would not fill the CUs once the 64 x 128 tile, or the 64 x 64 one below
+        // two 64 x 128 workgroups per CU (all bitwise equal; r3 exp_r3y)
         const int64_t t256 = (int64_t)cdiv(g.M, G2_BM) * (g.N / G2_BN) * g.ksplit * batch;
         const int64_t t128 = (int64_t)cdiv(g.M, BM) * (g.N / BN) * g.ksplit * batch;
-        if (g.N % G2_BN != 0 || t256 < 96) variant = t128 < 256 ? 4 : 1;
+        const int64_t t64 = (int64_t)cdiv(g.M, 64) * (g.N / BN) * g.ksplit * batch;
+        if (g.N % G2_BN != 0 || t256 < 96) variant = t128 >= 256 ? 1 : t64 >= 512 ? 4 : 5;
     }
     const bool use256 = variant == 2 || (variant == 0 && !force128);
     const bool fits32 = (int64_t)g.M * g.lda < (1ll << 31) && (int64_t)g.N * g.ldw < (1ll << 31);

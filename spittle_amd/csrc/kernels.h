@@ -40,6 +40,7 @@ void gemm_nt(int dtype, int epi, const GemmArgs& g, int batch, hipStream_t st);
 // variant 0: automatic (bf16 N % 256 == 0 -> 256 x 256 tile); 1: 128 x 128 tile; 2: prefer 256 x 256;
 // 3: skinny (M <= 64, 16-bit dtypes: 16 columns per workgroup, the weight stream spread over the grid)
 // 4: 64 x 128 tile (16-bit or f32; small M: two workgroups per CU where the 128-row tile gives one)
+// 5: 64 x 64 tile (N % 64; up to four workgroups per CU)
 // sets the > 64 KiB dynamic-LDS attribute of every GEMM kernel on the current device (engine
 // constructors call it before any stream capture; launches check it too)
 void gemm_prepare();

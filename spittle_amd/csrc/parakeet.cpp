@@ -476,12 +476,12 @@ void ParakeetEngine::run_mel(const float* pcm_dev, int64_t stride, int B, int Tp
 
 // GEMM tile choice: the 256 x 256 tile whenever at least ~96 of its workgroups are in flight
 // (its MFMA efficiency beats the 128 x 128 tile's even with part of the chip idle), else the
-// 128 x 128 tile, or the 64 x 128 tile where the 128 x 128 one would leave CUs without a second
-// workgroup (the C5 shape, M = 832: two waves per SIMD cover each other's LDS reads and slab
-// waits; r3 exp_r3v / exp_r3w: 19-35 % faster than either larger tile there, bitwise equal).
-// Residual products (EPI_PARTIAL, N = d) also split K over grid.y toward ~192 (256-tile) or ~512
-// (128-tile) workgroups, the 64-row tile keeping >= 8 K-steps per split; their f32 slabs are
-// summed, with the bias and the 1/2 FFN scale, by the LayerNorm that reads the residual next.
+// 128 x 128 tile, or the 64 x 128 / 64 x 64 tile where the 128 x 128 one would leave CUs without a
+// second workgroup (the C5 shape, M = 832: several waves per SIMD cover each other's LDS reads and
+// slab waits; r3 exp_r3v / exp_r3y: 20-45 % faster than the larger tiles there, bitwise equal).
+// Residual products (EPI_PARTIAL, N = d) also split K over grid.y toward ~192 (256-tile), ~512
+// (128 / 64 x 128) or ~1024 (64 x 64) workgroups, the small tiles keeping >= 8 K-steps per split;
+// their f32 slabs are summed, with the bias and the 1/2 FFN scale, by the next LayerNorm.
 // Returns the split used.
 int ParakeetEngine::gemm(int dt, int epi, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
                          const float* bias, void* Cp, int ldc, float alpha) {
@@ -505,13 +505,15 @@ int ParakeetEngine::gemm(int dt, int epi, const void* A, int lda, const void* W,
             while (k2 < 8 && t * k2 < 192 && K % (2 * k2) == 0 && (K / (2 * k2)) % 64 == 0 && K / (2 * k2) >= 256) k2 *= 2;
         if (t * k2 >= t256) { variant = 2; ks = k2; }
     }
-    if (variant == 1 && dt != DT_F32 && M > 64 && (int64_t)cdiv(M, 128) * (N / 128) < 256 && t64_ok) variant = 4;
+    if (variant == 1 && dt != DT_F32 && M > 64 && (int64_t)cdiv(M, 128) * (N / 128) < 256 && t64_ok)
+        variant = (int64_t)cdiv(M, 64) * (N / 128) >= 512 ? 4 : 5;
     if (variant == 1 && epi == EPI_PARTIAL) {
         const int64_t t = (int64_t)cdiv(M, 128) * (N / 128);
         while (ks < 8 && t * ks * 2 <= 512 && K % (2 * ks) == 0 && (K / (2 * ks)) % 64 == 0) ks *= 2;
-    } else if (variant == 4 && epi == EPI_PARTIAL) {
-        const int64_t t = (int64_t)cdiv(M, 64) * (N / 128);
-        while (ks < 8 && t * ks * 2 <= 512 && K % (2 * ks) == 0 && K / (2 * ks) >= 512 && (K / (2 * ks)) % 64 == 0) ks *= 2;
+    } else if ((variant == 4 || variant == 5) && epi == EPI_PARTIAL) {
+        const int64_t t = (int64_t)cdiv(M, 64) * (N / (variant == 4 ? 128 : 64));
+        const int64_t cap = variant == 4 ? 512 : 1024;
+        while (ks < 8 && t * ks * 2 <= cap && K % (2 * ks) == 0 && K / (2 * ks) >= 512 && (K / (2 * ks)) % 64 == 0) ks *= 2;
     }
     GemmArgs g{};
     g.A = A; g.lda = lda; g.W = W; g.ldw = ldw; g.M = M; g.N = N; g.K = K; g.bias = bias;

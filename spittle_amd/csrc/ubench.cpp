@@ -341,17 +341,21 @@ int main(int argc, char** argv) {
         if (epi == EPI_BIAS_GELU_POS) g.pos = frand((size_t)M * N, 4, 0);
         HIP_CHECK(hipDeviceSynchronize());  // inputs are generated on the null stream
         std::vector<char> ref(cbytes), out(cbytes);
-        double us[5] = {0, 0, 0, 0, 0};
-        std::vector<char> out64(cbytes);
-        for (int v : {1, 2, 4}) {
+        double us[6] = {0, 0, 0, 0, 0, 0};
+        std::vector<char> out64(cbytes), out6464(cbytes);
+        for (int v : {1, 2, 4, 5}) {
             HIP_CHECK(hipMemcpyAsync(C, C0, cbytes, hipMemcpyDeviceToDevice, st));
             gemm_nt_variant(dt, epi, g, 1, v, st);
             HIP_CHECK(hipStreamSynchronize(st));
-            HIP_CHECK(hipMemcpy(v == 1 ? ref.data() : v == 2 ? out.data() : out64.data(), C, cbytes, hipMemcpyDeviceToHost));
+            HIP_CHECK(hipMemcpy(v == 1 ? ref.data() : v == 2 ? out.data() : v == 4 ? out64.data() : out6464.data(), C, cbytes,
+                                hipMemcpyDeviceToHost));
             us[v] = time_us(st, 20, [&] { gemm_nt_variant(dt, epi, g, 1, v, st); });
         }
-        size_t diff64 = 0;
-        for (size_t i = 0; i < cbytes; ++i) diff64 += ref[i] != out64[i];
+        size_t diff64 = 0, diff6464 = 0;
+        for (size_t i = 0; i < cbytes; ++i) {
+            diff64 += ref[i] != out64[i];
+            diff6464 += ref[i] != out6464[i];
+        }
         size_t diff = 0, shown = 0;
         for (size_t i = 0; i < cbytes; ++i) {
             if (ref[i] == out[i]) continue;
@@ -366,8 +370,9 @@ int main(int argc, char** argv) {
         }
         const double fl = 2.0 * M * N * K;
         printf("gemm M=%d N=%d K=%d ks=%d epi=%d dt=%d : 128-tile %.2f us %.1f TF/s | 256-tile %.2f us %.1f TF/s | bytes differing %zu"
-               " | 64x128 %.2f us %.1f TF/s, bytes differing from 128-tile %zu\n",
-               M, N, K, ks, epi, dt, us[1], fl / us[1] / 1e6, us[2], fl / us[2] / 1e6, diff, us[4], fl / us[4] / 1e6, diff64);
+               " | 64x128 %.2f us %.1f TF/s, bytes differing from 128-tile %zu | 64x64 %.2f us, differing %zu\n",
+               M, N, K, ks, epi, dt, us[1], fl / us[1] / 1e6, us[2], fl / us[2] / 1e6, diff, us[4], fl / us[4] / 1e6, diff64,
+               us[5], diff6464);
         return 0;
     }
     if (what == "layer" || what == "layer2") {
