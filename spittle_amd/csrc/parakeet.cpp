@@ -474,13 +474,13 @@ void ParakeetEngine::run_mel(const float* pcm_dev, int64_t stride, int B, int Tp
     pk_mel_norm(mel_, lens_, B, Tp, dm_.n_mels, st_);
 }
 
-// GEMM tile choice: the 256 x 256 tile whenever at least ~96 of its workgroups are in flight
-// (its MFMA efficiency beats the 128 x 128 tile's even with part of the chip idle), else the
-// 128 x 128 tile, or the 64 x 128 / 64 x 64 tile where the 128 x 128 one would leave CUs without a
-// second workgroup (the C5 shape, M = 832: several waves per SIMD cover each other's LDS reads and
-// slab waits; r3 exp_r3v / exp_r3y: 20-45 % faster than the larger tiles there, bitwise equal).
+// GEMM tile choice: the 256 x 256 tile whenever at least ~128 of its workgroups are in flight
+// (its MFMA efficiency beats the smaller tiles' even with part of the chip idle), else the 64 x 128
+// tile from two workgroups per CU up, else the 64 x 64 one (several waves per SIMD cover each
+// other's LDS reads and slab waits; r3 exp_r3v / exp_r3y / exp_r3z: 20-45 % faster than the
+// 128 x 128 tile at M = 832 and M = 3000, bitwise equal; the 128 x 128 tile stays for f32).
 // Residual products (EPI_PARTIAL, N = d) also split K over grid.y toward ~192 (256-tile), ~512
-// (128 / 64 x 128) or ~1024 (64 x 64) workgroups, the small tiles keeping >= 8 K-steps per split;
+// (128 / 64 x 128) or ~1024 (64 x 64) workgroups, keeping >= 8 K-steps per split;
 // their f32 slabs are summed, with the bias and the 1/2 FFN scale, by the next LayerNorm.
 // Returns the split used.
 int ParakeetEngine::gemm(int dt, int epi, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
@@ -488,7 +488,7 @@ int ParakeetEngine::gemm(int dt, int epi, const void* A, int lda, const void* W,
     // SPT_GEMM_T256 / SPT_GEMM_T64 / SPT_NO_SKINNY: read per call so tests can pin each variant
     // (eager calls only: a captured encoder graph keeps the variants it was captured with)
     const char* t256e = getenv("SPT_GEMM_T256");
-    const int t256 = t256e ? atoi(t256e) : 96;
+    const int t256 = t256e ? atoi(t256e) : 128;
     const char* t64e = getenv("SPT_GEMM_T64");
     const bool t64_ok = !(t64e && atoi(t64e) == 0);
     const bool no_skinny = getenv("SPT_NO_SKINNY") != nullptr;
@@ -502,11 +502,10 @@ int ParakeetEngine::gemm(int dt, int epi, const void* A, int lda, const void* W,
         const int64_t t = (int64_t)cdiv(M, 256) * (N / 256);
         int k2 = 1;
         if (epi == EPI_PARTIAL)
-            while (k2 < 8 && t * k2 < 192 && K % (2 * k2) == 0 && (K / (2 * k2)) % 64 == 0 && K / (2 * k2) >= 256) k2 *= 2;
+            while (k2 < 8 && t * k2 < 192 && K % (2 * k2) == 0 && (K / (2 * k2)) % 64 == 0 && K / (2 * k2) >= 512) k2 *= 2;
         if (t * k2 >= t256) { variant = 2; ks = k2; }
     }
-    if (variant == 1 && dt != DT_F32 && M > 64 && (int64_t)cdiv(M, 128) * (N / 128) < 256 && t64_ok)
-        variant = (int64_t)cdiv(M, 64) * (N / 128) >= 512 ? 4 : 5;
+    if (variant == 1 && dt != DT_F32 && M > 64 && t64_ok) variant = (int64_t)cdiv(M, 64) * (N / 128) >= 512 ? 4 : 5;
     if (variant == 1 && epi == EPI_PARTIAL) {
         const int64_t t = (int64_t)cdiv(M, 128) * (N / 128);
         while (ks < 8 && t * ks * 2 <= 512 && K % (2 * ks) == 0 && (K / (2 * ks)) % 64 == 0) ks *= 2;
