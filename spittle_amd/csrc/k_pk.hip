@@ -324,32 +324,39 @@ __global__ __launch_bounds__(64) void rel_attn_mfma_kernel(const f16* __restrict
             const int key = min(j0 + c / (DK / 8), Tp - 1);
             vreg[u] = *(const u32x4*)(base + (size_t)key * ld + 2 * d + h * DK + 8 * (c % (DK / 8)));
         }
-        // S^T = K . QU^T
-        f32x16 sc;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sc[r] = 0.0f;
+        // the tile's K rows and relative-position rows, all issued before the first product: loads
+        // written inside the MFMA loop were each issued just before their MFMA and waited with
+        // vmcnt(0), one dependent round trip per 16-wide slice (r3)
+        f16x8 kf[NS], pf0[NS], pf1[NS];
         {
             const f16* kp = base + (size_t)min(j0 + l32, Tp - 1) * ld + d + h * DK + 8 * hf;
-#pragma unroll
-            for (int s = 0; s < NS; ++s)
-                sc = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const f16x8*)(kp + 16 * s), qu[s], sc, 0, 0, 0);
-        }
-        // G^T = P[r0 ..] . QV^T (two 32-row halves)
-        f32x16 g0, g1;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) { g0[r] = 0.0f; g1[r] = 0.0f; }
-        {
             const int r0 = (Tp - 1) + j0 - i0 - 31;
             const int pr0 = min(max(r0 + l32, 0), 2 * Tp - 2), pr1 = min(max(r0 + 32 + l32, 0), 2 * Tp - 2);
             const f16* p0 = p + (size_t)pr0 * ldp + h * DK + 8 * hf;
             const f16* p1 = p + (size_t)pr1 * ldp + h * DK + 8 * hf;
 #pragma unroll
             for (int s = 0; s < NS; ++s) {
-                g0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const f16x8*)(p0 + 16 * s), qv[s], g0, 0, 0, 0);
-                g1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const f16x8*)(p1 + 16 * s), qv[s], g1, 0, 0, 0);
+                kf[s] = *(const f16x8*)(kp + 16 * s);
+                pf0[s] = *(const f16x8*)(p0 + 16 * s);
+                pf1[s] = *(const f16x8*)(p1 + 16 * s);
             }
         }
-        __syncthreads();  // the previous tile's LDS reads are done
+        __builtin_amdgcn_sched_barrier(0);  // keep the scheduler from sinking the loads to their MFMAs
+        // S^T = K . QU^T, G^T = P[r0 ..] . QV^T (two 32-row halves)
+        f32x16 sc, g0, g1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { sc[r] = 0.0f; g0[r] = 0.0f; g1[r] = 0.0f; }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) sc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[s], qu[s], sc, 0, 0, 0);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            g0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(pf0[s], qv[s], g0, 0, 0, 0);
+            g1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(pf1[s], qv[s], g1, 0, 0, 0);
+        }
+        // one wave: the LDS hand-offs need only its own lgkmcnt waits.  __syncthreads() is also a
+        // release fence, and hipcc drained the tile's in-flight loads (vmcnt(0)) at each one
+        // (r3: 69 -> 55 us per offline layer without them)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous tile's LDS reads are done
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int row = (r & 3) + 8 * (r >> 2) + 4 * hf;
@@ -358,7 +365,8 @@ __global__ __launch_bounds__(64) void rel_attn_mfma_kernel(const f16* __restrict
         }
 #pragma unroll
         for (int u = 0; u < DK / 16; ++u) *(SPT_LDS u32x4*)(lv + (lane + 64 * u) * 16) = vreg[u];
-        __syncthreads();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
         float mloc = -INFINITY;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
