@@ -1,4 +1,4 @@
-# r3 s2: Parakeet relative attention, one wave: wave-local LDS sync (no __syncthreads drain) and the
+# r3 s2: Parakeet relative attention (wave-local LDS sync, tile loads before products, then one tile ahead) and the block-boundary LayerNorm pair fused: parity, then the Parakeet lines
 # tile's K / position rows issued before its products (sched_barrier): parity, then the Parakeet lines
 export TMPDIR=/tmp
 mkdir -p gpurun_out
