@@ -1,4 +1,4 @@
-# r3 s2: Parakeet relative attention (wave-local LDS sync, tile loads before products, then one tile ahead) and the block-boundary LayerNorm pair fused: parity, then the Parakeet lines
+# r3 s2: Parakeet block-boundary LayerNorm pair fused (ln_pend2_kernel); earlier runs of this script: relative attention variants (wave-local sync + loads before products kept; one-tile-ahead prefetch measured slower, 0.96 -> 1.27 ms offline, dropped)
 # tile's K / position rows issued before its products (sched_barrier): parity, then the Parakeet lines
 export TMPDIR=/tmp
 mkdir -p gpurun_out

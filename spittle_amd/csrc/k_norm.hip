@@ -163,6 +163,121 @@ __global__ __launch_bounds__(256) void ln_pend_kernel(float* __restrict__ x, int
     }
 }
 
+// ln_pend_kernel (f32 output, x not written back) followed by a second LayerNorm of its output row,
+// still in registers: the Parakeet layer boundary (the block's output LayerNorm, then the next
+// block's first).  Both results are bitwise those of ln_pend_kernel + ln_kernel (the second LN
+// sums the f32 row it would have read back, in the same lane order).
+template <typename T2, int NV, int KS>
+__global__ __launch_bounds__(256) void ln_pend2_kernel(const float* __restrict__ x, int M, int d,
+                                                       const float* __restrict__ slab, int64_t sst,
+                                                       const float* __restrict__ pbias, float alpha,
+                                                       const float* __restrict__ w, const float* __restrict__ bb,
+                                                       float* __restrict__ y, const float* __restrict__ w2,
+                                                       const float* __restrict__ b2, T2* __restrict__ y2) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const int n4 = d >> 2;
+    const float4* xr = (const float4*)(x + (size_t)row * d);
+    float4 v[NV], g[NV], o[NV], g2[NV], o2[NV], u[NV][KS], x0[NV], pb[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int idx = min(lane + 64 * i, n4 - 1);
+#pragma unroll
+        for (int q = 0; q < KS; ++q) u[i][q] = *(const float4*)(slab + q * sst + (size_t)row * d + 4 * idx);
+        x0[i] = xr[idx];
+        pb[i] = ((const float4*)pbias)[idx];
+        g[i] = ((const float4*)w)[idx];
+        o[i] = ((const float4*)bb)[idx];
+        g2[i] = ((const float4*)w2)[idx];
+        o2[i] = ((const float4*)b2)[idx];
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        float4 p = u[i][0];
+#pragma unroll
+        for (int q = 1; q < KS; ++q) {
+            p.x += u[i][q].x; p.y += u[i][q].y; p.z += u[i][q].z; p.w += u[i][q].w;
+        }
+        if (lane + 64 * i < n4) {
+            v[i] = make_float4(x0[i].x + alpha * (p.x + pb[i].x), x0[i].y + alpha * (p.y + pb[i].y),
+                               x0[i].z + alpha * (p.z + pb[i].z), x0[i].w + alpha * (p.w + pb[i].w));
+            s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+        } else {
+            v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+    float mean = wave_sum(s) / (float)d;
+    float s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        if (lane + 64 * i < n4) {
+            const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, e = v[i].w - mean;
+            s2 += (a * a + b * b) + (c * c + e * e);
+        }
+    }
+    float rstd = 1.0f / sqrtf(wave_sum(s2) / (float)d + 1e-5f);
+    float* yr = y + (size_t)row * d;
+    s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int idx = lane + 64 * i;
+        if (idx < n4) {
+            v[i] = make_float4((v[i].x - mean) * rstd * g[i].x + o[i].x, (v[i].y - mean) * rstd * g[i].y + o[i].y,
+                               (v[i].z - mean) * rstd * g[i].z + o[i].z, (v[i].w - mean) * rstd * g[i].w + o[i].w);
+            *(float4*)(yr + 4 * idx) = v[i];
+        } else {
+            v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    }
+    mean = wave_sum(s) / (float)d;
+    s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        if (lane + 64 * i < n4) {
+            const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, e = v[i].w - mean;
+            s2 += (a * a + b * b) + (c * c + e * e);
+        }
+    }
+    rstd = 1.0f / sqrtf(wave_sum(s2) / (float)d + 1e-5f);
+    T2* y2r = y2 + (size_t)row * d;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int idx = lane + 64 * i;
+        if (idx < n4)
+            store4<T2>(y2r + 4 * idx, (v[i].x - mean) * rstd * g2[i].x + o2[i].x, (v[i].y - mean) * rstd * g2[i].y + o2[i].y,
+                       (v[i].z - mean) * rstd * g2[i].z + o2[i].z, (v[i].w - mean) * rstd * g2[i].w + o2[i].w);
+    }
+}
+
+template <typename T2, int NV>
+void ln_pend2_nv(dim3 grid, const float* x, int M, int d, const float* slab, int ks, int64_t sst, const float* pb,
+                 float alpha, const float* w, const float* b, float* y, const float* w2, const float* b2, T2* y2,
+                 hipStream_t st) {
+    switch (ks) {
+        case 1: hipLaunchKernelGGL((ln_pend2_kernel<T2, NV, 1>), grid, dim3(256), 0, st, x, M, d, slab, sst, pb, alpha, w, b, y, w2, b2, y2); break;
+        case 2: hipLaunchKernelGGL((ln_pend2_kernel<T2, NV, 2>), grid, dim3(256), 0, st, x, M, d, slab, sst, pb, alpha, w, b, y, w2, b2, y2); break;
+        case 4: hipLaunchKernelGGL((ln_pend2_kernel<T2, NV, 4>), grid, dim3(256), 0, st, x, M, d, slab, sst, pb, alpha, w, b, y, w2, b2, y2); break;
+        case 8: hipLaunchKernelGGL((ln_pend2_kernel<T2, NV, 8>), grid, dim3(256), 0, st, x, M, d, slab, sst, pb, alpha, w, b, y, w2, b2, y2); break;
+        default: throw std::runtime_error("layernorm_pend2: split count must be 1, 2, 4 or 8");
+    }
+}
+
+template <typename T2>
+void ln_pend2_dispatch(const float* x, int M, int d, const float* slab, int ks, int64_t sst, const float* pb, float alpha,
+                       const float* w, const float* b, float* y, const float* w2, const float* b2, T2* y2, hipStream_t st) {
+    dim3 grid(cdiv(M, 4));
+    switch (cdiv(d, 256)) {
+        case 1: ln_pend2_nv<T2, 1>(grid, x, M, d, slab, ks, sst, pb, alpha, w, b, y, w2, b2, y2, st); break;
+        case 2: ln_pend2_nv<T2, 2>(grid, x, M, d, slab, ks, sst, pb, alpha, w, b, y, w2, b2, y2, st); break;
+        case 3: ln_pend2_nv<T2, 3>(grid, x, M, d, slab, ks, sst, pb, alpha, w, b, y, w2, b2, y2, st); break;
+        case 4: ln_pend2_nv<T2, 4>(grid, x, M, d, slab, ks, sst, pb, alpha, w, b, y, w2, b2, y2, st); break;
+        default: throw std::runtime_error("layernorm_pend2: d too large");
+    }
+}
+
 template <typename T, int NV>
 void ln_pend_nv(dim3 grid, float* x, int M, int d, const float* slab, int ks, int64_t sst, const float* pb, float alpha,
                 const float* w, const float* b, T* y, int wx, hipStream_t st) {
@@ -227,6 +342,16 @@ void layernorm_pend(int dtype, float* x, int M, int d, const float* slab, int ks
     if (dtype == DT_BF16) ln_pend_dispatch<bf16>(x, M, d, slab, ks, slab_stride, pbias, alpha, w, b, (bf16*)y, write_x, st);
     else if (dtype == DT_F16) ln_pend_dispatch<f16>(x, M, d, slab, ks, slab_stride, pbias, alpha, w, b, (f16*)y, write_x, st);
     else ln_pend_dispatch<float>(x, M, d, slab, ks, slab_stride, pbias, alpha, w, b, (float*)y, write_x, st);
+    SPT_LAUNCH_CHECK();
+}
+
+void layernorm_pend2(int dtype2, const float* x, int M, int d, const float* slab, int ks, int64_t slab_stride,
+                     const float* pbias, float alpha, const float* w, const float* b, float* y, const float* w2,
+                     const float* b2, void* y2, hipStream_t st) {
+    if (d % 4) throw std::runtime_error("layernorm_pend2: d % 4");
+    if (dtype2 == DT_BF16) ln_pend2_dispatch<bf16>(x, M, d, slab, ks, slab_stride, pbias, alpha, w, b, y, w2, b2, (bf16*)y2, st);
+    else if (dtype2 == DT_F16) ln_pend2_dispatch<f16>(x, M, d, slab, ks, slab_stride, pbias, alpha, w, b, y, w2, b2, (f16*)y2, st);
+    else ln_pend2_dispatch<float>(x, M, d, slab, ks, slab_stride, pbias, alpha, w, b, y, w2, b2, (float*)y2, st);
     SPT_LAUNCH_CHECK();
 }
 

@@ -92,6 +92,11 @@ void layernorm(int dtype, const float* x, int M, int d, const float* w, const fl
 void layernorm_pend(int dtype, float* x, int M, int d, const float* slab, int ks, int64_t slab_stride,
                     const float* pbias, float alpha, const float* w, const float* b, void* y, bool write_x,
                     hipStream_t st);
+// layernorm_pend with the f32 result y (x not written back) normalised once more into y2 (w2, b2;
+// dtype2): the Parakeet block boundary in one launch, bitwise the two-launch result
+void layernorm_pend2(int dtype2, const float* x, int M, int d, const float* slab, int ks, int64_t slab_stride,
+                     const float* pbias, float alpha, const float* w, const float* b, float* y, const float* w2,
+                     const float* b2, void* y2, hipStream_t st);
 // convert an activation buffer to f32 (debug / tests)
 void to_f32(int dtype, const void* src, float* dst, int64_t n, hipStream_t st);
 

@@ -543,9 +543,12 @@ void ParakeetEngine::run_encoder(int B, int Tp, int T1p, int T2p, int T3p) {
     int ks;
     for (int l = 0; l < Ln; ++l) {
         const Layer& y = L_[l];
-        // 1/2 FFN; its product stays pending in the slabs until the next LayerNorm
-        layernorm(dt_, x, M, d, y.ln1_w, y.ln1_b, xn_, st_);
-        mark(PK_ST_LN);
+        // 1/2 FFN; its product stays pending in the slabs until the next LayerNorm (the first
+        // block's input LayerNorm here, the others' in the previous block's output LayerNorm)
+        if (l == 0) {
+            layernorm(dt_, x, M, d, y.ln1_w, y.ln1_b, xn_, st_);
+            mark(PK_ST_LN);
+        }
         gemm(dt_, EPI_BIAS_SWISH, xn_, d, y.ff1_w1, d, M, ff, d, y.ff1_b1, ffh_, ff);
         ks = gemm(dt_, EPI_PARTIAL, ffh_, ff, y.ff1_w2, ff, M, d, ff, nullptr, slab_, d);
         mark(PK_ST_FFN);
@@ -574,8 +577,13 @@ void ParakeetEngine::run_encoder(int B, int Tp, int T1p, int T2p, int T3p) {
         gemm(dt_, EPI_BIAS_SWISH, xn_, d, y.ff2_w1, d, M, ff, d, y.ff2_b1, ffh_, ff);
         ks = gemm(dt_, EPI_PARTIAL, ffh_, ff, y.ff2_w2, ff, M, d, ff, nullptr, slab_, d);
         mark(PK_ST_FFN);
-        // LayerNorm out (f32) of x + the pending 1/2 FFN into the other residual buffer
-        layernorm_pend(DT_F32, x, M, d, slab_, ks, sst, y.ff2_b2, 0.5f, y.lno_w, y.lno_b, x2, false, st_);
+        // LayerNorm out (f32) of x + the pending 1/2 FFN into the other residual buffer, and with
+        // it the next block's input LayerNorm
+        if (l + 1 < Ln)
+            layernorm_pend2(dt_, x, M, d, slab_, ks, sst, y.ff2_b2, 0.5f, y.lno_w, y.lno_b, x2, L_[l + 1].ln1_w,
+                            L_[l + 1].ln1_b, xn_, st_);
+        else
+            layernorm_pend(DT_F32, x, M, d, slab_, ks, sst, y.ff2_b2, 0.5f, y.lno_w, y.lno_b, x2, false, st_);
         mark(PK_ST_LN);
         std::swap(x, x2);
     }
