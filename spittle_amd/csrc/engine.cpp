@@ -97,7 +97,6 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     cp_ = ((dm_.n_mels + 63) / 64) * 64;
     if ((3 * cp_ * esz_) % 128) cp_ = ((dm_.n_mels + 127) / 128) * 128;
     if (const char* g = getenv("SPT_DECODE_GROUPS")) n_groups_ = std::max(1, std::min(4, atoi(g)));
-    if (const char* v = getenv("SPT_FUSED_QKV")) fused_qkv_ = atoi(v) != 0;
     if (const char* v = getenv("SPT_XATTN_SPLIT")) xsplit_ = std::max(1, std::min(4, atoi(v)));
     // cross-attention key split: fixed per engine (never per batch).  The fc2 K split (2; r1
     // exp14 measured 2 slightly faster per layer than 4: the next QKV LayerNorm prologue sums
@@ -735,13 +734,8 @@ float* Engine::enqueue_layers(DecGroup& g, int B_total, int Tq) {
         void* skv_l = (char*)g.skv + self_layer * l * esz_;
         // this group's sequences inside the cross K/V of layer l (kv_offset layout, B_total sequences)
         const void* ckv_l = (const char*)ckv_ + (cross_layer * l + (int64_t)g.b0 * H * 4096) * esz_;
-        // LN1 + QKV projection + self K/V append (+ the self-attention, fused for decode steps)
-        if (fused_qkv_ && Tq == 1 && dec_qkv_attn_supported(dt_, d)) {
-            const float* pend[2] = {g.pend, g.pend + (int64_t)R * d};
-            dec_qkv_attn(xc, pend, np, np > 0 ? xo : nullptr, e.ln1_w, e.ln1_b, e.qkv_w, e.qkv_b, skv_l, B, H,
-                         ctx, g.ds, g.dao, st);
-            consumed();
-        } else {
+        // LN1 + QKV projection + self K/V append, then the self-attention
+        {
             GemvArgs a{};
             ln_input(a); a.lda = d; a.ln_w = e.ln1_w; a.ln_b = e.ln1_b; a.R = R;
             a.W = e.qkv_w; a.N = 3 * d; a.K = d; a.bias = e.qkv_b; a.C = g.dq; a.ldc = d;

@@ -190,7 +190,6 @@ private:
     int cp_;      // padded mel channels (conv1 K = 3 * cp_)
     static constexpr int fc2_split_ = 2;  // K split of the fc2 projection (pending slabs)
     int xsplit_ = 1;  // cross-attention key chunks per (b, h) (merged by the output projection)
-    bool fused_qkv_ = false;  // SPT_FUSED_QKV=1: decode-step LN1 + QKV + self-attention in one launch (r2: slower)
     int n_groups_ = 1;
     int max_rows_ = 64;  // decoder rows per pass (gemv_max_image_rows); larger batches use more groups  // SPT_DECODE_GROUPS=2 splits the batch over two streams
     hipStream_t st_ = nullptr;

@@ -760,209 +760,6 @@ __global__ __launch_bounds__(64 * AW) void self_attn_kernel(const T* __restrict_
     }
 }
 
-// ------------------------------------------------------------------ fused decode-step QKV + self-attention
-// One decode step (Tq = 1) of LN1 + QKV projection + self K/V append + self-attention, one
-// workgroup per (b, h): the workgroup projects only head h's 192 columns (q, k, v) of its own
-// row, so the attention that follows needs nothing from another workgroup and the launch
-// boundary between the QKV GEMV and self_attn_kernel disappears.  Head h's weights (3 x 64 rows
-// of d) are read by the B workgroups of that head; the block -> (h, b) map keeps them on one or
-// two XCDs so the re-reads are L2 hits.
-//
-// Measured slower on MI355X (r2, profiles/r2/exp_fused_qkv_attn.txt: decode pass 1.807 -> 2.006 ms):
-// each workgroup streams all 491 KB of its head's weights through one CU (160 KB in flight), so the
-// workgroup takes ~21 us against 15 us for the two launches it replaces.  Off by default
-// (SPT_FUSED_QKV=1 selects it).
-//
-// The arithmetic is the GEMV's and self_attn_kernel's, operation for operation, so the result is
-// bitwise the unfused path's (tests/test_gpu_fused_qkv.py):
-//   * the LayerNorm of row b is gemv_kernel's A_LN prologue (one wave, same lane order);
-//   * each (16-column tile, 128-K super-step) unit is the same 4 MFMAs from a zero accumulator,
-//     with the row in MFMA row 0 (an MFMA output element depends only on its own row and
-//     column); the NSS unit results of a tile are summed in super-step order, then the bias:
-//     the EXACT 10-wave GEMV's cross-wave reduction;
-//   * the attention is self_attn_kernel<bf16, 1> with the same 8 waves.
-struct QkvAttnArgs {
-    const float* x; const float* pend[4]; float* x_out;  // residual rows [B][d] (+ pending slabs)
-    const float* ln_w; const float* ln_b;
-    const bf16* W; const float* bias;                     // W [3d][d], bias [3d]
-    bf16* cache; int B, H, ctx;                           // [2][B][H][ctx][64]
-    const DecState* ds;
-    bf16* out;                                            // attention output [B][d]
-};
-constexpr int QA_RING = 5;  // weight units in flight per wave (4 KB per wave each)
-
-template <int NP, int NSS>
-__global__ __launch_bounds__(64 * AW) void qkv_attn_kernel(QkvAttnArgs a) {
-    constexpr int K = NSS * 128, KS = 128, CPE = 8;
-    constexpr int NU = 12 * NSS;               // (tile, super-step) units: 12 tiles of 16 columns
-    constexpr int UJ = (NU + AW - 1) / AW;     // units per wave
-    constexpr int LDS_LD = K + CPE;
-    __shared__ __attribute__((aligned(16))) bf16 s_img[LDS_LD];
-    __shared__ float s_part[NU][16];
-    __shared__ bf16 s_q[64];
-    __shared__ float s_m[AW][1], s_l[AW][1];
-    __shared__ float s_o[AW][1][64];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int fr = lane & 15, fq = lane >> 4;
-    const int B = a.B, H = a.H, nblk = B * H;
-    // blocks land on XCD blockIdx % 8: give XCD x the consecutive pairs p = h * B + b of one
-    // slice, so a head's B workgroups share an L2
-    const int p = (nblk & 7) ? (int)blockIdx.x : ((int)blockIdx.x & 7) * (nblk >> 3) + ((int)blockIdx.x >> 3);
-    const int h = p / B, b = p - h * B;
-    const int d = H * 64;
-
-    // LayerNorm row, prefetched operands: exactly gemv_kernel's A_LN order (row first, then LN params)
-    float4 x0[NP + 1][6];
-    float4 lnw_pre[6], lnb_pre[6];
-    if (wid == 0) {
-        const size_t ro = (size_t)b * d;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            const int k = lane * 4 + 256 * i;
-            if (k < K) {
-                x0[0][i] = *(const float4*)(a.x + ro + k);
-#pragma unroll
-                for (int q = 0; q < NP; ++q) x0[q + 1][i] = *(const float4*)(a.pend[q] + ro + k);
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            const int k = lane * 4 + 256 * i;
-            if (k < K) {
-                lnw_pre[i] = *(const float4*)(a.ln_w + k);
-                lnb_pre[i] = *(const float4*)(a.ln_b + k);
-            }
-        }
-    }
-    const int pos0 = a.ds->pos0;
-    // the epilogue's bias, fetched up front like the GEMV's
-    float bias_pre = 0.f;
-    if (tid < 192) bias_pre = a.bias[(tid >> 6) * d + h * 64 + (tid & 63)];
-    // weight units u = wid + AW * j: tile u / NSS (q0..q3, k0..k3, v0..v3), super-step u % NSS;
-    // loads are unconditional (clamped to the last unit) so the waits stay counted
-    auto wptr = [&](int j) {
-        const int u = min(wid + AW * j, NU - 1);
-        const int t = u / NSS, ss = u - t * NSS;
-        const int n = (t >> 2) * d + h * 64 + (t & 3) * 16 + fr;
-        return a.W + (size_t)n * K + ss * KS + fq * CPE;
-    };
-    bf16x8 w[QA_RING][4];
-#pragma unroll
-    for (int j = 0; j < QA_RING; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) w[j][i] = *(const bf16x8*)(wptr(j) + i * 4 * CPE);
-    // the attention's first key block streams in now when it holds only cached keys (< pos0);
-    // the block holding the new key pos0 is loaded after the append
-    const int g = lane & 7;
-    AttnWave<bf16, 1> aw;
-    aw.init(a.cache + (((size_t)0 * B + b) * H + h) * (size_t)a.ctx * 64 + 8 * g,
-            a.cache + (((size_t)1 * B + b) * H + h) * (size_t)a.ctx * 64 + 8 * g, max(pos0, 1), lane);
-    aw.load_blk(aw.kA, aw.vA, wid);
-    const bool first_loaded = (wid + 1) * AttnWave<bf16, 1>::KB <= pos0;
-
-    if (wid == 0) {
-        const bool wr_x = a.x_out && h == 0;
-        const size_t ro = (size_t)b * d;
-        float4 v[6];
-        float s = 0.f;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            const int k = lane * 4 + 256 * i;
-            if (k < K) {
-                v[i] = x0[0][i];
-#pragma unroll
-                for (int q = 1; q <= NP; ++q) {
-                    v[i].x += x0[q][i].x; v[i].y += x0[q][i].y; v[i].z += x0[q][i].z; v[i].w += x0[q][i].w;
-                }
-                if (wr_x) *(float4*)(a.x_out + ro + k) = v[i];
-                s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
-            }
-        }
-        const float mean = wave_sum(s) / (float)K;
-        float s2 = 0.f;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            const int k = lane * 4 + 256 * i;
-            if (k < K) {
-                const float p0 = v[i].x - mean, q0 = v[i].y - mean, u0 = v[i].z - mean, w0 = v[i].w - mean;
-                s2 += (p0 * p0 + q0 * q0) + (u0 * u0 + w0 * w0);
-            }
-        }
-        const float rstd = 1.0f / sqrtf(wave_sum(s2) / (float)K + 1e-5f);
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            const int k = lane * 4 + 256 * i;
-            if (k < K) {
-                const float4 g = lnw_pre[i];
-                const float4 bb = lnb_pre[i];
-                bf16* o = s_img + k;
-                o[0] = from_f<bf16>((v[i].x - mean) * rstd * g.x + bb.x);
-                o[1] = from_f<bf16>((v[i].y - mean) * rstd * g.y + bb.y);
-                o[2] = from_f<bf16>((v[i].z - mean) * rstd * g.z + bb.z);
-                o[3] = from_f<bf16>((v[i].w - mean) * rstd * g.w + bb.w);
-            }
-        }
-    }
-    __syncthreads();
-
-    // units: 4 MFMAs each from zero; MFMA row 0 is the LayerNorm row, rows 1..15 zero
-#pragma unroll
-    for (int j = 0; j < UJ; ++j) {
-        const int u = wid + AW * j;
-        const int ss = (min(u, NU - 1)) % NSS;
-        bf16x8 af[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            af[i] = fr == 0 ? *(const bf16x8*)(s_img + ss * KS + fq * CPE + i * 4 * CPE) : bf16x8{};
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], w[j % QA_RING][i], acc, 0, 0, 0);
-        if (j + QA_RING < UJ) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) w[j % QA_RING][i] = *(const bf16x8*)(wptr(j + QA_RING) + i * 4 * CPE);
-        }
-        if (u < NU && fq == 0) s_part[u][fr] = acc[0];  // row 0 = 4 * fq + 0
-    }
-    __syncthreads();
-
-    // epilogue: column c of head h's q | k | v; tile sums in super-step order, then the bias
-    if (tid < 192) {
-        const int t = tid >> 4, c = tid & 15;
-        float v = s_part[t * NSS][c];
-#pragma unroll
-        for (int s = 1; s < NSS; ++s) v += s_part[t * NSS + s][c];
-        const int part = t >> 2, e = (t & 3) * 16 + c;
-        const float y = v + bias_pre;
-        const bf16 yb = from_f<bf16>(y);
-        if (part == 0) {
-            s_q[e] = yb;
-        } else {
-            const size_t off = ((((size_t)(part - 1) * B + b) * H + h) * a.ctx + pos0) * 64 + e;
-            a.cache[off] = yb;
-        }
-    }
-    // the appended key / value row is read back below by other waves of this workgroup: the
-    // barrier's workgroup-scope release / acquire suffices (one L1; an agent-scope fence here
-    // would write back and invalidate the L2 that holds the head's shared weights)
-    __syncthreads();
-
-    // self_attn_kernel<bf16, 1> for (b, h)
-    const int n_keys = pos0 + 1;
-    aw.n_keys = n_keys;
-    float qv[1][8];
-    int lim[1] = {pos0 + 1};
-#pragma unroll
-    for (int e = 0; e < 8; ++e) qv[0][e] = to_f<bf16>(s_q[8 * g + e]) * kLog2Scale;
-    aw.run(wid, cdiv(n_keys, AttnWave<bf16, 1>::KB), first_loaded, qv, lim, 1);
-    aw.to_lds(s_m, s_l, s_o, wid, lane);
-    __syncthreads();
-    if (tid < 64) {
-        float M, L, O;
-        attn_merge<1>(s_m, s_l, s_o, 0, tid, M, L, O);
-        a.out[(size_t)b * d + h * 64 + tid] = from_f<bf16>(O / L);
-    }
-}
-
 // Cross-attention over the cached encoder K/V (all T_enc keys), one workgroup per (b, h).
 // kv: [2][B_layout][H][T_enc][64] at the group's first sequence.  (A fused LayerNorm + cross-Q
 // projection prologue and key-chunk splits were measured slower on MI355X: r1
@@ -1151,26 +948,6 @@ void dec_self_attn(int dtype, const void* q, const void* cache, int B, int H, in
         if (Tq == 1) SPT_SA(float, 1); else SPT_SA(float, 4);
     }
 #undef SPT_SA
-    SPT_LAUNCH_CHECK();
-}
-
-bool dec_qkv_attn_supported(int dtype, int d) { return dtype == DT_BF16 && d == 1280; }
-
-void dec_qkv_attn(const float* x, const float* const* pend, int n_pend, float* x_out, const float* ln_w,
-                  const float* ln_b, const void* W, const float* bias, void* cache, int B, int H, int ctx,
-                  const DecState* ds, void* out, hipStream_t st) {
-    if (H * 64 != 1280) throw std::runtime_error("dec_qkv_attn: d = 1280 (10 super-steps) only");
-    if (n_pend != 0 && n_pend != 2) throw std::runtime_error("dec_qkv_attn: 0 or 2 pending slabs");
-    if (B < 1 || !x || !ln_w || !ln_b || !W || !bias || !cache || !ds || !out || (n_pend && (!pend[0] || !pend[1])))
-        throw std::runtime_error("dec_qkv_attn: bad arguments");
-    QkvAttnArgs a{};
-    a.x = x;
-    for (int p = 0; p < 4; ++p) a.pend[p] = p < n_pend ? pend[p] : nullptr;
-    a.x_out = x_out; a.ln_w = ln_w; a.ln_b = ln_b;
-    a.W = (const bf16*)W; a.bias = bias; a.cache = (bf16*)cache; a.B = B; a.H = H; a.ctx = ctx; a.ds = ds;
-    a.out = (bf16*)out;
-    if (n_pend == 2) hipLaunchKernelGGL((qkv_attn_kernel<2, 10>), dim3(B * H), dim3(64 * AW), 0, st, a);
-    else hipLaunchKernelGGL((qkv_attn_kernel<0, 10>), dim3(B * H), dim3(64 * AW), 0, st, a);
     SPT_LAUNCH_CHECK();
 }
 

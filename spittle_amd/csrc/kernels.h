@@ -148,13 +148,6 @@ void dec_embed(int dtype, const int* tok, int R, int Tq, int d, const void* tok_
 // self attention over the cache: q [R][d] (row b*Tq + t at position pos0 + t), keys 0..pos0+t
 void dec_self_attn(int dtype, const void* q, const void* cache, int B, int H, int ctx, int Tq,
                    const DecState* ds, void* out, hipStream_t st);
-// One decode step (Tq = 1) of LN1(x + pend) + QKV projection + self K/V append at pos0 +
-// self-attention, one workgroup per (b, h); bitwise the gemv(GV_QKV_CACHE, A_LN) +
-// dec_self_attn pair.  bf16, d = 1280 only (dec_qkv_attn_supported); x_out as A_LN's.
-bool dec_qkv_attn_supported(int dtype, int d);
-void dec_qkv_attn(const float* x, const float* const* pend, int n_pend, float* x_out, const float* ln_w,
-                  const float* ln_b, const void* W, const float* bias, void* cache, int B, int H, int ctx,
-                  const DecState* ds, void* out, hipStream_t st);
 // cross attention over all T_enc cached encoder keys: q [R][d] -> out [R][d]
 // kv: [2][B_layout][H][T_enc][64] (already offset to the first of the B sequences).
 // splits > 1: the keys of each (b, h) in `splits` chunks (one workgroup each) that write
