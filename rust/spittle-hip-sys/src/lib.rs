@@ -338,7 +338,6 @@ extern "C" {
     pub fn spt_parakeet_onnx_tensor(h: *const spt_pk_onnx, tensor_id: i32, data: *mut *const f32) -> i64;
     pub fn spt_parakeet_onnx_piece(h: *const spt_pk_onnx, token_id: i32) -> *const c_char;
     pub fn spt_parakeet_onnx_close(h: *mut spt_pk_onnx);
-    pub fn spt_parakeet_debug_last_encoder(ctx: *mut spt_pk_ctx, b: i32, out: *mut f32, t3: *mut i32) -> spt_status;
 
     // ---- ABI 8: voice-activity gate (audio_toolkit/vad: SmoothedVad over SileroVad)
     pub fn spt_vad_default_params(p: *mut spt_vad_params);

@@ -61,25 +61,36 @@ uint64_t as_varint(const Reader& r) {
     return t.varint();
 }
 std::string as_string(const Reader& r) { return std::string((const char*)r.p, (size_t)(r.end - r.p)); }
-float as_f32(const Reader& r) {
-    float f;
-    memcpy(&f, r.p, 4);
-    return f;
+// a fixed32 float: only from a wire-type-5 field (exactly 4 payload bytes); anything else is a
+// malformed file, not 4 bytes read past a shorter field
+bool as_f32(int wt, const Reader& r, float* f) {
+    if (wt != 5 || r.end - r.p != 4) return false;
+    memcpy(f, r.p, 4);
+    return true;
 }
 
-// repeated scalar fields, packed (wire type 2) or not
-void rep_varint(int wt, const Reader& r, std::vector<int64_t>* out) {
-    if (wt == 0) { out->push_back((int64_t)as_varint(r)); return; }
+// repeated scalar fields, packed (wire type 2) or not; a wrong wire type fails the parse
+bool rep_varint(int wt, const Reader& r, std::vector<int64_t>* out) {
+    if (wt == 0) { out->push_back((int64_t)as_varint(r)); return true; }
+    if (wt != 2) return false;
     Reader t = r;
     while (!t.done()) out->push_back((int64_t)t.varint());
+    return t.ok;
 }
-void rep_f32(int wt, const Reader& r, std::vector<float>* out) {
-    if (wt == 5) { out->push_back(as_f32(r)); return; }
+bool rep_f32(int wt, const Reader& r, std::vector<float>* out) {
+    if (wt == 5) {
+        float f;
+        if (!as_f32(wt, r, &f)) return false;
+        out->push_back(f);
+        return true;
+    }
+    if (wt != 2 || (r.end - r.p) % 4) return false;
     for (const uint8_t* q = r.p; q + 4 <= r.end; q += 4) {
         float f;
         memcpy(&f, q, 4);
         out->push_back(f);
     }
+    return true;
 }
 
 bool parse_tensor(Reader r, Tensor* t) {
@@ -88,14 +99,15 @@ bool parse_tensor(Reader r, Tensor* t) {
     while (!r.done()) {
         if (!r.field(&num, &wt, &s)) return false;
         switch (num) {
-            case 1: rep_varint(wt, s, &t->dims); break;
-            case 2: t->data_type = (int)as_varint(s); break;
-            case 4: rep_f32(wt, s, &t->f32); break;
-            case 5: case 7: rep_varint(wt, s, &t->i64); break;
+            case 1: if (!rep_varint(wt, s, &t->dims)) return false; break;
+            case 2: if (wt != 0) return false; t->data_type = (int)as_varint(s); break;
+            case 4: if (!rep_f32(wt, s, &t->f32)) return false; break;
+            case 5: case 7: if (!rep_varint(wt, s, &t->i64)) return false; break;
             case 8: t->name = as_string(s); break;
             case 9: t->raw = s.p; t->raw_len = (size_t)(s.end - s.p); break;
             case 10: {  // double_data: fixed64, packed or not
-                if (wt == 1) { double d; memcpy(&d, s.p, 8); t->f32.push_back((float)d); }
+                if (wt == 1) { double d; memcpy(&d, s.p, 8); t->f32.push_back((float)d); }  // field() gave 8 bytes
+                else if (wt != 2 || (s.end - s.p) % 8) return false;
                 else for (const uint8_t* q = s.p; q + 8 <= s.end; q += 8) { double d; memcpy(&d, q, 8); t->f32.push_back((float)d); }
                 break;
             }
@@ -111,14 +123,20 @@ bool parse_tensor(Reader r, Tensor* t) {
                 else if (k == "length") t->ext_length = strtoll(v.c_str(), nullptr, 10);
                 break;
             }
-            case 14: external = as_varint(s) == 1; break;
+            case 14: if (wt != 0) return false; external = as_varint(s) == 1; break;
             default: break;
         }
     }
     if (external && t->ext_location.empty()) return false;
     if (!external) t->ext_location.clear();
-    for (int64_t d : t->dims)
-        if (d < 0 || d > (int64_t)1 << 40) return false;
+    // each extent and their product bounded (2^34 elements = 64 GiB of f32): no wrapped int64
+    // reaches Tensor::numel / to_f32's resize
+    int64_t n = 1;
+    for (int64_t d : t->dims) {
+        if (d < 0 || d > (int64_t)1 << 34) return false;
+        if (d > 0 && n > (((int64_t)1 << 34) / d)) return false;
+        n *= d;
+    }
     return true;
 }
 
@@ -130,15 +148,15 @@ bool parse_attr(Reader r, Attribute* a, int depth) {
         if (!r.field(&num, &wt, &s)) return false;
         switch (num) {
             case 1: a->name = as_string(s); break;
-            case 2: a->f = as_f32(s); break;
-            case 3: a->i = (int64_t)as_varint(s); break;
+            case 2: if (!as_f32(wt, s, &a->f)) return false; break;
+            case 3: if (wt != 0) return false; a->i = (int64_t)as_varint(s); break;
             case 4: a->s = as_string(s); break;
             case 6:
                 if (depth > 8) return false;  // nested subgraphs: bounded
                 a->g = std::make_shared<Graph>();
                 if (!parse_graph(s, a->g.get(), depth + 1)) return false;
                 break;
-            case 8: rep_varint(wt, s, &a->ints); break;
+            case 8: if (!rep_varint(wt, s, &a->ints)) return false; break;
             default: break;
         }
     }

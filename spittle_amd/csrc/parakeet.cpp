@@ -351,6 +351,11 @@ bool ParakeetEngine::reserve_samples(int n, int64_t max_bytes) {
     const int old = max_samples_;
     HIP_CHECK(hipFree(aarena_));
     aarena_ = nullptr;
+    // the last call's encoder output lived in the freed workspace: no completed call remains
+    enc_out_ = nullptr;
+    enc_out_graph_.clear();
+    last_lens_.clear();
+    for (int& v : last_dims_) v = 0;
     max_samples_ = (int)want;
     set_frame_limits();
     try {
@@ -630,7 +635,7 @@ void ParakeetEngine::mark(int cls) {
 void ParakeetEngine::profile_encoder(int iters, double ms[PK_ST_COUNT]) {
     select();
     const int B = last_dims_[0];
-    if (B < 1) throw std::runtime_error("profile_encoder needs a completed transcription call first");
+    if (B < 1 || !enc_out_) throw std::runtime_error("profile_encoder needs a completed transcription call first");
     if (iters < 1 || iters > 1000) throw std::runtime_error("iters out of range");
     const size_t need = (size_t)14 * dm_.n_layers + 8;  // 13 marks per layer
     while (prof_ev_.size() < need) {
@@ -825,6 +830,7 @@ void ParakeetEngine::debug_encode(const float* mel_host, int T, float* out_host)
 
 int ParakeetEngine::debug_last_encoder(int b, float* out_host) {
     select();
+    if (!enc_out_ || last_lens_.empty()) throw std::runtime_error("no completed transcription call");
     if (b < 0 || (size_t)b * 4 >= last_lens_.size()) throw std::runtime_error("no such row in the last call");
     const int T3 = last_lens_[b * 4 + 3];
     HIP_CHECK(hipStreamSynchronize(st_));

@@ -126,10 +126,18 @@ struct Mapper {
         }
         return hit;
     }
+    // a tensor id takes one value: the same value again (a weight consumed by two nodes) is
+    // accepted, a different one means the graph maps two tensors onto one role -- an error, not a
+    // silent first-wins choice
     bool put(int tid, Val v, std::string* err, const std::string& what) {
+        if (tid == -2) { *err = "node '" + what + "': its parameter matches several tensors"; return false; }
         if (tid < 0) return true;
-        if (assigned.count(tid)) return true;  // first assignment wins (node semantics before names)
-        (void)err; (void)what;
+        if (assigned.count(tid)) {
+            const Val& o = (*out)[tid];
+            if (o.dims == v.dims && o.v == v.v) return true;
+            *err = "node '" + what + "': a second, different value for " + pk_tensor_name(tid);
+            return false;
+        }
         assigned.insert(tid);
         (*out)[tid] = std::move(v);
         return true;
@@ -248,6 +256,7 @@ Val lstm_gates(const float* src, int64_t H, int64_t cols) {
 }
 
 bool map_graph(const onnx::Model& m, Mapper* mp, int* n_q, std::string* err) {
+#define PUT(...) do { if (!mp->put(__VA_ARGS__)) return false; } while (0)
     std::map<std::string, Val> vals;
     if (!values(m, &vals, n_q, err)) return false;
     std::map<std::string, int> bias_uv;  // per self_attn path: pos_bias Adds seen (u, then v)
@@ -258,35 +267,44 @@ bool map_graph(const onnx::Model& m, Mapper* mp, int* n_q, std::string* err) {
         auto in = [&](size_t i) -> const Val* { return i < n.inputs.size() ? find_val(vals, n.inputs[i]) : nullptr; };
         if (op == "MatMul" || op == "MatMulInteger" || op == "MatMulIntegerToFloat") {
             const Val* w = in(1);
-            if (w && w->dims.size() == 2) mp->put(mp->lookup(path + ".weight"), transpose2(*w), err, n.name);
+            if (w && w->dims.size() == 2) PUT(mp->lookup(path + ".weight"), transpose2(*w), err, n.name);
         } else if (op == "Gemm") {
             const onnx::Attribute* tb = n.attr("transB");
             if (const Val* w = in(1); w && w->dims.size() == 2)
-                mp->put(mp->lookup(path + ".weight"), tb && tb->i ? *w : transpose2(*w), err, n.name);
-            if (const Val* b = in(2)) mp->put(mp->lookup(path + ".bias"), *b, err, n.name);
+                PUT(mp->lookup(path + ".weight"), tb && tb->i ? *w : transpose2(*w), err, n.name);
+            if (const Val* b = in(2)) PUT(mp->lookup(path + ".bias"), *b, err, n.name);
         } else if (op == "Conv" || op == "ConvInteger") {
-            if (const Val* w = in(1)) mp->put(mp->lookup(path + ".weight"), *w, err, n.name);
+            if (const Val* w = in(1)) PUT(mp->lookup(path + ".weight"), *w, err, n.name);
             if (op == "Conv")
-                if (const Val* b = in(2)) mp->put(mp->lookup(path + ".bias"), *b, err, n.name);
+                if (const Val* b = in(2)) PUT(mp->lookup(path + ".bias"), *b, err, n.name);
         } else if (op == "LayerNormalization") {
-            if (const Val* w = in(1)) mp->put(mp->lookup(path + ".weight"), *w, err, n.name);
-            if (const Val* b = in(2)) mp->put(mp->lookup(path + ".bias"), *b, err, n.name);
+            if (const Val* w = in(1)) PUT(mp->lookup(path + ".weight"), *w, err, n.name);
+            if (const Val* b = in(2)) PUT(mp->lookup(path + ".bias"), *b, err, n.name);
         } else if (op == "BatchNormalization") {
             const char* f[4] = {".weight", ".bias", ".running_mean", ".running_var"};
             for (int i = 0; i < 4; ++i)
-                if (const Val* v = in(1 + i)) mp->put(mp->lookup(path + f[i]), *v, err, n.name);
+                if (const Val* v = in(1 + i)) PUT(mp->lookup(path + f[i]), *v, err, n.name);
         } else if (op == "Gather") {
             const Val* w = in(0);
-            if (w && w->dims.size() == 2) mp->put(mp->lookup(path + ".weight"), *w, err, n.name);
+            if (w && w->dims.size() == 2) PUT(mp->lookup(path + ".weight"), *w, err, n.name);
         } else if (op == "Add" || op == "Sub") {
             for (size_t i = 0; i < n.inputs.size(); ++i) {
                 const Val* v = in(i);
                 if (!v) continue;
                 int tid = mp->lookup(n.inputs[i]);  // a parameter used as it is keeps its name
-                if (tid < 0 && v->dims.size() == 2 && path.size() >= 9 && path.compare(path.size() - 9, 9, "self_attn") == 0)
-                    tid = mp->lookup(path + (bias_uv[path]++ == 0 ? ".pos_bias_u" : ".pos_bias_v"));
+                if (tid == -2) tid = -1;            // a generic initializer name is no role
+                if (tid < 0 && v->dims.size() == 2 && path.size() >= 9 && path.compare(path.size() - 9, 9, "self_attn") == 0) {
+                    // unnamed [H][dk] operands of the relative attention: pos_bias_u, then pos_bias_v
+                    const int k = bias_uv[path]++;
+                    if (k >= 2) {
+                        *err = "node '" + n.name + "': a third unnamed [H][dk] Add operand in " + path +
+                               " (only pos_bias_u then pos_bias_v are expected)";
+                        return false;
+                    }
+                    tid = mp->lookup(path + (k == 0 ? ".pos_bias_u" : ".pos_bias_v"));
+                }
                 if (tid < 0 && v->dims.size() == 1) tid = mp->lookup(path + ".bias");
-                mp->put(tid, *v, err, n.name);
+                PUT(tid, *v, err, n.name);
             }
         } else if (op == "LSTM" || op == "DynamicQuantizeLSTM") {
             const Val* W = in(1);
@@ -306,8 +324,8 @@ bool map_graph(const onnx::Model& m, Mapper* mp, int* n_q, std::string* err) {
             const int64_t H4 = w.dims[1], H = H4 / 4, IN = w.dims[2];
             if (H4 % 4 || r.dims[1] != H4 || r.dims[2] != H) { *err = "LSTM node '" + n.name + "': bad weight shapes"; return false; }
             const int base = 90001 + 4 * lstm_layer;
-            mp->put(base + 0, lstm_gates(w.v.data(), H, IN), err, n.name);
-            mp->put(base + 1, lstm_gates(r.v.data(), H, H), err, n.name);
+            PUT(base + 0, lstm_gates(w.v.data(), H, IN), err, n.name);
+            PUT(base + 1, lstm_gates(r.v.data(), H, H), err, n.name);
             Val bi, bh;
             if (B && (int64_t)B->v.size() == 8 * H) {
                 bi = lstm_gates(B->v.data(), H, 1);
@@ -317,15 +335,15 @@ bool map_graph(const onnx::Model& m, Mapper* mp, int* n_q, std::string* err) {
                 bh.v.assign((size_t)(4 * H), 0.f);
             }
             bi.dims = {4 * H}; bh.dims = {4 * H};
-            mp->put(base + 2, bi, err, n.name);
-            mp->put(base + 3, bh, err, n.name);
+            PUT(base + 2, bi, err, n.name);
+            PUT(base + 3, bh, err, n.name);
             ++lstm_layer;
         }
     }
     // parameters consumed by ops the node pass does not know keep their state-dict names
     for (auto& kv : vals) {
         const int tid = mp->lookup(kv.first);
-        if (tid >= 0 && !mp->assigned.count(tid)) mp->put(tid, kv.second, err, kv.first);
+        if (tid >= 0 && !mp->assigned.count(tid)) PUT(tid, kv.second, err, kv.first);
     }
     return true;
 }
@@ -433,6 +451,49 @@ bool load_parakeet_onnx(const std::string& dir, PkOnnxModel* out, std::string* e
             t[b + 28] = Val{{(int64_t)d.d}, std::vector<float>((size_t)d.d, 1.f - 1e-5f)};  // 1 / sqrt(var + eps) = 1
         }
         if (!t.count(b + 24)) t[b + 24] = Val{{(int64_t)d.d}, std::vector<float>((size_t)d.d, 0.f)};  // no conv bias
+    }
+    // every tensor in its NeMo shape: the leading (output) extent and the product of the rest, so a
+    // weight mapped in the wrong orientation fails here rather than loading with the right element
+    // count (square d x d projections cannot be told apart by shape)
+    {
+        const int64_t D = d.d, C = d.sub_ch, FF = d.ff, P = d.pred, F3 = d.n_mels / 8;
+        const int64_t NO = d.n_vocab + 1 + d.n_dur, dk = D / std::max(1, d.n_heads);
+        std::map<int, std::pair<int64_t, int64_t>> want = {
+            {1, {C, 9}}, {2, {C, 1}}, {3, {C, 9}}, {4, {C, 1}}, {5, {C, C}}, {6, {C, 1}}, {7, {C, 9}}, {8, {C, 1}},
+            {9, {C, C}}, {10, {C, 1}}, {11, {D, C * F3}}, {12, {D, 1}},
+            {90000, {d.n_vocab + 1, P}}, {90009, {P, D}}, {90010, {P, 1}}, {90011, {P, P}}, {90012, {P, 1}},
+            {90013, {NO, P}}, {90014, {NO, 1}}};
+        for (int j = 0; j < 2; ++j) {
+            want[90001 + 4 * j] = {4 * P, P};
+            want[90002 + 4 * j] = {4 * P, P};
+            want[90003 + 4 * j] = {4 * P, 1};
+            want[90004 + 4 * j] = {4 * P, 1};
+        }
+        for (int l = 0; l < d.n_layers; ++l) {
+            const int b = 1000 + 64 * l;
+            const std::pair<int, std::pair<int64_t, int64_t>> lw[] = {
+                {2, {FF, D}}, {3, {FF, 1}}, {4, {D, FF}}, {8, {D, D}}, {10, {D, D}}, {12, {D, D}}, {14, {D, D}},
+                {16, {D, D}}, {17, {d.n_heads, dk}}, {18, {d.n_heads, dk}}, {21, {2 * D, D}}, {22, {2 * D, 1}},
+                {23, {D, d.conv_k}}, {29, {D, D}}, {33, {FF, D}}, {34, {FF, 1}}, {35, {D, FF}}};
+            for (auto& x : lw) want[b + x.first] = x.second;
+            for (int k : {0, 1, 5, 6, 7, 9, 11, 13, 15, 19, 20, 24, 25, 26, 27, 28, 30, 31, 32, 36, 37, 38})
+                want[b + k] = {D, 1};
+        }
+        for (auto& kv : t) {
+            auto w = want.find(kv.first);
+            if (w == want.end()) continue;
+            const std::vector<int64_t>& dm = kv.second.dims;
+            int64_t rest = 1;
+            for (size_t a = 1; a < dm.size(); ++a) rest *= dm[a];
+            const int64_t lead = dm.empty() ? 1 : dm[0];
+            if (lead != w->second.first || rest != w->second.second) {
+                std::string s;
+                for (int64_t x : dm) s += (s.empty() ? "" : " x ") + std::to_string(x);
+                *err = pk_tensor_name(kv.first) + ": shape [" + s + "], expected [" + std::to_string(w->second.first) +
+                       "][" + std::to_string(w->second.second) + "]";
+                return false;
+            }
+        }
     }
     out->dims = d;
     for (auto& kv : t) out->tensors[kv.first] = std::move(kv.second.v);

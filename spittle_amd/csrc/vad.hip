@@ -10,181 +10,19 @@
 #include <stdexcept>
 
 #include "common.h"
-#include "onnx_pb.h"
+#include "vad_model.h"
 
 namespace spt {
 
-constexpr int kPadL = 96;      // reflect padding of the frame on both sides (the graph's Pad)
 constexpr int kPadded = kVadFrame + 2 * kPadL;  // 672
 constexpr int kT = 7;          // STFT steps: (672 - 256) / 64 + 1
 
-// ------------------------------------------------------------------ model (host)
-struct ConvW {  // one Conv node: weight [out][in / group][k], bias [out]
-    int out = 0, in_g = 0, k = 0, group = 1, stride = 1, pad = 0;
-    std::vector<float> w, b;
-};
-struct SileroHost {
-    ConvW stft, filt;                 // forward basis (258 x 256, stride 64), adaptive-normalisation filter (7)
-    ConvW blk[17];                    // the encoder's convolutions in graph order (below)
-    ConvW dec;                        // decoder 1x1 conv 64 -> 1
-    std::vector<float> lw[2], lr[2], lb[2];  // LSTM layers: W [256][64], R [256][64], B [512] (ONNX gates i, o, f, c)
-    float pad_left = 96.f, pad_right = 96.f, mag_scale = 1048576.f;
-};
-
-namespace {
-
-const onnx::Tensor* find_t(const std::vector<const onnx::Graph*>& scopes, const std::string& name) {
-    for (auto it = scopes.rbegin(); it != scopes.rend(); ++it)
-        if (const onnx::Tensor* t = (*it)->find(name)) return t;
-    return nullptr;
-}
-
-std::vector<float> vals(const std::vector<const onnx::Graph*>& scopes, const std::string& name, std::string* err) {
-    const onnx::Tensor* t = find_t(scopes, name);
-    std::vector<float> v;
-    if (!t) { *err = "Silero model: no initializer '" + name + "'"; return v; }
-    if (!t->to_f32(&v, err)) v.clear();
-    return v;
-}
-
-bool read_conv(const onnx::Node& n, const std::vector<const onnx::Graph*>& sc, ConvW* c, std::string* err) {
-    const onnx::Tensor* w = n.inputs.size() > 1 ? find_t(sc, n.inputs[1]) : nullptr;
-    if (!w || w->dims.size() != 3) { *err = "Silero model: Conv '" + n.name + "' weight is not a 1-D conv initializer"; return false; }
-    c->out = (int)w->dims[0]; c->in_g = (int)w->dims[1]; c->k = (int)w->dims[2];
-    if (const onnx::Attribute* a = n.attr("group")) c->group = (int)a->i;
-    if (const onnx::Attribute* a = n.attr("strides"); a && !a->ints.empty()) c->stride = (int)a->ints[0];
-    if (const onnx::Attribute* a = n.attr("pads"); a && !a->ints.empty()) c->pad = (int)a->ints[0];
-    if (!w->to_f32(&c->w, err)) return false;
-    if (n.inputs.size() > 2 && !n.inputs[2].empty()) {
-        c->b = vals(sc, n.inputs[2], err);
-        if (c->b.empty()) return false;
-    } else c->b.assign(c->out, 0.f);
-    return (int)c->b.size() == c->out;
-}
-
-const onnx::Graph* branch(const onnx::Node& n, const char* which) {
-    const onnx::Attribute* a = n.attr(which);
-    return a ? a->g.get() : nullptr;
-}
-
-// expected encoder conv shapes (out, in/group, k, group, stride) in graph order
-struct Shape { int out, in_g, k, group, stride; };
-const Shape kBlk[17] = {
-    {258, 1, 5, 258, 1}, {16, 258, 1, 1, 1}, {16, 258, 1, 1, 1},   // first_layer: dw, pw, proj
-    {16, 16, 1, 1, 2},                                              // stride-2 1x1
-    {16, 1, 5, 16, 1}, {32, 16, 1, 1, 1}, {32, 16, 1, 1, 1},       // encoder.3: dw, pw, proj
-    {32, 32, 1, 1, 2},
-    {32, 1, 5, 32, 1}, {32, 32, 1, 1, 1},                           // encoder.7: dw, pw (identity residual)
-    {32, 32, 1, 1, 2},
-    {32, 1, 5, 32, 1}, {64, 32, 1, 1, 1}, {64, 32, 1, 1, 1},       // encoder.11: dw, pw, proj
-    {64, 64, 1, 1, 1},                                              // 1x1 before the LSTM
-    {0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}};
-constexpr int kNBlk = 15;
-
-bool load_silero(const std::string& path, SileroHost* m, std::string* err) {
-    onnx::Model model;
-    if (!model.open(path, err)) return false;
-    const onnx::Graph& top = model.graph();
-    // the top-level If on sr == 16000: its then branch is the 16 kHz model
-    const onnx::Graph* g16 = nullptr;
-    for (const onnx::Node& n : top.nodes)
-        if (n.op_type == "If") g16 = branch(n, "then_branch");
-    if (!g16) { *err = path + ": not the Silero VAD graph (no sample-rate If)"; return false; }
-    std::vector<const onnx::Graph*> sc{&top, g16};
-    std::vector<const onnx::Node*> convs;
-    const onnx::Node* lstm_if = nullptr;
-    for (const onnx::Node& n : g16->nodes) {
-        if (n.op_type == "Conv") convs.push_back(&n);
-        if (n.op_type == "If")
-            if (const onnx::Graph* t = branch(n, "then_branch"))
-                for (const onnx::Node& x : t->nodes)
-                    if (x.op_type == "LSTM") lstm_if = &n;
-        if (n.op_type == "Pad" && n.inputs.size() > 1) {
-            std::vector<float> p = vals(sc, n.inputs[1], err);
-            if (p.size() >= 2 && p.size() % 2 == 0) {  // [begins..., ends...]: the time (last) axis
-                m->pad_left = p[p.size() / 2 - 1];
-                m->pad_right = p[p.size() - 1];
-            }
-        }
-        if (n.op_type == "Mul")
-            for (const std::string& in : n.inputs)
-                if (const onnx::Tensor* t = find_t(sc, in); t && t->numel() == 1) {
-                    std::vector<float> v;
-                    if (t->to_f32(&v, err)) m->mag_scale = v[0];
-                }
-    }
-    // graph order: STFT basis, normalisation filter, 15 encoder convs, decoder conv
-    if (convs.size() != (size_t)(2 + kNBlk + 1)) {
-        *err = path + ": expected " + std::to_string(2 + kNBlk + 1) + " Conv nodes in the 16 kHz branch, found " +
-               std::to_string(convs.size());
-        return false;
-    }
-    if (!read_conv(*convs[0], sc, &m->stft, err) || !read_conv(*convs[1], sc, &m->filt, err) ||
-        !read_conv(*convs.back(), sc, &m->dec, err))
-        return false;
-    if (m->stft.out != 258 || m->stft.k != 256 || m->stft.stride != 64 || m->filt.k != 7 || m->dec.out != 1 || m->dec.in_g != 64) {
-        *err = path + ": unexpected STFT / filter / decoder shapes";
-        return false;
-    }
-    for (int i = 0; i < kNBlk; ++i) {
-        if (!read_conv(*convs[2 + i], sc, &m->blk[i], err)) return false;
-        const ConvW& c = m->blk[i];
-        const Shape& s = kBlk[i];
-        if (c.out != s.out || c.in_g != s.in_g || c.k != s.k || c.group != s.group || c.stride != s.stride ||
-            (c.k == 5 && c.pad != 2)) {
-            *err = path + ": encoder conv " + std::to_string(i) + " has an unexpected shape";
-            return false;
-        }
-    }
-    if (!lstm_if) { *err = path + ": no LSTM in the 16 kHz branch"; return false; }
-    const onnx::Graph* with_state = branch(*lstm_if, "then_branch");  // the caller's h / c
-    std::vector<const onnx::Graph*> sc2{&top, g16, with_state};
-    int layer = 0;
-    for (const onnx::Node& x : with_state->nodes) {
-        if (x.op_type != "LSTM" || layer >= 2) continue;
-        if (x.inputs.size() < 4) { *err = path + ": LSTM without bias"; return false; }
-        m->lw[layer] = vals(sc2, x.inputs[1], err);
-        m->lr[layer] = vals(sc2, x.inputs[2], err);
-        m->lb[layer] = vals(sc2, x.inputs[3], err);
-        if (m->lw[layer].size() != 256 * 64 || m->lr[layer].size() != 256 * 64 || m->lb[layer].size() != 512) {
-            *err = path + ": LSTM layer " + std::to_string(layer) + " is not 64 units over 64 inputs";
-            return false;
-        }
-        ++layer;
-    }
-    if (layer != 2) { *err = path + ": expected two LSTM layers"; return false; }
-    if (m->pad_left != (float)kPadL || m->pad_right != (float)kPadL) { *err = path + ": unexpected STFT padding"; return false; }
-    return true;
-}
-
-// ------------------------------------------------------------------ device layout
-// one f32 blob; offsets (floats) of every tensor
-struct Off {
-    int64_t stft_w, filt_w, blk_w[kNBlk], blk_b[kNBlk], dec_w, dec_b, lw[2], lr[2], lb[2], total;
-};
-
-Off layout(const SileroHost& m) {
-    Off o{};
-    int64_t p = 0;
-    auto take = [&](int64_t n) { const int64_t r = p; p += (n + 63) / 64 * 64; return r; };
-    o.stft_w = take(258 * 256);
-    o.filt_w = take(7);
-    for (int i = 0; i < kNBlk; ++i) {
-        o.blk_w[i] = take((int64_t)m.blk[i].w.size());
-        o.blk_b[i] = take(m.blk[i].out);
-    }
-    o.dec_w = take(64);
-    o.dec_b = take(1);
-    for (int l = 0; l < 2; ++l) { o.lw[l] = take(256 * 64); o.lr[l] = take(256 * 64); o.lb[l] = take(256); }
-    o.total = p;
-    return o;
-}
-
 // ------------------------------------------------------------------ kernels
+namespace {
 
 struct FrontArgs {
     const float* w;            // the weight blob
-    Off o;
+    SileroOff o;
     float mag_scale;
     const float* pcm;          // [frames][480]
     float* feat;               // [frames][64]
@@ -278,7 +116,7 @@ __global__ __launch_bounds__(256) void vad_front_kernel(FrontArgs a) {
     for (int i = tid; i < 129 * kT; i += 256) x1[129 * kT + i] = d1[i] - mm;  // [magnitude | normalised]
     __syncthreads();
     const float* W = a.w;
-    const Off& o = a.o;
+    const SileroOff& o = a.o;
     // first_layer: dw(258) -> pw 258 -> 16, proj 258 -> 16 of x1, ReLU(sum)
     dw5(W + o.blk_w[0], W + o.blk_b[0], x1, d1, 258, kT);
     __syncthreads();
@@ -314,7 +152,7 @@ __global__ __launch_bounds__(256) void vad_front_kernel(FrontArgs a) {
 
 struct LstmArgs {
     const float* w;
-    Off o;
+    SileroOff o;
     const float* feat;   // [frames][64]
     int n;
     float* state;        // h [2][64], c [2][64]: in and out
@@ -374,7 +212,7 @@ __global__ __launch_bounds__(512) void vad_lstm_kernel(LstmArgs a) {
 }  // namespace
 
 struct VadEngine::Ptrs {
-    Off o;
+    SileroOff o;
     float mag_scale;
 };
 
@@ -382,21 +220,8 @@ VadEngine::VadEngine(const std::string& model_path, int device) : dev_(device) {
     SileroHost m;
     std::string err;
     if (!load_silero(model_path, &m, &err)) throw std::runtime_error(err);
-    p_ = new Ptrs{layout(m), m.mag_scale};
-    std::vector<float> blob((size_t)p_->o.total, 0.f);
-    auto put = [&](int64_t off, const std::vector<float>& v) { std::copy(v.begin(), v.end(), blob.begin() + off); };
-    put(p_->o.stft_w, m.stft.w);
-    put(p_->o.filt_w, m.filt.w);
-    for (int i = 0; i < kNBlk; ++i) { put(p_->o.blk_w[i], m.blk[i].w); put(p_->o.blk_b[i], m.blk[i].b); }
-    put(p_->o.dec_w, m.dec.w);
-    put(p_->o.dec_b, m.dec.b);
-    for (int l = 0; l < 2; ++l) {
-        put(p_->o.lw[l], m.lw[l]);
-        put(p_->o.lr[l], m.lr[l]);
-        std::vector<float> b(256);
-        for (int i = 0; i < 256; ++i) b[i] = m.lb[l][i] + m.lb[l][256 + i];
-        put(p_->o.lb[l], b);
-    }
+    p_ = new Ptrs{SileroOff{}, m.mag_scale};
+    const std::vector<float> blob = silero_blob(m, &p_->o);
     select();
     HIP_CHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
@@ -426,8 +251,13 @@ void VadEngine::reset_state() {
 
 void VadEngine::ensure(int n) {
     if (n <= cap_frames_) return;
+    // freed and cleared first: if an allocation below throws, the destructor finds no stale pointer
     for (void* p : {(void*)pcm_, (void*)feat_, (void*)prob_})
         if (p) HIP_CHECK(hipFree(p));
+    pcm_ = nullptr;
+    feat_ = nullptr;
+    prob_ = nullptr;
+    cap_frames_ = 0;
     const int cap = std::max(n, 1024);
     HIP_CHECK(hipMalloc(&pcm_, (size_t)cap * kVadFrame * 4));
     HIP_CHECK(hipMalloc(&feat_, (size_t)cap * 64 * 4));

@@ -214,8 +214,11 @@ LSTM_PERM = [0, 3, 1, 2]  # ONNX gate block g <- torch block LSTM_PERM[g]: (i, o
 
 
 def write_dir(path: str, model, dims, quant: str = "int8", fold_bn: bool = False, anon_pos_bias: bool = False,
-              qdq: bool = False, external: bool = False, lstm_quant: bool = True) -> dict:
-    """Write the model directory; return {tensor id: f32 values (NeMo layout)} a loader must recover."""
+              qdq: bool = False, external: bool = False, lstm_quant: bool = True, faults=()) -> dict:
+    """Write the model directory; return {tensor id: f32 values (NeMo layout)} a loader must recover.
+    faults (negative tests of the loader): "transposed_ff1" writes layer 0's feed_forward1.linear1
+    MatMul operand as W instead of W^T; "third_pos_bias" adds a third unnamed [H][dk] Add in layer
+    0's self_attn; "conflicting_q" adds a second linear_q MatMul with a different weight."""
     os.makedirs(path, exist_ok=True)
     d, C, H, L, ff, K, P, V = dims.d, dims.sub_ch, dims.n_heads, dims.n_layers, dims.ff, dims.conv_k, dims.pred, dims.n_vocab
     F3 = dims.n_mels
@@ -247,8 +250,13 @@ def write_dir(path: str, model, dims, quant: str = "int8", fold_bn: bool = False
                                 (8, "self_attn/linear_q", d, d), (10, "self_attn/linear_k", d, d),
                                 (12, "self_attn/linear_v", d, d), (14, "self_attn/linear_out", d, d),
                                 (33, "feed_forward2/linear1", ff, d), (35, "feed_forward2/linear2", d, ff)):
-            W, _ = g.linear(f"{p}/{nm}", _w(model, b + off, n_, k_), model.tensor(b + off + 1), x)
+            Wm = _w(model, b + off, n_, k_)
+            if l == 0 and off == 2 and "transposed_ff1" in faults:
+                Wm = np.ascontiguousarray(Wm.T)
+            W, _ = g.linear(f"{p}/{nm}", Wm, model.tensor(b + off + 1), x)
             exp[b + off], exp[b + off + 1] = W, model.tensor(b + off + 1)
+            if l == 0 and off == 8 and "conflicting_q" in faults:
+                g.linear(f"{p}/{nm}", Wm * 2, model.tensor(b + off + 1), x)
         W, _ = g.linear(f"{p}/self_attn/linear_pos", _w(model, b + 16, d, d), None, "pos_emb")
         exp[b + 16] = W
         for k, (off, suf) in enumerate(((17, "u"), (18, "v"))):
@@ -256,6 +264,10 @@ def write_dir(path: str, model, dims, quant: str = "int8", fold_bn: bool = False
             g.init(nm, _w(model, b + off, H, d // H))
             g.nodes.append(node_proto("Add", f"/{p}/self_attn/Add" + ("" if k == 0 else "_1"), ["q", nm], [f"qb{k}"]))
             exp[b + off] = model.tensor(b + off)
+        if l == 0 and "third_pos_bias" in faults:
+            nm = g.anon("Add")
+            g.init(nm, _w(model, b + 17, H, d // H))
+            g.nodes.append(node_proto("Add", f"/{p}/self_attn/Add_2", ["q", nm], ["qb2"]))
         W = g.conv(f"{p}/conv/pointwise_conv1", _w(model, b + 21, 2 * d, d, 1), model.tensor(b + 22), x, 1, True)
         exp[b + 21], exp[b + 22] = W.reshape(-1), model.tensor(b + 22)
         dw, dwb = _w(model, b + 23, d, 1, K), model.tensor(b + 24)

@@ -22,6 +22,17 @@ def test_header_and_binding_agree():
     assert _header_symbols() == sorted(L.EXPORTS)
 
 
+def test_rust_sys_crate_mirrors_header():
+    """rust/spittle-hip-sys declares every header entry point exactly once (no cargo in this
+    image, so the extern block is checked as text: a duplicate item is rustc error E0428)."""
+    src = open(os.path.join(ROOT, "rust", "spittle-hip-sys", "src", "lib.rs")).read()
+    names = re.findall(r"\bpub fn (spt_[a-z_0-9]+)\s*\(", src)
+    dups = sorted({n for n in names if names.count(n) > 1})
+    assert not dups, f"declared more than once: {dups}"
+    hdr = set(_header_symbols())
+    assert set(names) == hdr, (sorted(hdr - set(names)), sorted(set(names) - hdr))
+
+
 def test_library_exports_every_declared_symbol():
     lib = L.load()
     for name in _header_symbols():

@@ -110,3 +110,147 @@ def test_random_bit_flips(harness, tmp_path):
             i = int(rng.integers(0, len(d)))
             d[i] ^= 1 << int(rng.integers(0, 8))
         _run(harness, tmp_path, bytes(d), f"flip{k}")
+
+
+# ---------------------------------------------------------------------------------------------
+# The ONNX readers: the Parakeet model directory the app downloads (onnx_pb.cpp + pk_onnx.cpp) and
+# the Silero VAD model it ships (vad_model.cpp), under the same sanitizers (tests/native/onnx_fuzz.cpp).
+
+VAD_ONNX = os.path.join(ROOT, "tests", "golden", "silero_vad_v4.onnx")
+
+
+@pytest.fixture(scope="module")
+def onnx_harness(tmp_path_factory):
+    if not shutil.which("g++"):
+        pytest.skip("g++ not available")
+    out = str(tmp_path_factory.mktemp("asan_onnx") / "onnx_fuzz")
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+           "-fno-omit-frame-pointer", "-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__",
+           os.path.join(ROOT, "tests", "native", "onnx_fuzz.cpp"), os.path.join(CSRC, "onnx_pb.cpp"),
+           os.path.join(CSRC, "pk_onnx.cpp"), os.path.join(CSRC, "vad_model.cpp"), "-o", out]
+    r = subprocess.run(cmd, capture_output=True, timeout=600)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    return out
+
+
+def _onnx_run(harness, mode: str, path: str, tag: str) -> str:
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([harness, mode, path], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0 and "Sanitizer" not in r.stderr and "runtime error" not in r.stderr, \
+        (tag, r.returncode, r.stderr[-2000:])
+    assert r.stdout.startswith("parsed") or r.stdout.startswith("rejected"), (tag, r.stdout)
+    return r.stdout
+
+
+@pytest.fixture(scope="module")
+def pk_dir(tmp_path_factory):
+    """A small valid model directory in the export's layout (int8, tests/onnx_parakeet.py)."""
+    onnx_parakeet = pytest.importorskip("tests.onnx_parakeet")
+    from oracle import parakeet as P
+    d = P.dims_for("test-small", d=64, n_layers=1, n_heads=2, ff=128, sub_ch=16, pred=32, n_vocab=64)
+    path = str(tmp_path_factory.mktemp("pkdir"))
+    onnx_parakeet.write_dir(path, P.Model(d, seed=3), d, quant="int8")
+    return path
+
+
+def _variant_dir(src: str, dst, name: str, data: bytes) -> str:
+    """a copy of the model directory with one file replaced"""
+    dst = str(dst)
+    if os.path.exists(dst):
+        shutil.rmtree(dst)
+    shutil.copytree(src, dst)
+    with open(os.path.join(dst, name), "wb") as f:
+        f.write(data)
+    return dst
+
+
+def test_onnx_valid_files_parse_clean(onnx_harness, pk_dir):
+    out = _onnx_run(onnx_harness, "parakeet", pk_dir, "valid")
+    assert "d 64, layers 1, 64 pieces" in out and "quantised" in out
+    out = _onnx_run(onnx_harness, "vad", VAD_ONNX, "vad")
+    assert out.startswith("parsed: blob"), out
+
+
+def test_onnx_truncations(onnx_harness, pk_dir, tmp_path):
+    for name in ("encoder-model.int8.onnx", "decoder_joint-model.int8.onnx"):
+        data = open(os.path.join(pk_dir, name), "rb").read()
+        cuts = sorted(set(list(range(0, 24)) + list(range(24, len(data), max(1, len(data) // 60))) + [len(data) - 1]))
+        for n in cuts:
+            out = _onnx_run(onnx_harness, "parakeet", _variant_dir(pk_dir, tmp_path / "v", name, data[:n]), f"{name}:{n}")
+            assert out.startswith("rejected"), (name, n, out)
+    data = open(VAD_ONNX, "rb").read()
+    for n in sorted(set(list(range(0, 16)) + list(range(16, len(data), max(1, len(data) // 80))))):
+        p = tmp_path / "vad.onnx"
+        p.write_bytes(data[:n])
+        assert _onnx_run(onnx_harness, "vad", str(p), f"vad:{n}").startswith("rejected"), n
+
+
+def test_onnx_oversized_varints_and_lengths(onnx_harness, pk_dir, tmp_path):
+    from tests.onnx_parakeet import _int, _key, _ld, _str, _varint
+    name = "encoder-model.int8.onnx"
+    data = open(os.path.join(pk_dir, name), "rb").read()
+    cases = {
+        "varint_11_bytes": b"\xff" * 11 + data,
+        "graph_len_2^40": _key(7, 2) + _varint(1 << 40) + data,
+        "graph_len_past_end": _key(7, 2) + _varint(len(data) + 5) + data,
+        "wire_type_group": bytes([(7 << 3) | 3]) + data,
+        "deep_subgraphs": _ld(7, _ld(1, _ld(5, _ld(6, _ld(1, _ld(5, _ld(6, b"\xff" * 9))))))) + data,
+    }
+    # tensors whose fields lie: dims inflated / overflowing / negative, raw_data shorter than the dims,
+    # a float attribute carried as a 1-byte varint, an external-data file that does not exist
+    def graph_with(init=b"", node=b""):
+        return _ld(7, (_ld(1, node) if node else b"") + (_ld(5, init) if init else b""))
+    raw = np.arange(3, dtype=np.float32).tobytes()
+    cases["raw_short"] = graph_with(_int(1, 1000) + _int(2, 1) + _str(8, "w") + _ld(9, raw))
+    cases["dims_product_overflow"] = graph_with(b"".join(_int(1, 1 << 33) for _ in range(4)) + _int(2, 1) + _str(8, "w") + _ld(9, raw))
+    cases["dim_negative"] = graph_with(_int(1, (1 << 64) - 3) + _int(2, 1) + _str(8, "w") + _ld(9, raw))
+    cases["float_attr_as_varint"] = graph_with(node=_str(4, "Conv") + _ld(5, _str(1, "alpha") + _int(2, 1)))
+    cases["packed_float_ragged"] = graph_with(_int(1, 2) + _int(2, 1) + _str(8, "w") + _ld(4, b"\0" * 7))
+    cases["dtype_as_string"] = graph_with(_int(1, 2) + _ld(2, b"xx") + _str(8, "w") + _ld(9, raw[:8]))
+    ext = _ld(13, _str(1, "location") + _str(2, "missing.data")) + _int(14, 1)
+    cases["external_missing"] = graph_with(_int(1, 4) + _int(2, 1) + _str(8, "w") + ext)
+    ext_out = _ld(13, _str(1, "location") + _str(2, "../x.data")) + _int(14, 1)
+    cases["external_outside_dir"] = graph_with(_int(1, 4) + _int(2, 1) + _str(8, "w") + ext_out)
+    for tag, blob in cases.items():
+        out = _onnx_run(onnx_harness, "parakeet", _variant_dir(pk_dir, tmp_path / "v", name, blob), tag)
+        assert out.startswith("rejected"), (tag, out)
+        p = tmp_path / "vad.onnx"
+        p.write_bytes(blob)
+        _onnx_run(onnx_harness, "vad", str(p), "vad-" + tag)
+
+
+def test_onnx_external_data_offsets(onnx_harness, pk_dir, tmp_path):
+    """external data: a range past the end of its file, and the file removed"""
+    onnx_parakeet = pytest.importorskip("tests.onnx_parakeet")
+    from oracle import parakeet as P
+    d = P.dims_for("test-small", d=64, n_layers=1, n_heads=2, ff=128, sub_ch=16, pred=32, n_vocab=64)
+    path = tmp_path / "ext"
+    onnx_parakeet.write_dir(str(path), P.Model(d, seed=3), d, quant="int8", external=True)
+    assert _onnx_run(onnx_harness, "parakeet", str(path), "ext-valid").startswith("parsed")
+    data_file = [f for f in os.listdir(path) if f.endswith(".data")][0]
+    blob = (path / data_file).read_bytes()
+    (path / data_file).write_bytes(blob[: len(blob) // 2])
+    assert _onnx_run(onnx_harness, "parakeet", str(path), "ext-short").startswith("rejected")
+    os.remove(path / data_file)
+    assert _onnx_run(onnx_harness, "parakeet", str(path), "ext-missing").startswith("rejected")
+
+
+def test_onnx_random_bit_flips(onnx_harness, pk_dir, tmp_path):
+    rng = np.random.default_rng(17)
+    for name in ("encoder-model.int8.onnx", "decoder_joint-model.int8.onnx"):
+        data = open(os.path.join(pk_dir, name), "rb").read()
+        for k in range(60):
+            d = bytearray(data)
+            for _ in range(int(rng.integers(1, 8))):
+                i = int(rng.integers(0, len(d)))
+                d[i] ^= 1 << int(rng.integers(0, 8))
+            _onnx_run(onnx_harness, "parakeet", _variant_dir(pk_dir, tmp_path / "v", name, bytes(d)), f"{name}:flip{k}")
+    data = open(VAD_ONNX, "rb").read()
+    for k in range(60):
+        d = bytearray(data)
+        for _ in range(int(rng.integers(1, 8))):
+            i = int(rng.integers(0, len(d)))
+            d[i] ^= 1 << int(rng.integers(0, 8))
+        p = tmp_path / "vad.onnx"
+        p.write_bytes(bytes(d))
+        _onnx_run(onnx_harness, "vad", str(p), f"vad:flip{k}")

@@ -79,6 +79,20 @@ def test_loader_errors(tmp_path, small):
         OnnxModelDir(str(tmp_path))
 
 
+@pytest.mark.parametrize("fault,msg", [("transposed_ff1", "shape"), ("third_pos_bias", "third unnamed"),
+                                       ("conflicting_q", "second, different value")])
+def test_loader_rejects_ambiguous_graphs(tmp_path, small, fault, msg):
+    """A graph that maps a weight in the wrong orientation, has an unexpected unnamed pos-bias
+    operand, or gives one role two different values fails to load with the tensor named, instead of
+    loading a silently wrong model."""
+    from spittle_amd import TranscriptionError
+    from spittle_amd.parakeet import OnnxModelDir
+    d, m = small
+    onnx_parakeet.write_dir(str(tmp_path), m, d, quant="int8", anon_pos_bias=True, faults=(fault,))
+    with pytest.raises(TranscriptionError, match=msg):
+        OnnxModelDir(str(tmp_path))
+
+
 def test_loader_full_shape_dims(tmp_path):
     """parakeet-tdt-0.6b-v3's own shape (24 layers, d 1024, 8 heads, 8192 tokens + 5 durations),
     written int8 as the catalog model is: dimensions and a sample of tensors."""
