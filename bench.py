@@ -60,6 +60,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-app-latency", action="store_true", help="skip the B=1 whisper_full (app default) latency")
     ap.add_argument("--no-probe", action="store_true", help="skip the per-kernel HIP-event probes")
+    ap.add_argument("--no-turbo", action="store_true", help="skip the Whisper Turbo (4 decoder layers) line")
     ap.add_argument("--no-parakeet", action="store_true", help="skip the Parakeet-V3 (BASELINE config 5) lines")
     ap.add_argument("--parakeet-only", action="store_true", help="only the Parakeet-V3 lines (developer runs)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -414,7 +415,8 @@ def _stats_fields(eng, ms: float) -> dict:
     """The call's engine runs and decoder passes (spt_get_call_stats) beside its wall time."""
     cs = eng.call_stats()
     n = max(1, cs["decoder_passes"])
-    return {"ms": round(ms, 2), "engine_calls": cs["engine_calls"], "decoder_passes": cs["decoder_passes"],
+    return {"ms": round(ms, 2), "engine_calls": cs["engine_calls"], "encoder_windows": cs["encoder_windows"],
+            "decoder_passes": cs["decoder_passes"],
             "device_ms": round(cs["device_ms"], 2), "encoder_ms": round(cs["encoder_ms"], 2),
             "decode_ms": round(cs["decode_ms"], 2), "decode_ms_per_pass": round(cs["decode_ms"] / n, 4),
             "host_ms": round(ms - cs["device_ms"], 2)}
@@ -425,8 +427,10 @@ def app_latency(eng, info: dict, dtype: str, dur_s=(5, 10, 30)) -> dict:
     its default parameters (timestamps on, temperature fallback 0.2 / best_of 5), language
     "en", through spt_transcribe.  Random-init weights never emit EOT or confident tokens, so
     every window decodes to its token limit and falls back through every temperature: an
-    upper bound of the app's latency.  Each case reports its engine calls (one per window and
-    temperature), decoder passes and the device time behind them (spt_get_call_stats);
+    upper bound of the app's latency.  Each case reports its decoder runs (engine_calls: one per
+    window and temperature), its encoder runs (encoder_windows: one per window, shared by every
+    temperature and decoder since ABI 11), decoder passes and the device time behind them
+    (spt_get_call_stats);
     decode_ms_per_pass mixes 1-row greedy passes and 5-row (best_of) sampled passes.
     `b1_greedy_pass` isolates the B = 1 pass: one 30 s window on the greedy fast path, its mean
     decoder pass against the bytes that pass streams (every layer weight, the logits matrix, one
@@ -468,6 +472,32 @@ def app_latency(eng, info: dict, dtype: str, dur_s=(5, 10, 30)) -> dict:
                                  ms_per_pass=roof.get("ms_per_pass"), achieved_GBs=roof.get("achieved"),
                                  frac_of_hbm_peak=roof.get("frac"))
     return out
+
+
+def turbo_bench(device: int, pcm_list, steps: int, warmup: int, decode_steps: int) -> dict:
+    """The catalog's Whisper Turbo (ggml-large-v3-turbo.bin: model_catalog.json:169-173) on the
+    same protocol and batch: large-v3's 32-layer encoder with 4 decoder layers (synthetic weights,
+    synthetic:large-v3:dec=4).  RTFx of the median step, phase times, decoder pass time."""
+    import numpy as np
+    from spittle_amd import WhisperEngine, WhisperInferenceParams, WhisperModelParams
+    B = len(pcm_list)
+    e = WhisperEngine(WhisperModelParams(dtype="bf16", device=device, max_batch=B, seed=1234))
+    e.load_model("synthetic:large-v3:dec=4")
+    p = WhisperInferenceParams(language="en", no_timestamps=True, temperature_inc=0.0, ignore_eot=True,
+                               max_new_tokens=decode_steps)
+    for _ in range(warmup):
+        e.transcribe_batch(pcm_list, p)
+    marks = [time.perf_counter()]
+    for _ in range(steps):
+        e.transcribe_batch(pcm_list, p)
+        marks.append(time.perf_counter())
+    med = float(np.median(np.diff(marks)))
+    t = e.timings()
+    e.unload_model()
+    return {"model": "synthetic:large-v3:dec=4 (ggml-large-v3-turbo geometry: 32 encoder + 4 decoder layers)",
+            "batch": B, "steps": steps, "rtfx": round(B * CHUNK_S / med, 2), "ms_per_step": round(med * 1e3, 3),
+            "phases_ms": {k: round(v, 3) for k, v in t.items() if k.endswith("_ms")},
+            "decode_ms_per_pass": round(t["decode_ms"] / max(1, t["n_decode_passes"]), 4)}
 
 
 def main():
@@ -585,6 +615,9 @@ def main():
     rs = None
     if rank == 0 and world == 1 and not args.no_parakeet:
         rs = resampler_bench(local, not args.no_cpu_baseline)
+    tb = None
+    if rank == 0 and world == 1 and not args.no_turbo and args.model == "synthetic:large-v3":
+        tb = turbo_bench(local, pcm_list, min(args.steps, 5), 1, args.decode_steps)
     pk = None
     if rank == 0 and world == 1 and not args.no_parakeet:
         eng.unload_model()  # free the Whisper arenas first
@@ -614,6 +647,8 @@ def main():
             out["ms_per_step_per_rank"] = rank_ms
         if wload:
             out["weight_load"] = wload
+        if tb:
+            out["whisper_turbo"] = tb
         if pk:
             out["parakeet_v3"] = pk
         if rs:

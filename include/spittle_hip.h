@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 10
+#define SPT_ABI_VERSION 11
 
 typedef enum {
     SPT_OK = 0,
@@ -92,6 +92,10 @@ typedef struct {
     float entropy_thold;         /* a decoder whose last 32 tokens' entropy is lower fails (2.4) */
     float logprob_thold;         /* fall back when the average log-probability is lower (-1.0) */
     float max_initial_ts;        /* the first timestamp is at most this many seconds (1.0) */
+    /* whisper_full_params.no_speech_thold has no counterpart: whisper.cpp 1.7.1 (vendored by
+     * whisper-rs-sys 0.11.1, the reference's engine) declares it "TODO: not implemented" and never
+     * reads it, so the reference skips no window for no-speech probability [recalled; whisper.cpp
+     * is not in /root/reference].  A later whisper.cpp's skip would be added here, not emulated. */
     int32_t reserved0;
     uint64_t seed;               /* temperature sampling stream */
 } spt_infer_params;
@@ -174,14 +178,20 @@ const char* spt_token_to_str(const spt_ctx* ctx, int32_t id);
 spt_status spt_get_timings(const spt_ctx* ctx, spt_timings* t);
 
 /* ABI 9: everything the last spt_transcribe* call ran, summed.  spt_timings holds the last engine
- * run only; a whisper_full call (the app's default parameters) runs one engine call per window
+ * run only; a whisper_full call (the app's default parameters) runs one decoder run per window
  * batch and temperature, and beam search one decoder pass per step, so its latency reads per
- * decoder pass from here: device_ms / decoder_passes bounds the pass time from above. */
+ * decoder pass from here: device_ms / decoder_passes bounds the pass time from above.
+ * ABI 11: whisper_full computes the log-mel of each whole utterance once (whisper_pcm_to_mel: its
+ * own reflective head, the utterance's global max - 8 clamp) and encodes each 30 s window at
+ * `seek` once (whisper_encode_internal), shared by every temperature fallback and by the
+ * utterance's beam / best_of decoders: encoder_windows counts those encoder runs. */
 typedef struct {
-    int32_t engine_calls;     /* mel + encoder + cross K/V + decode runs */
+    int32_t engine_calls;     /* decoder runs (a prompt pass + its steps; ABI <= 10: each with its own
+                                 mel + encoder + cross K/V) */
     int32_t decoder_passes;   /* every decoder pass: prompt passes, decode steps, beam steps */
     int32_t beam_steps;       /* host-driven beam steps among them */
-    int32_t reserved0;
+    int32_t encoder_windows;  /* ABI 11: 30 s windows encoded (conv stem + encoder + cross K/V): one
+                                 per window, shared by every temperature fallback and decoder */
     double device_ms;         /* device time of those runs and steps (HIP events) */
     double encoder_ms;
     double decode_ms;         /* decoder passes incl. prompt prefill and sampling */
@@ -243,6 +253,9 @@ spt_status spt_probe_kernel(spt_ctx* ctx, int32_t kind, int32_t iters, double* a
 /* test hooks (parity against the CPU restatement) */
 /* normalised log-mel of one window [n_mels][3000] (f32) */
 spt_status spt_debug_mel(spt_ctx* ctx, const float* pcm16k, size_t n_samples, float* out);
+/* ABI 11: the normalised log-mel [n_mels][3000] the encoder takes for the window at frame `seek` of
+ * an utterance of any length: frames [seek, seek + 3000) of the utterance's whole log-mel */
+spt_status spt_debug_mel_at(spt_ctx* ctx, const float* pcm16k, size_t n_samples, int32_t seek, float* out);
 /* encoder output [1500][d] (f32) from a host mel [n_mels][3000] */
 spt_status spt_debug_encode(spt_ctx* ctx, const float* mel, float* out);
 /* sum|w| and sum w of the weight tensor with a given id (oracle/wo_model.c table) */

@@ -73,6 +73,8 @@ def lib():
         L.wo_mel_filters.argtypes = [C.c_int, fp]
         L.wo_tables.argtypes = [fp, fp, fp]
         L.wo_mel.argtypes = [C.c_int, fp, C.c_int, C.c_int, fp]
+        L.wo_mel_len.argtypes = [C.c_int]
+        L.wo_mel_full.argtypes = [C.c_int, fp, C.c_int, fp]
         L.wo_encode.argtypes = [C.c_void_p, fp, C.c_int, fp]
         L.wo_decode.argtypes = [C.c_void_p, fp, ip, C.c_int, C.c_int, C.c_uint32, C.c_int, ip, ip, fp, fp]
         L.wo_decode_logits.argtypes = [C.c_void_p, fp, ip, C.c_int, C.c_int, fp]
@@ -101,6 +103,28 @@ def mel(pcm: np.ndarray, n_mels: int, mode: int = MEL_WHISPER_CPP) -> np.ndarray
     rc = lib().wo_mel(n_mels, _f(pcm), int(pcm.size), mode, _f(out))
     if rc != 0:
         raise ValueError(f"wo_mel failed rc={rc}")
+    return out
+
+
+def mel_full(pcm: np.ndarray, n_mels: int) -> np.ndarray:
+    """whisper.cpp's log-mel of a whole input of any length: [n_mels][(n + 480000) // 160], clamped
+    at the input's global max - 8 (whisper_pcm_to_mel, once per whisper_full call)."""
+    pcm = np.ascontiguousarray(pcm, dtype=np.float32)
+    n_len = lib().wo_mel_len(int(pcm.size))
+    out = np.empty((n_mels, n_len), np.float32)
+    rc = lib().wo_mel_full(n_mels, _f(pcm), int(pcm.size), _f(out))
+    if rc != 0:
+        raise ValueError(f"wo_mel_full failed rc={rc}")
+    return out
+
+
+def mel_window(full: np.ndarray, seek: int) -> np.ndarray:
+    """whisper_encode_internal's input: frames [seek, seek + 3000) of a whole-input log-mel, zero
+    past its end."""
+    out = np.zeros((full.shape[0], 3000), np.float32)
+    i1 = min(full.shape[1], seek + 3000)
+    if i1 > seek:
+        out[:, :i1 - seek] = full[:, seek:i1]
     return out
 
 

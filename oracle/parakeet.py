@@ -24,6 +24,9 @@ FIELDS = ("n_mels", "d", "n_layers", "n_heads", "ff", "sub_ch", "conv_k", "pred"
 # parakeet-tdt-0.6b-v3 (NeMo FastConformer-TDT, 24 layers, d 1024) and a small test shape
 CONFIGS = {
     "parakeet-tdt-0.6b-v3": (128, 1024, 24, 8, 4096, 256, 9, 640, 8192, 5),
+    # the catalog's English-only parakeet-tdt-0.6b-v2 (model_catalog.json:214-217): v3's network with
+    # a 1024-piece vocabulary [upstream, recalled]
+    "parakeet-tdt-0.6b-v2": (128, 1024, 24, 8, 4096, 256, 9, 640, 1024, 5),
     "test-small": (128, 256, 2, 4, 1024, 128, 9, 128, 1024, 5),  # engine spec "synthetic:parakeet-test-small"
 }
 

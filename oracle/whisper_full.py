@@ -13,7 +13,9 @@ Cargo.lock:8156-8174; not present here, so "parity unpinned" against whisper.cpp
     whisper_sequence_score, seek loop, prompt_past, segment assembly.
 Temperature sampling (fallback) draws from a device stream and is not restated; the window
 loop here runs greedy decoding at temperature 0 only (temperature_inc = 0).
-Each step recomputes the decoder over the whole token prefix (oracle.wo_decode_logits).
+Each step recomputes the decoder over the whole token prefix (oracle.wo_decode_logits).  Every
+window's encoder input is frames [seek, seek + 3000) of ONE log-mel of the whole input
+(oracle.mel_full: whisper_pcm_to_mel's global max - 8 clamp), as whisper_full_with_state does.
 """
 from __future__ import annotations
 
@@ -265,6 +267,8 @@ def transcribe(m: O.Model, pcm: np.ndarray, p: Params, prompt=(), lang_tok: int 
     n_max = m.dims.n_text_ctx // 2 - 4
     seek, seek_end = 0, n_len_org(len(pcm))
     past = list(prompt)
+    # whisper_pcm_to_mel: one log-mel of the whole input (global max), sliced per window
+    mel_all = O.mel_full(pcm, m.dims.n_mels)
     wins, segs, all_toks, kept = [], [], [], []
     while seek + 100 < seek_end:
         if seek > 0 and seek + 500 >= seek_end:
@@ -273,8 +277,7 @@ def transcribe(m: O.Model, pcm: np.ndarray, p: Params, prompt=(), lang_tok: int 
         if past and p.n_max_text_ctx > 0:
             n_take = min(p.n_max_text_ctx, m.dims.n_text_ctx // 2, len(past))
             pf = [sp["prev"]] + past[len(past) - n_take:]
-        chunk = pcm[seek * N_LEN_HOP: seek * N_LEN_HOP + 480000]
-        enc = m.encode(O.mel(chunk, m.dims.n_mels))
+        enc = m.encode(O.mel_window(mel_all, seek))
         steps = min(n_max, m.dims.n_text_ctx + 1 - len(pf) - len(init))
         if p.beam_size > 1:
             decs = decode_window_beam(m, enc, pf + init, seek, seek_end, pp, steps)

@@ -13,7 +13,9 @@
  *     float groups of 4 summed into a double, log10(max(sum,1e-10)))
  *   log_mel_spectrogram (200-sample reflective head, 30 s zero tail,
  *     n_len = (n + 480000)/160 frames, frames past (n+200)/160+1 = -10,
- *     global max - 8 clamp, (x + 4)/4)                         -> wo_mel
+ *     global max - 8 clamp, (x + 4)/4) over the WHOLE input     -> wo_mel_full
+ *     (whisper_pcm_to_mel runs once per whisper_full call; each window's
+ *     encoder takes frames [seek, seek + 3000)); its first window  -> wo_mel
  * The reference app feeds this 16 kHz mono f32 (src-tauri/src/managers/audio.rs:466-475
  * pads clips < 1 s to 20 000 samples; src-tauri/src/managers/transcription.rs:412-416
  * returns "" for empty audio without calling the engine).
@@ -158,6 +160,62 @@ static void mel_frame(const float* filt, int n_mels, const float* frame, int n_v
     }
 }
 
+int wo_mel_len(int n_samples) { return (int)(((long)n_samples + CHUNK) / HOP); }
+
+/* log_mel_spectrogram over the whole input: [n_mels][n_len] normalised (global max - 8) */
+static int mel_whole(int n_mels, const float* filt, const float* pcm, int n_samples, float* mel) {
+    /* samples_padded = [reflect 200][x][zeros 480000 + 200] */
+    const long n_pad = (long)n_samples + CHUNK + 2 * (N_FFT / 2);
+    float* sp = (float*)calloc(n_pad, sizeof(float));
+    if (!sp) return -3;
+    memcpy(sp + N_FFT / 2, pcm, sizeof(float) * n_samples);
+    for (int i = 0; i < N_FFT / 2; i++) {
+        int src = N_FFT / 2 - i; /* reverse_copy(samples+1, samples+1+200) */
+        sp[i] = src < n_samples ? pcm[src] : 0.0f;
+    }
+    const int n_len = (int)((n_pad - N_FFT) / HOP);
+    const int n_sig = n_samples + N_FFT / 2;
+    int n_comp = n_sig / HOP + 1;
+    if (n_comp > n_len) n_comp = n_len;
+    #pragma omp parallel
+    {
+        float fin[2 * N_FFT], fout[8 * N_FFT], col[256];
+        #pragma omp for schedule(static)
+        for (int i = 0; i < n_len; i++) {
+            if (i < n_comp) {
+                const long off = (long)i * HOP;
+                int nv = (int)(n_sig - off);
+                if (nv > N_FFT) nv = N_FFT;
+                mel_frame(filt, n_mels, sp + off, nv, fin, fout, col);
+                for (int j = 0; j < n_mels; j++) mel[(size_t)j * n_len + i] = col[j];
+            } else {
+                for (int j = 0; j < n_mels; j++) mel[(size_t)j * n_len + i] = (float)log10(1e-10);
+            }
+        }
+    }
+    double mmax = -1e20;
+    for (size_t i = 0; i < (size_t)n_mels * n_len; i++)
+        if (mel[i] > mmax) mmax = mel[i];
+    mmax -= 8.0;
+    for (size_t i = 0; i < (size_t)n_mels * n_len; i++) {
+        float v = mel[i];
+        if (v < mmax) v = (float)mmax;
+        mel[i] = (float)((v + 4.0) / 4.0);
+    }
+    free(sp);
+    return 0;
+}
+
+int wo_mel_full(int n_mels, const float* pcm, int n_samples, float* out) {
+    if (n_samples < 0) return -1;
+    init_tables();
+    float* filt = (float*)malloc(sizeof(float) * n_mels * N_BINS);
+    wo_mel_filters(n_mels, filt);
+    const int rc = mel_whole(n_mels, filt, pcm, n_samples, out);
+    free(filt);
+    return rc;
+}
+
 int wo_mel(int n_mels, const float* pcm, int n_samples, int mode, float* out) {
     if (n_samples < 0 || n_samples > CHUNK) return -1;
     init_tables();
@@ -165,47 +223,13 @@ int wo_mel(int n_mels, const float* pcm, int n_samples, int mode, float* out) {
     wo_mel_filters(n_mels, filt);
     int rc = 0;
     if (mode == WO_MEL_WHISPER_CPP) {
-        /* samples_padded = [reflect 200][x][zeros 480000 + 200] */
-        const long n_pad = (long)n_samples + CHUNK + 2 * (N_FFT / 2);
-        float* sp = (float*)calloc(n_pad, sizeof(float));
-        memcpy(sp + N_FFT / 2, pcm, sizeof(float) * n_samples);
-        for (int i = 0; i < N_FFT / 2; i++) {
-            int src = N_FFT / 2 - i; /* reverse_copy(samples+1, samples+1+200) */
-            sp[i] = src < n_samples ? pcm[src] : 0.0f;
-        }
-        const int n_len = (int)((n_pad - N_FFT) / HOP);
-        const int n_sig = n_samples + N_FFT / 2;
-        int n_comp = n_sig / HOP + 1;
-        if (n_comp > n_len) n_comp = n_len;
+        /* the first window of the whole-input log-mel (n_len >= 3000 frames) */
+        const int n_len = wo_mel_len(n_samples);
         float* mel = (float*)malloc(sizeof(float) * (size_t)n_mels * n_len);
-        #pragma omp parallel
-        {
-            float fin[2 * N_FFT], fout[8 * N_FFT], col[256];
-            #pragma omp for schedule(static)
-            for (int i = 0; i < n_len; i++) {
-                if (i < n_comp) {
-                    const int off = i * HOP;
-                    int nv = n_sig - off;
-                    if (nv > N_FFT) nv = N_FFT;
-                    mel_frame(filt, n_mels, sp + off, nv, fin, fout, col);
-                    for (int j = 0; j < n_mels; j++) mel[(size_t)j * n_len + i] = col[j];
-                } else {
-                    for (int j = 0; j < n_mels; j++) mel[(size_t)j * n_len + i] = (float)log10(1e-10);
-                }
-            }
-        }
-        double mmax = -1e20;
-        for (size_t i = 0; i < (size_t)n_mels * n_len; i++)
-            if (mel[i] > mmax) mmax = mel[i];
-        mmax -= 8.0;
-        for (int j = 0; j < n_mels; j++)
-            for (int i = 0; i < N_FRAMES; i++) {
-                float v = i < n_len ? mel[(size_t)j * n_len + i] : 0.0f;
-                if (v < mmax) v = (float)mmax;
-                out[j * N_FRAMES + i] = (float)((v + 4.0) / 4.0);
-            }
+        rc = mel_whole(n_mels, filt, pcm, n_samples, mel);
+        for (int j = 0; rc == 0 && j < n_mels; j++)
+            memcpy(out + (size_t)j * N_FRAMES, mel + (size_t)j * n_len, sizeof(float) * N_FRAMES);
         free(mel);
-        free(sp);
     } else if (mode == WO_MEL_HF) {
         /* HF: pad/truncate to 480000, centre reflect pad 200 both sides, 3000 frames */
         const int n = CHUNK, pad = N_FFT / 2;

@@ -1,4 +1,4 @@
-//! Raw bindings to `include/spittle_hip.h` (ABI 10), the C boundary of the MI355X-native Whisper
+//! Raw bindings to `include/spittle_hip.h` (ABI 11), the C boundary of the MI355X-native Whisper
 //! and Parakeet-V3 backend.  One item per declaration of the header, same names, same layouts (x86-64 SysV; the
 //! layouts are checked field by field against gcc by tests/test_capi.py).  Safe wrappers live in
 //! the `spittle-hip` crate.
@@ -6,7 +6,7 @@
 
 use std::os::raw::{c_char, c_int, c_void};
 
-pub const SPT_ABI_VERSION: c_int = 10;
+pub const SPT_ABI_VERSION: c_int = 11;
 pub const SPT_PK_STAGE_COUNT: c_int = 9;
 
 pub type spt_status = c_int;
@@ -112,7 +112,8 @@ pub struct spt_call_stats {
     pub engine_calls: i32,
     pub decoder_passes: i32,
     pub beam_steps: i32,
-    pub reserved0: i32,
+    /// ABI 11: 30 s windows encoded (one per window, shared by fallbacks and decoders)
+    pub encoder_windows: i32,
     pub device_ms: f64,
     pub encoder_ms: f64,
     pub decode_ms: f64,
@@ -236,6 +237,7 @@ extern "C" {
     ) -> spt_status;
 
     pub fn spt_debug_mel(ctx: *mut spt_ctx, pcm16k: *const f32, n_samples: usize, out: *mut f32) -> spt_status;
+    pub fn spt_debug_mel_at(ctx: *mut spt_ctx, pcm16k: *const f32, n_samples: usize, seek: i32, out: *mut f32) -> spt_status;
     pub fn spt_debug_encode(ctx: *mut spt_ctx, mel: *const f32, out: *mut f32) -> spt_status;
     pub fn spt_debug_weight_checksum(ctx: *mut spt_ctx, tensor_id: i32, out2: *mut f64) -> spt_status;
     pub fn spt_debug_ggml_tokenize(

@@ -12,6 +12,6 @@ fi
 timeout -k 10 400 python -u bench.py "$@" > gpurun_out/bench_$TAG.log 2>&1 || { echo "bench failed"; tail -5 gpurun_out/bench_$TAG.log; exit 1; }
 tail -1 gpurun_out/bench_$TAG.log
 if [ -z "$SKIP_PROF" ]; then
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-app-latency --no-probe "$@" > gpurun_out/prof_$TAG.log 2>&1 || { echo "rocprof failed"; exit 1; }
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-app-latency --no-probe --no-turbo "$@" > gpurun_out/prof_$TAG.log 2>&1 || { echo "rocprof failed"; exit 1; }
 fi
 echo done

@@ -22,7 +22,7 @@ EXPORTS = [
     "spt_version", "spt_default_model_params", "spt_default_infer_params", "spt_ctx_create",
     "spt_ctx_destroy", "spt_last_error", "spt_ctx_info", "spt_transcribe", "spt_transcribe_batch",
     "spt_transcribe_batch_device", "spt_result_free", "spt_get_timings", "spt_get_call_stats", "spt_debug_mel",
-    "spt_debug_encode", "spt_debug_weight_checksum", "spt_probe_kernel", "spt_language_code",
+    "spt_debug_mel_at", "spt_debug_encode", "spt_debug_weight_checksum", "spt_probe_kernel", "spt_language_code",
     "spt_tokenize", "spt_token_to_str", "spt_debug_ggml_tokenize", "spt_debug_ggml_dequant",
     "spt_weights_export", "spt_weights_import", "spt_weights_arena", "spt_weights_commit",
     "spt_ctx_create_replicas", "spt_transcribe_batch_replicas",
@@ -91,7 +91,7 @@ class Timings(C.Structure):
 
 
 class CallStats(C.Structure):
-    _fields_ = [(n, C.c_int32) for n in ("engine_calls", "decoder_passes", "beam_steps", "reserved0")] + \
+    _fields_ = [(n, C.c_int32) for n in ("engine_calls", "decoder_passes", "beam_steps", "encoder_windows")] + \
                [(n, C.c_double) for n in ("device_ms", "encoder_ms", "decode_ms")]
 
 
@@ -179,6 +179,7 @@ def load():
     L.spt_get_timings.argtypes = [vp, C.POINTER(Timings)]
     L.spt_get_call_stats.argtypes = [vp, C.POINTER(CallStats)]
     L.spt_debug_mel.argtypes = [vp, fp, C.c_size_t, fp]
+    L.spt_debug_mel_at.argtypes = [vp, fp, C.c_size_t, C.c_int32, fp]
     L.spt_debug_encode.argtypes = [vp, fp, fp]
     L.spt_debug_weight_checksum.argtypes = [vp, C.c_int32, C.POINTER(C.c_double)]
     L.spt_probe_kernel.argtypes = [vp, C.c_int32, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_double),
@@ -258,7 +259,7 @@ def load():
             getattr(L, fn).restype = C.c_int
     for fn in ("spt_weights_arena", "spt_weights_commit", "spt_ctx_create_replicas", "spt_transcribe_batch_replicas",
                "spt_weights_export", "spt_weights_import", "spt_ctx_info", "spt_transcribe", "spt_transcribe_batch", "spt_transcribe_batch_device",
-               "spt_get_timings", "spt_get_call_stats", "spt_debug_mel", "spt_debug_encode", "spt_debug_weight_checksum",
+               "spt_get_timings", "spt_get_call_stats", "spt_debug_mel", "spt_debug_mel_at", "spt_debug_encode", "spt_debug_weight_checksum",
                "spt_probe_kernel", "spt_tokenize", "spt_debug_ggml_tokenize", "spt_debug_ggml_dequant"):
         getattr(L, fn).restype = C.c_int
     _lib = L

@@ -3,10 +3,10 @@
 // Mirrors transcribe-rs' WhisperEngine surface as Spittle uses it
 // (/root/reference/src-tauri/src/managers/transcription.rs: new + load_model 261-276,
 // transcribe_samples 494-503, unload_model 175-208): status codes + message,
-// borrowed input PCM, library-owned results.  Utterances longer than 30 s are cut
-// into 30 s windows that are decoded as independent batch items and their text is
-// concatenated (whisper.cpp's seek loop conditions each window on the previous
-// text and timestamps; that is a documented difference).
+// borrowed input PCM, library-owned results.  On the fast path an utterance longer than
+// 30 s is decoded as 30 s windows of its whole log-mel (frames 3000 k ..), independent
+// batch items whose text is concatenated (whisper.cpp's seek loop also conditions each
+// window on the previous text: a documented difference).
 #include <hip/hip_runtime.h>
 #include <string.h>
 
@@ -260,11 +260,13 @@ spt_status run_full(spt_ctx* c, const float* const* pcm, const size_t* n_samples
     return SPT_OK;
 }
 
-// shared driver: windows (device or host) -> per-utterance results
-struct Window { int utt; const float* host; const float* dev; int n; };
+// shared driver: 30 s windows of host utterances -> per-utterance results.  Window k of an
+// utterance starts at frame 3000 k of the utterance's whole log-mel (whisper_full with
+// no_timestamps advances seek by 3000 frames per window).
+struct Window { int utt; int seek; };
 
-spt_status run_windows(spt_ctx* c, std::vector<Window>& win, size_t n_utt, const spt_infer_params* p,
-                       spt_result** out) {
+spt_status run_windows(spt_ctx* c, std::vector<Window>& win, const float* const* pcm, const size_t* n_samples,
+                       size_t n_utt, const spt_infer_params* p, spt_result** out) {
     spt::DecodeRequest rq;
     bool autolang = false;
     spt_status s = build_request(c, p, &rq, &autolang);
@@ -282,11 +284,18 @@ spt_status run_windows(spt_ctx* c, std::vector<Window>& win, size_t n_utt, const
     const int cap = e.max_batch();
     for (size_t g0 = 0; g0 < win.size(); g0 += cap) {
         const int B = (int)std::min<size_t>(cap, win.size() - g0);
-        std::vector<int> ns(B);
-        std::vector<const float*> hp(B);
+        // the utterances of this batch of windows, each log-mel computed whole (an utterance whose
+        // windows span two batches is loaded by both: the same bytes, the same mel)
+        std::vector<const float*> up;
+        std::vector<int> un, wu(B), ws(B);
         for (int b = 0; b < B; ++b) {
-            ns[b] = win[g0 + b].n;
-            hp[b] = win[g0 + b].host;
+            const int u = win[g0 + b].utt;
+            if (b == 0 || win[g0 + b - 1].utt != u) {
+                up.push_back(pcm[u]);
+                un.push_back((int)n_samples[u]);
+            }
+            wu[b] = (int)up.size() - 1;
+            ws[b] = win[g0 + b].seek;
         }
         if (autolang) {
             rq.lang_tok.assign(B, 0);
@@ -300,12 +309,9 @@ spt_status run_windows(spt_ctx* c, std::vector<Window>& win, size_t n_utt, const
         }
         std::vector<int> otok((size_t)B * rq.n_steps), lang(B, -1);
         std::vector<float> o1((size_t)B * rq.n_steps), o2((size_t)B * rq.n_steps);
-        if (win[g0].dev) {
-            // device windows are laid out contiguously by the caller (stride in Window.n is the slot)
-            e.transcribe_device(win[g0].dev, kWindow, ns.data(), B, rq, otok.data(), o1.data(), o2.data(), lang.data());
-        } else {
-            e.transcribe_host(hp.data(), ns.data(), B, rq, otok.data(), o1.data(), o2.data(), lang.data());
-        }
+        e.load_utterances(up.data(), un.data(), (int)up.size());
+        e.encode_windows(wu.data(), ws.data(), B);
+        e.decode(B, rq, otok.data(), o1.data(), o2.data(), lang.data());
         for (int b = 0; b < B; ++b) {
             const int u = win[g0 + b].utt;
             if (utt_lang[u] < 0) utt_lang[u] = lang[b];
@@ -335,7 +341,7 @@ spt_status run_windows(spt_ctx* c, std::vector<Window>& win, size_t n_utt, const
 
 extern "C" {
 
-const char* spt_version(void) { return "spittle_amd 0.10.0 (gfx950, ABI 10)"; }
+const char* spt_version(void) { return "spittle_amd 0.11.0 (gfx950, ABI 11)"; }
 
 const char* spt_language_code(int32_t lang_id) { return spt::lang_code(lang_id); }
 
@@ -470,15 +476,15 @@ spt_status spt_transcribe_batch(spt_ctx* ctx, const float* const* pcm, const siz
         out[u] = nullptr;
         if (n_samples[u] == 0) { empty.push_back(u); continue; }  // "" without an engine call
         if (!pcm[u]) return fail(ctx, SPT_ERR_INVALID_ARG, "null pcm");
-        for (size_t o = 0; o < n_samples[u]; o += kWindow)
-            win.push_back(Window{(int)u, pcm[u] + o, nullptr, (int)std::min<size_t>(kWindow, n_samples[u] - o)});
+        if (n_samples[u] > (size_t)INT32_MAX / 2) return fail(ctx, SPT_ERR_INVALID_ARG, "utterance too long");
+        for (size_t o = 0; o < n_samples[u]; o += kWindow) win.push_back(Window{(int)u, (int)(o / 160)});
     }
     try {
         spt_status s = SPT_OK;
         if (!win.empty()) {
             // results for non-empty utterances
             std::vector<spt_result*> tmp(batch, nullptr);
-            s = run_windows(ctx, win, batch, params, tmp.data());
+            s = run_windows(ctx, win, pcm, n_samples, batch, params, tmp.data());
             if (s != SPT_OK) return s;
             for (size_t u = 0; u < batch; ++u) out[u] = tmp[u];
         }
@@ -595,7 +601,7 @@ spt_status spt_get_call_stats(const spt_ctx* ctx, spt_call_stats* s) {
     if (!ctx || !s) return SPT_ERR_INVALID_ARG;
     const spt::CallStats& c = ctx->eng->call_stats();
     s->engine_calls = c.engine_calls; s->decoder_passes = c.decoder_passes; s->beam_steps = c.beam_steps;
-    s->reserved0 = 0;
+    s->encoder_windows = c.encoder_windows;
     s->device_ms = c.device_ms; s->encoder_ms = c.encoder_ms; s->decode_ms = c.decode_ms;
     return SPT_OK;
 }
@@ -623,8 +629,14 @@ spt_status spt_weights_import(spt_ctx* ctx, const void* dev_src, size_t bytes) {
 spt_status spt_debug_mel(spt_ctx* ctx, const float* pcm16k, size_t n_samples, float* out) {
     if (!ctx || !out || (n_samples && !pcm16k)) return fail(ctx, SPT_ERR_INVALID_ARG, "null argument");
     if (n_samples > (size_t)kWindow) return fail(ctx, SPT_ERR_INVALID_ARG, "window longer than 30 s");
+    return spt_debug_mel_at(ctx, pcm16k, n_samples, 0, out);
+}
+
+spt_status spt_debug_mel_at(spt_ctx* ctx, const float* pcm16k, size_t n_samples, int32_t seek, float* out) {
+    if (!ctx || !out || (n_samples && !pcm16k)) return fail(ctx, SPT_ERR_INVALID_ARG, "null argument");
+    if (n_samples > (size_t)INT32_MAX / 2) return fail(ctx, SPT_ERR_INVALID_ARG, "utterance too long");
     try {
-        ctx->eng->debug_mel(pcm16k, (int)n_samples, out);
+        ctx->eng->debug_mel(pcm16k, (int)n_samples, seek, out);
         return SPT_OK;
     } catch (const std::exception& e) {
         return fail(ctx, classify(e), e.what());

@@ -104,7 +104,7 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     // a kernel template constant.
     select();
     HIP_CHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
-    ev_.resize(10);  // 0-5 phases, 6-7 PCM staging, 8-9 a beam step
+    ev_.resize(12);  // 0-1 mel, 2-5 window / encoder / cross K/V, 6-7 decode, 8-9 a beam step, 10-11 H2D
     for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
     // a decoder pass stages at most max_rows_ rows in its LayerNorm GEMVs' LDS images; a batch
     // above that is decoded as several groups (each sized for the whole batch, re-sliced per call)
@@ -152,6 +152,12 @@ void Engine::release() {
     if (warena_) (void)hipFree(warena_);
     if (aarena_) (void)hipFree(aarena_);
     if (kvtmp_) (void)hipFree(kvtmp_);
+    for (void* p : {(void*)upcm_, (void*)umel_, (void*)uinfo_})
+        if (p) (void)hipFree(p);
+    upcm_ = umel_ = nullptr;
+    uinfo_ = nullptr;
+    upcm_cap_ = umel_cap_ = 0;
+    uinfo_cap_ = 0;
     for (void* p : {(void*)hann_, (void*)sinv_, (void*)cosv_, (void*)filt_, (void*)grp_})
         if (p) (void)hipFree(p);
     for (auto& e : ev_) (void)hipEventDestroy(e);
@@ -541,10 +547,8 @@ void Engine::alloc_workspace() {
     for (int pass = 0; pass < 2; ++pass) {
         Carver c{pass ? aarena_ : nullptr};
         auto A = [&](int64_t n) { return c.take(n * esz_); };
-        pcm_ = (float*)c.take(B * 480000 * 4);
-        nsamp_ = (int*)c.take(B * 4);
-        mel_raw_ = (float*)c.take(B * MEL_ROWS * dm_.n_mels * 4);
-        mel_max_ = (unsigned*)c.take(B * 4);
+        win_utt_ = (int*)c.take(B * 4);
+        win_seek_ = (int*)c.take(B * 4);
         mel_in_ = A(B * MEL_ROWS * cp_);
         y1p_ = A(B * MEL_ROWS * d);
         x_ = (float*)c.take(B * T * d * 4);
@@ -587,6 +591,7 @@ void Engine::alloc_workspace() {
             g.cand_id = (int*)c.take(B * 8 * 4);
             g.cand_lp = (float*)c.take(B * 8 * 4);
             g.beam_tid = (int*)c.take(B * 4);
+            g.kvrow = (int*)c.take(B * 4);
         }
         zero_ = (float*)c.take(R * d * 4);  // never written: the "no pending slab" operand
         if (!pass) {
@@ -602,10 +607,137 @@ void Engine::alloc_workspace() {
 }
 
 // ----------------------------------------------------------------------------- pipeline
-void Engine::run_mel(const float* pcm_dev, int64_t stride, int B, float* dbg) {
+// ----------------------------------------------------------------------------- utterances
+// a device buffer of at least `need` elements (grown by a quarter at a time; the old contents are
+// not kept).  Only between calls: everything on the engine's streams has finished.
+void Engine::ensure_capacity(void** p, int64_t* cap, int64_t need, size_t esz, const char* what) {
+    if (need <= *cap) return;
+    const int64_t want = std::max<int64_t>(need, *cap + *cap / 4);
+    HIP_CHECK(hipDeviceSynchronize());
+    if (*p) HIP_CHECK(hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc(p, (size_t)want * esz) != hipSuccess) {
+        *p = nullptr;
+        (void)hipGetLastError();
+        throw std::runtime_error(std::string("out of device memory for ") + what + " (" +
+                                 std::to_string((size_t)want * esz) + " B)");
+    }
+    *cap = want;
+}
+
+// whisper_pcm_to_mel of each whole utterance (k_mel.hip): pcm + pcm_off[u], n[u] samples each
+void Engine::run_mel_utts(const float* pcm, const std::vector<int64_t>& pcm_off, const int* n, int U) {
+    if (U < 1) throw std::runtime_error("no utterances");
+    int64_t rows = 0;
+    int max_rows = 0;
+    uhost_.assign((size_t)U * 3, 0);  // pcm_off | row_off | n (as int64, unpacked on upload)
+    for (int u = 0; u < U; ++u) {
+        if (n[u] < 0) throw std::runtime_error("negative sample count");
+        const int r = mel_rows(n[u]);
+        uhost_[u] = pcm_off[u];
+        uhost_[U + u] = rows;
+        rows += r;
+        max_rows = std::max(max_rows, r);
+    }
+    void* pm = umel_;
+    ensure_capacity(&pm, &umel_cap_, std::max<int64_t>(rows, 1), (size_t)dm_.n_mels * 4, "the utterance log-mel");
+    umel_ = (float*)pm;
+    // info block: pcm_off [U] int64 | row_off [U] int64 | n [U] int | max [U] unsigned
+    const int64_t info_bytes = (int64_t)U * 24;
+    if (U > uinfo_cap_) {
+        int64_t cap = uinfo_cap_ ? (int64_t)uinfo_cap_ * 24 : 0;
+        void* pi = uinfo_;
+        ensure_capacity(&pi, &cap, info_bytes, 1, "utterance descriptors");
+        uinfo_ = (char*)pi;
+        uinfo_cap_ = (int)(cap / 24);
+    }
+    mel_img_.assign((size_t)info_bytes, 0);
+    memcpy(mel_img_.data(), uhost_.data(), (size_t)U * 16);
+    for (int u = 0; u < U; ++u) memcpy(mel_img_.data() + (size_t)U * 16 + 4 * u, &n[u], 4);
+    HIP_CHECK(hipMemcpyAsync(uinfo_, mel_img_.data(), (size_t)U * 20, hipMemcpyHostToDevice, st_));
+    mu_.pcm_off = (const int64_t*)uinfo_;
+    mu_.row_off = (const int64_t*)(uinfo_ + (size_t)U * 8);
+    mu_.n = (const int*)(uinfo_ + (size_t)U * 16);
+    umax_ = (unsigned*)(uinfo_ + (size_t)U * 20);
+    un_.assign(n, n + U);
+    HIP_CHECK(hipEventRecord(ev_[0], st_));
     MelTables t{hann_, sinv_, cosv_, filt_, grp_};
-    mel_frames(pcm_dev, stride, nsamp_, B, dm_.n_mels, t, mel_raw_, mel_max_, st_);
-    mel_norm(dt_, mel_raw_, mel_max_, nsamp_, B, dm_.n_mels, cp_, mel_in_, dbg, st_);
+    mel_frames(pcm, mu_, U, max_rows, dm_.n_mels, t, umel_, umax_, st_);
+    HIP_CHECK(hipEventRecord(ev_[1], st_));
+    mel_pending_ = true;
+    enc_E_ = 0;  // windows of an earlier set refer to its utterances
+}
+
+void Engine::load_utterances(const float* const* pcm, const int* n, int U) {
+    select();
+    require_weights();
+    std::vector<int64_t> off(U);
+    int64_t tot = 0;
+    for (int u = 0; u < U; ++u) {
+        if (n[u] < 0) throw std::runtime_error("negative sample count");
+        if (n[u] > 0 && !pcm[u]) throw std::runtime_error("null pcm");
+        off[u] = tot;
+        tot += n[u];
+    }
+    void* pp = upcm_;
+    ensure_capacity(&pp, &upcm_cap_, std::max<int64_t>(tot, 1), 4, "utterance PCM");
+    upcm_ = (float*)pp;
+    HIP_CHECK(hipEventRecord(ev_[10], st_));
+    for (int u = 0; u < U; ++u)
+        if (n[u] > 0)
+            HIP_CHECK(hipMemcpyAsync(upcm_ + off[u], pcm[u], (size_t)n[u] * 4, hipMemcpyHostToDevice, st_));
+    HIP_CHECK(hipEventRecord(ev_[11], st_));
+    HIP_CHECK(hipEventSynchronize(ev_[11]));  // pageable sources: the caller may reuse them on return
+    float ms;
+    HIP_CHECK(hipEventElapsedTime(&ms, ev_[10], ev_[11]));
+    tm_.h2d_ms = ms;
+    run_mel_utts(upcm_, off, n, U);
+}
+
+void Engine::load_utterances_device(const float* pcm_dev, int64_t stride, const int* n, int U) {
+    select();
+    require_weights();
+    std::vector<int64_t> off(U);
+    for (int u = 0; u < U; ++u) {
+        if (n[u] < 0 || (int64_t)n[u] > stride) throw std::runtime_error("each utterance must hold 0..stride samples");
+        off[u] = (int64_t)u * stride;
+    }
+    tm_.h2d_ms = 0.0;
+    run_mel_utts(pcm_dev, off, n, U);
+}
+
+void Engine::upload_windows(const int* utt, const int* seek, int E) {
+    if (E < 1 || E > max_batch_) throw std::runtime_error("encoder windows must be 1..max_batch");
+    if (un_.empty()) throw std::runtime_error("encode_windows before load_utterances");
+    whost_.assign((size_t)2 * E, 0);
+    for (int e = 0; e < E; ++e) {
+        if (utt[e] < 0 || utt[e] >= (int)un_.size()) throw std::runtime_error("window of an unknown utterance");
+        // whisper_full only encodes at seek < n_len_org <= n / 160 + 1, so the 3000 frames lie
+        // inside the (n + 480000) / 160 of the utterance's mel
+        const int n_len = (int)(((int64_t)un_[utt[e]] + 480000) / 160);
+        if (seek[e] < 0 || seek[e] + 3000 > n_len) throw std::runtime_error("window past the end of its utterance");
+        whost_[e] = utt[e];
+        whost_[E + e] = seek[e];
+    }
+    HIP_CHECK(hipMemcpyAsync(win_utt_, whost_.data(), (size_t)E * 4, hipMemcpyHostToDevice, st_));
+    HIP_CHECK(hipMemcpyAsync(win_seek_, whost_.data() + E, (size_t)E * 4, hipMemcpyHostToDevice, st_));
+}
+
+void Engine::encode_windows(const int* utt, const int* seek, int E) {
+    select();
+    require_weights();
+    upload_windows(utt, seek, E);
+    HIP_CHECK(hipEventRecord(ev_[2], st_));
+    mel_norm(dt_, umel_, umax_, mu_, win_utt_, win_seek_, E, dm_.n_mels, cp_, mel_in_, nullptr, st_);
+    HIP_CHECK(hipEventRecord(ev_[3], st_));
+    enqueue_encoder(E);
+    HIP_CHECK(hipEventRecord(ev_[4], st_));
+    run_cross_kv(E);
+    HIP_CHECK(hipEventRecord(ev_[5], st_));
+    enc_E_ = E;
+    enc_pending_ = true;
+    cs_.encoder_windows += E;
 }
 
 void Engine::run_encoder(int B) {
@@ -698,16 +830,20 @@ void Engine::run_cross_kv(int B) {
 // residual add: every workgroup of the LayerNorm GEMV after them re-reads the residual rows,
 // so slabs there cost more than they save (cross-out: +1.2 us per slab on fc1; self-out:
 // r1 exp24, in place +0.4 % RTFx over 2 slabs).
-void Engine::enqueue_decoder_pass(DecGroup& g, int B_total, int Tq, const DecodeRequest& rq, int out_cap) {
-    float* x = enqueue_layers(g, B_total, Tq);
+void Engine::enqueue_decoder_pass(DecGroup& g, int E, int Tq, const DecodeRequest& rq, int out_cap) {
+    float* x = enqueue_layers(g, E, Tq);
     enqueue_head(g, Tq, rq, out_cap, x, suppress_, (rq.flags & 1u) != 0);
 }
 
 // The decoder layers over this pass's Tq input rows per sequence (embedded in g.dx); returns
 // the residual buffer holding the result (plus g.pend's pending slabs, n = fc2's split).
-float* Engine::enqueue_layers(DecGroup& g, int B_total, int Tq) {
+float* Engine::enqueue_layers(DecGroup& g, int E, int Tq) {
     const int d = dm_.d, H = dm_.n_head, ctx = dm_.n_text_ctx, T = dm_.n_audio_ctx, B = g.B, R = B * Tq;
-    const int64_t self_layer = (int64_t)2 * B * H * ctx * 64, cross_layer = kv_layer_elems(B_total, H, T);
+    const int64_t self_layer = (int64_t)2 * B * H * ctx * 64, cross_layer = kv_layer_elems(E, H, T);
+    // window map: rows j * share .. + share - 1 attend to window g.kvrow[j * share]; without one,
+    // row b attends to window g.b0 + b (the cross-attention key split applies there only)
+    const bool mapped = g.share > 0;
+    const int xs = mapped ? 1 : xsplit_;
     const int ks = dt_ == DT_BF16 ? 128 : 64;
     hipStream_t st = g.st;
     float* xc = g.dx;   // current residual rows (dec_embed / dec_finalize wrote this pass's input here)
@@ -732,8 +868,9 @@ float* Engine::enqueue_layers(DecGroup& g, int B_total, int Tq) {
     for (int l = 0; l < dm_.n_dec; ++l) {
         const DecL& e = dec_[l];
         void* skv_l = (char*)g.skv + self_layer * l * esz_;
-        // this group's sequences inside the cross K/V of layer l (kv_offset layout, B_total sequences)
-        const void* ckv_l = (const char*)ckv_ + (cross_layer * l + (int64_t)g.b0 * H * 4096) * esz_;
+        // layer l of the cross K/V (kv_offset layout, E windows), at this group's first window when
+        // the rows map to windows one to one
+        const void* ckv_l = (const char*)ckv_ + (cross_layer * l + (mapped ? 0 : (int64_t)g.b0 * H * 4096)) * esz_;
         // LN1 + QKV projection + self K/V append, then the self-attention
         {
             GemvArgs a{};
@@ -756,12 +893,13 @@ float* Engine::enqueue_layers(DecGroup& g, int B_total, int Tq) {
         a.W = e.cq_w; a.N = d; a.K = d; a.bias = e.cq_b; a.C = g.dq; a.ldc = d;
         gemv(dt_, GV_BIAS, A_LN, a, st);
         consumed();
-        dec_cross_attn(dt_, g.dq, ckv_l, B, B_total, H, T, Tq, g.dao, st, xsplit_, g.xpart);
+        dec_cross_attn(dt_, g.dq, ckv_l, B, E, H, T, Tq, g.dao, st, xs, g.xpart, mapped ? g.kvrow : nullptr,
+                       mapped ? g.share : 1);
         // cross output projection (merging the key chunks in its prologue), residual add in place
         a = GemvArgs{};
         a.A = g.dao; a.lda = d; a.R = R; a.W = e.co_w; a.N = d; a.K = d; a.bias = e.co_b; a.C = xc; a.ldc = d;
-        if (xsplit_ > 1) { a.apart = g.xpart; a.a_splits = xsplit_; a.a_heads = H; }
-        gemv(dt_, GV_BIAS_RESID, xsplit_ > 1 ? A_ATTN : A_DIRECT, a, st);
+        if (xs > 1) { a.apart = g.xpart; a.a_splits = xs; a.a_heads = H; }
+        gemv(dt_, GV_BIAS_RESID, xs > 1 ? A_ATTN : A_DIRECT, a, st);
         // LN3 + fc1 + GELU
         a = GemvArgs{};
         ln_input(a); a.lda = d; a.ln_w = e.ln3_w; a.ln_b = e.ln3_b; a.R = R;
@@ -838,13 +976,33 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
     const int ctx = dm_.n_text_ctx;
     const int P = rq.row_prefix.empty() ? (int)rq.prefix.size() : (int)rq.row_prefix[0].size();
     if (Tq < 1 || Tq > 4) throw std::runtime_error("prompt must have 1..4 tokens");
-    if (B < 1 || B > 64) throw std::runtime_error("batch out of range");
+    if (B < 1 || B > max_batch_) throw std::runtime_error("batch out of range");
+    const int E = enc_E_;
+    if (E < 1) throw std::runtime_error("decode before encode_windows");
+    // the rows' window map: S = rows per window (consecutive runs of equal length), 0 = none
+    int S = 0;
+    if (!rq.kv_row.empty()) {
+        if ((int)rq.kv_row.size() != B) throw std::runtime_error("kv_row needs one window per row");
+        for (int v : rq.kv_row)
+            if (v < 0 || v >= E) throw std::runtime_error("kv_row names a window that was not encoded");
+        S = 1;
+        for (int sh = std::min(8, B); sh > 1 && S == 1; --sh) {
+            if (B % sh) continue;
+            bool ok = true;
+            for (int b = 0; b < B && ok; ++b) ok = rq.kv_row[b] == rq.kv_row[b - b % sh];
+            if (ok) S = sh;
+        }
+    } else if (B > E) {
+        throw std::runtime_error("more decoder rows than encoded windows (and no kv_row map)");
+    }
     // decoder passes carry at most max_rows_ rows: a batch above that is split over decode
-    // groups, and a group whose prompt rows exceed it prefills the prompt a chunk of tokens at a
-    // time (the same rows, positions and keys) and runs the logits pass on the last prompt token
-    // alone
-    const int G = std::min((int)groups_.size(), std::max(std::min(n_groups_, B), cdiv(B, max_rows_)));
-    const int Bg = cdiv(B, G);  // the largest group
+    // groups (in whole windows of S rows), and a group whose prompt rows exceed it prefills the
+    // prompt a chunk of tokens at a time (the same rows, positions and keys) and runs the logits
+    // pass on the last prompt token alone
+    const int unit = std::max(1, S), nU = B / unit;
+    const int G = std::min((int)groups_.size(),
+                           std::max(std::min(n_groups_, nU), cdiv(nU, std::max(1, max_rows_ / unit))));
+    const int Bg = cdiv(nU, G) * unit;  // the largest group
     if (Bg > max_rows_) throw std::runtime_error("batch exceeds the decoder's rows per pass");
     const int cmax = std::max(1, std::min(4, max_rows_ / Bg));
     const int Tq_head = Bg * Tq > max_rows_ ? 1 : Tq;
@@ -888,13 +1046,17 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
     // split the batch over the decode groups; each waits for the encoder / cross-K/V
     HIP_CHECK(hipEventRecord(ev_[6], st_));
     std::vector<DecGroup*> act;
+    kvrow_host_ = rq.kv_row;  // host source of the asynchronous uploads below
     for (int gi = 0, b0 = 0; gi < G; ++gi) {
         DecGroup& g = groups_[gi];
         g.b0 = b0;
-        g.B = B / G + (gi < B % G ? 1 : 0);
+        g.B = (nU / G + (gi < nU % G ? 1 : 0)) * unit;
+        g.share = S;
         b0 += g.B;
         act.push_back(&g);
         HIP_CHECK(hipStreamWaitEvent(g.st, ev_[6], 0));
+        if (S > 0)
+            HIP_CHECK(hipMemcpyAsync(g.kvrow, kvrow_host_.data() + g.b0, (size_t)g.B * 4, hipMemcpyHostToDevice, g.st));
         // host sources of this call's token uploads (kept alive in the group until the next call)
         g.host_tok.assign((size_t)g.B * (P + Tq + 8), 0);
         g.host_used = 0;
@@ -946,7 +1108,7 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
             reset_outputs(*g);
             upload_tokens(*g, [&](int, int) { return sp.sot; }, 1);
             dec_embed(dt_, g->tok_in, g->B, 1, dm_.d, tok_emb_, dec_pos_, g->ds, g->dx, g->st);
-            float* x = enqueue_layers(*g, B, 1);
+            float* x = enqueue_layers(*g, E, 1);
             enqueue_head(*g, 1, dq, out_cap, x, suppress_lang_, false);
         }
         std::vector<int> first((size_t)B * out_cap);
@@ -976,7 +1138,7 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
             const int n = std::min(cmax, P - c0);
             upload_tokens(g, [&](int b, int t) { return rows ? rq.row_prefix[b][c0 + t] : rq.prefix[c0 + t]; }, n);
             dec_embed(dt_, g.tok_in, g.B * n, n, dm_.d, tok_emb_, dec_pos_, g.ds, g.dx, g.st);
-            enqueue_layers(g, B, n);
+            enqueue_layers(g, E, n);
             dec_advance(g.ds, n, g.st);
         }
         auto prompt_tok = [&](int b, int t) { return (t == 1 && lang[b] >= 0) ? lang[b] : rq.prompt[t]; };
@@ -984,7 +1146,7 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
             const int n = std::min(cmax, Tq - Tq_head - c0);
             upload_tokens(g, [&](int b, int t) { return prompt_tok(b, c0 + t); }, n);
             dec_embed(dt_, g.tok_in, g.B * n, n, dm_.d, tok_emb_, dec_pos_, g.ds, g.dx, g.st);
-            enqueue_layers(g, B, n);
+            enqueue_layers(g, E, n);
             dec_advance(g.ds, n, g.st);
         }
         upload_tokens(g, [&](int b, int t) { return prompt_tok(b, Tq - Tq_head + t); }, Tq_head);
@@ -995,7 +1157,7 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
             HIP_CHECK(hipMemcpyAsync(g.beam_row, beam_host_.data(), (size_t)g.B * 16, hipMemcpyHostToDevice, g.st));
             HIP_CHECK(hipMemcpyAsync(g.beam_step, beam_host_.data() + (size_t)g.B * 4, 4, hipMemcpyHostToDevice, g.st));
         }
-        enqueue_decoder_pass(g, B, Tq_head, rq, out_cap);  // prompt pass produces token 0
+        enqueue_decoder_pass(g, E, Tq_head, rq, out_cap);  // prompt pass produces token 0
     }
     if (rq.beam_k > 0) {  // beam search continues step by step from the host (beam_next)
         tm_.n_decode_passes = 1;
@@ -1011,7 +1173,7 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
     if (rq.n_steps > 1 && no_graph) {
         for (int s = 1; s < rq.n_steps; ++s, ++passes)
             for (DecGroup* g : act) {
-                enqueue_decoder_pass(*g, B, 1, rq, out_cap);
+                enqueue_decoder_pass(*g, E, 1, rq, out_cap);
                 if (!sync_debug) continue;
                 const hipError_t e = hipStreamSynchronize(g->st);
                 DecState h{};
@@ -1023,13 +1185,15 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
     } else if (rq.n_steps > 1) {
         std::vector<hipGraphExec_t> ex;
         for (DecGroup* g : act) {
-            // B_total and b0 are baked into the captured cross-K/V addresses
-            const GraphKey key{g->B, B, g->b0, out_cap, rq.n_forced, rq.flags, rq.full};
+            // E and b0 are baked into the captured cross-K/V addresses, the window map's share
+            // into the cross-attention grid (the map itself is read from g->kvrow)
+            GraphKey key{g->B, E, g->b0, out_cap, rq.n_forced, rq.flags, rq.full};
+            key.share = S;
             auto it = g->graphs.find(key);
             if (it == g->graphs.end()) {
                 hipGraph_t graph;
                 HIP_CHECK(hipStreamBeginCapture(g->st, hipStreamCaptureModeThreadLocal));
-                enqueue_decoder_pass(*g, B, 1, rq, out_cap);
+                enqueue_decoder_pass(*g, E, 1, rq, out_cap);
                 HIP_CHECK(hipStreamEndCapture(g->st, &graph));
                 hipGraphExec_t exec;
                 HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
@@ -1068,65 +1232,80 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
     }
 }
 
+void Engine::decode(int B, const DecodeRequest& rq, int* tokens, float* top1, float* top2, int* lang_out,
+                    int* ts_state_out) {
+    select();
+    require_weights();
+    HIP_CHECK(hipEventRecord(ev_[6], st_));  // the decode groups wait for the encoded windows here
+    run_decode(B, rq, tokens, top1, top2, lang_out, ts_state_out);
+    HIP_CHECK(hipEventRecord(ev_[7], st_));
+    HIP_CHECK(hipStreamSynchronize(st_));
+    HIP_CHECK(hipGetLastError());
+    tm_.batch = B;
+    cs_.engine_calls++;
+    cs_.decoder_passes += tm_.n_decode_passes;
+    finish_call_timing();
+}
+
+// phase times of the stages since the last decode (HIP events; read after its synchronisation)
+void Engine::finish_call_timing() {
+    float ms;
+    HIP_CHECK(hipEventElapsedTime(&ms, ev_[6], ev_[7]));
+    tm_.decode_ms = ms;
+    double total = ms;
+    if (enc_pending_) {
+        float m_norm, m_enc, m_kv;
+        HIP_CHECK(hipEventElapsedTime(&m_norm, ev_[2], ev_[3]));
+        HIP_CHECK(hipEventElapsedTime(&m_enc, ev_[3], ev_[4]));
+        HIP_CHECK(hipEventElapsedTime(&m_kv, ev_[4], ev_[5]));
+        tm_.encoder_ms = m_enc;
+        tm_.cross_kv_ms = m_kv;
+        tm_.mel_ms = m_norm;
+        cs_.encoder_ms += m_enc;
+        total += m_norm + m_enc + m_kv;
+    } else {
+        tm_.encoder_ms = tm_.cross_kv_ms = tm_.mel_ms = 0.0;
+    }
+    if (mel_pending_) {
+        HIP_CHECK(hipEventElapsedTime(&ms, ev_[0], ev_[1]));
+        tm_.mel_ms += ms;
+        total += ms;
+    }
+    // the stages of one transcribe_* call run back to back on one stream: their span
+    if (mel_pending_ && enc_pending_) {
+        HIP_CHECK(hipEventElapsedTime(&ms, ev_[0], ev_[7]));
+        total = ms;
+    }
+    tm_.total_ms = total;
+    cs_.device_ms += total;
+    cs_.decode_ms += tm_.decode_ms;
+    mel_pending_ = enc_pending_ = false;
+}
+
 void Engine::transcribe_device(const float* pcm_dev, int64_t stride, const int* n_samples, int B,
                                const DecodeRequest& rq, int* tokens, float* top1, float* top2, int* lang_out,
                                int* ts_state_out) {
-    select();
-    require_weights();
     if (B < 1 || B > max_batch_) throw std::runtime_error("batch exceeds the context's max_batch");
     for (int b = 0; b < B; ++b)
         if (n_samples[b] < 0 || n_samples[b] > 480000 || (int64_t)n_samples[b] > stride)
             throw std::runtime_error("each window must hold 0..480000 samples within its stride");
-    HIP_CHECK(hipEventRecord(ev_[0], st_));
-    HIP_CHECK(hipMemcpyAsync(nsamp_, n_samples, B * 4, hipMemcpyHostToDevice, st_));
-    HIP_CHECK(hipEventRecord(ev_[1], st_));
-    run_mel(pcm_dev, stride, B, nullptr);
-    HIP_CHECK(hipEventRecord(ev_[2], st_));
-    enqueue_encoder(B);
-    HIP_CHECK(hipEventRecord(ev_[3], st_));
-    run_cross_kv(B);
-    HIP_CHECK(hipEventRecord(ev_[4], st_));
-    run_decode(B, rq, tokens, top1, top2, lang_out, ts_state_out);
-    HIP_CHECK(hipEventRecord(ev_[5], st_));
-    HIP_CHECK(hipStreamSynchronize(st_));
-    HIP_CHECK(hipGetLastError());
-    float ms;
-    const double h2d = tm_.h2d_ms;
-    HIP_CHECK(hipEventElapsedTime(&ms, ev_[1], ev_[2])); tm_.mel_ms = ms;
-    HIP_CHECK(hipEventElapsedTime(&ms, ev_[2], ev_[3])); tm_.encoder_ms = ms;
-    HIP_CHECK(hipEventElapsedTime(&ms, ev_[3], ev_[4])); tm_.cross_kv_ms = ms;
-    HIP_CHECK(hipEventElapsedTime(&ms, ev_[4], ev_[5])); tm_.decode_ms = ms;
-    HIP_CHECK(hipEventElapsedTime(&ms, ev_[0], ev_[5])); tm_.total_ms = ms;
-    tm_.h2d_ms = h2d;
-    tm_.batch = B;
-    cs_.engine_calls++;
-    cs_.decoder_passes += tm_.n_decode_passes;
-    cs_.device_ms += tm_.total_ms;
-    cs_.encoder_ms += tm_.encoder_ms;
-    cs_.decode_ms += tm_.decode_ms;
-}
-
-void Engine::stage_pcm(const float* const* pcm, const int* n, int B) {
-    HIP_CHECK(hipEventRecord(ev_[6], st_));
-    for (int b = 0; b < B; ++b) {
-        if (n[b] < 0 || n[b] > 480000) throw std::runtime_error("window longer than 30 s");
-        if (n[b] > 0)
-            HIP_CHECK(hipMemcpyAsync(pcm_ + (size_t)b * 480000, pcm[b], (size_t)n[b] * 4, hipMemcpyHostToDevice, st_));
-    }
-    HIP_CHECK(hipEventRecord(ev_[7], st_));
-    HIP_CHECK(hipEventSynchronize(ev_[7]));
-    float ms;
-    HIP_CHECK(hipEventElapsedTime(&ms, ev_[6], ev_[7]));
-    tm_.h2d_ms = ms;
+    load_utterances_device(pcm_dev, stride, n_samples, B);
+    std::vector<int> utt(B), seek(B, 0);
+    for (int b = 0; b < B; ++b) utt[b] = b;
+    encode_windows(utt.data(), seek.data(), B);
+    decode(B, rq, tokens, top1, top2, lang_out, ts_state_out);
 }
 
 void Engine::transcribe_host(const float* const* pcm, const int* n_samples, int B, const DecodeRequest& rq,
                              int* tokens, float* top1, float* top2, int* lang_out, int* ts_state_out) {
-    select();
-    require_weights();
     if (B < 1 || B > max_batch_) throw std::runtime_error("batch exceeds the context's max_batch");
-    stage_pcm(pcm, n_samples, B);
-    transcribe_device(pcm_, 480000, n_samples, B, rq, tokens, top1, top2, lang_out, ts_state_out);
+    for (int b = 0; b < B; ++b)
+        if (n_samples[b] < 0 || n_samples[b] > 480000) throw std::runtime_error("window longer than 30 s");
+    load_utterances(pcm, n_samples, B);
+    std::vector<int> utt(B), seek(B, 0);
+    for (int b = 0; b < B; ++b) utt[b] = b;
+    encode_windows(utt.data(), seek.data(), B);
+    decode(B, rq, tokens, top1, top2, lang_out, ts_state_out);
 }
 
 // ----------------------------------------------------------------------------- beam search
@@ -1141,8 +1320,7 @@ void Engine::read_cands(int B, BeamCands* out) {
     HIP_CHECK(hipStreamSynchronize(g.st));
 }
 
-void Engine::beam_begin(const float* const* pcm, const int* n_samples, int B, const DecodeRequest& rq, BeamCands* out,
-                        int* lang_out) {
+void Engine::beam_begin(int B, const DecodeRequest& rq, BeamCands* out, int* lang_out) {
     select();
     require_weights();
     if (rq.beam_k < 1 || rq.beam_k > 8) throw std::runtime_error("beam size must be in 1..8");
@@ -1160,7 +1338,7 @@ void Engine::beam_begin(const float* const* pcm, const int* n_samples, int B, co
     beam_rq_ = rq;
     beam_B_ = B;
     std::vector<int> tok((size_t)B * rq.n_steps);
-    transcribe_host(pcm, n_samples, B, rq, tok.data(), nullptr, nullptr, lang_out, nullptr);
+    decode(B, rq, tok.data(), nullptr, nullptr, lang_out, nullptr);
     std::vector<int> ident(B);
     for (int b = 0; b < B; ++b) ident[b] = b;
     HIP_CHECK(hipMemcpy(groups_[0].beam_ident, ident.data(), B * 4, hipMemcpyHostToDevice));
@@ -1192,7 +1370,7 @@ void Engine::beam_next(const int* src, const int* tokens, const int* rowstate, i
         dec_kv_gather(dt_, g.skv, kvtmp_, g.beam_src, dm_.n_dec, B, dm_.n_head, dm_.n_text_ctx, g.ds, g.st);
         dec_kv_gather(dt_, kvtmp_, g.skv, g.beam_ident, dm_.n_dec, B, dm_.n_head, dm_.n_text_ctx, g.ds, g.st);
         dec_embed(dt_, g.tok_in, B, 1, dm_.d, tok_emb_, dec_pos_, g.ds, g.dx, g.st);
-        float* x = enqueue_layers(g, B, 1);
+        float* x = enqueue_layers(g, enc_E_, 1);
         enqueue_head(g, 1, beam_rq_, beam_rq_.n_steps, x, suppress_, (beam_rq_.flags & 1u) != 0);
     };
     static const bool no_graph = getenv("SPT_NO_GRAPH") != nullptr;
@@ -1201,7 +1379,8 @@ void Engine::beam_next(const int* src, const int* tokens, const int* rowstate, i
         beam_pass();
     } else {
         // n_forced = -beam_k marks a beam-step graph (a real n_forced is >= 0)
-        const GraphKey key{B, B, 0, beam_rq_.n_steps, -beam_rq_.beam_k, beam_rq_.flags, beam_rq_.full};
+        GraphKey key{B, enc_E_, 0, beam_rq_.n_steps, -beam_rq_.beam_k, beam_rq_.flags, beam_rq_.full};
+        key.share = g.share;
         auto it = g.graphs.find(key);
         if (it == g.graphs.end()) {
             hipGraph_t graph;
@@ -1226,15 +1405,17 @@ void Engine::beam_next(const int* src, const int* tokens, const int* rowstate, i
 }
 
 // ----------------------------------------------------------------------------- debug hooks
-void Engine::debug_mel(const float* pcm_host, int n, float* out_host) {
+void Engine::debug_mel(const float* pcm_host, int n, int seek, float* out_host) {
     select();
     const float* p = pcm_host;
-    stage_pcm(&p, &n, 1);
-    HIP_CHECK(hipMemcpyAsync(nsamp_, &n, 4, hipMemcpyHostToDevice, st_));
+    load_utterances(&p, &n, 1);
+    const int u = 0;
+    upload_windows(&u, &seek, 1);
+    mel_pending_ = false;
     float* dbg = nullptr;
     const size_t bytes = (size_t)dm_.n_mels * 3000 * 4;
     HIP_CHECK(hipMalloc(&dbg, bytes));
-    run_mel(pcm_, 480000, 1, dbg);
+    mel_norm(dt_, umel_, umax_, mu_, win_utt_, win_seek_, 1, dm_.n_mels, cp_, mel_in_, dbg, st_);
     HIP_CHECK(hipMemcpyAsync(out_host, dbg, bytes, hipMemcpyDeviceToHost, st_));
     HIP_CHECK(hipStreamSynchronize(st_));
     HIP_CHECK(hipFree(dbg));
@@ -1279,8 +1460,8 @@ namespace spt {
 
 double Engine::probe(int kind, int iters, double* work, int* is_flops) {
     select();
-    const int B = tm_.batch;
-    if (B < 1) throw std::runtime_error("probe needs a completed transcription call first");
+    const int B = enc_E_;  // the encoded windows (cross K/V layout, encoder batch)
+    if (B < 1 || tm_.batch < 1) throw std::runtime_error("probe needs a completed transcription call first");
     if (iters < 1 || iters > 100000) throw std::runtime_error("iters out of range");
     const int d = dm_.d, H = dm_.n_head, T = dm_.n_audio_ctx, ctx = dm_.n_text_ctx, V = dm_.n_vocab;
     DecGroup& g = groups_[0];
@@ -1294,10 +1475,10 @@ double Engine::probe(int kind, int iters, double* work, int* is_flops) {
         case 0:  // cross-attention of layers 0..nl-1 (one launch each) over this group's cross K/V
             launch = [&] {
                 for (int l = 0; l < nl; ++l)
-                    dec_cross_attn(dt_, g.dq, (const char*)ckv_ + kv_layer_elems(B, H, T) * l * esz_, Bg, B, H,
-                                   T, 1, g.dao, st_, xsplit_, g.xpart);
+                    dec_cross_attn(dt_, g.dq, (const char*)ckv_ + kv_layer_elems(B, H, T) * l * esz_, std::min(Bg, B), B,
+                                   H, T, 1, g.dao, st_, xsplit_, g.xpart);
             };
-            *work = 2.0 * Bg * H * T * 64 * esz_;
+            *work = 2.0 * std::min(Bg, B) * H * T * 64 * esz_;
             break;
         case 1:
             launch = [&] { dec_self_attn(dt_, g.dq, g.skv, Bg, H, ctx, 1, g.ds, g.dao, st_); };

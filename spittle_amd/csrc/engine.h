@@ -42,6 +42,11 @@ struct DecodeRequest {
     std::vector<int> extra_suppress;           // e.g. the non-speech tokens of the vocabulary
     int blank_tok = 220;                       // " " (suppress_blank)
     int beam_k = 0;                            // > 0: beam search, host-driven (beam_begin / beam_next)
+    // per row: the encoded window (cross K/V row of the last encode_windows) it attends to; empty =
+    // row b attends to window b.  Rows sharing a window are consecutive runs of equal length (the
+    // decoders of one utterance: beam_size / best_of), so one workgroup reads a window's K/V once
+    // for all of them.
+    std::vector<int> kv_row;
 };
 
 // per-row beam candidates of one step (k <= 8 per row)
@@ -59,7 +64,7 @@ struct Timings {
 // everything one C-ABI call ran (a whisper_full call: every window batch, temperature fallback
 // and beam step), summed; reset by the C ABI at the start of each spt_transcribe* call
 struct CallStats {
-    int engine_calls = 0, decoder_passes = 0, beam_steps = 0;
+    int engine_calls = 0, decoder_passes = 0, beam_steps = 0, encoder_windows = 0;
     double device_ms = 0, encoder_ms = 0, decode_ms = 0;
 };
 
@@ -96,26 +101,43 @@ public:
     const CallStats& call_stats() const { return cs_; }
     void reset_call_stats() { cs_ = CallStats(); }
 
-    // pcm_dev: B windows of <= 480000 samples at pcm_dev + b * stride (device memory)
-    // tokens/top1/top2: host [B][n_steps]
-    // lang_out (optional, [B]): the language token each sequence was decoded with (-1: none)
-    // ts_state_out (optional, [B][4], whisper_full mode): has_ts, seek_delta, result_len, status
-    // (0 running, 1 completed, 2 failed) of each sequence's decoder
+    // ---- staged calls: utterances -> encoder windows -> decoder rows (whisper.cpp whisper_full:
+    // whisper_pcm_to_mel once per input, whisper_encode_internal once per window at `seek`, then
+    // the decoders of every temperature / beam share that window's cross K/V)
+    // 1. the log-mel of each WHOLE utterance on the device: 200-sample reflective head from the
+    //    utterance itself, (n + 480000) / 160 frames, the utterance's global max - 8 clamp.  Replaces
+    //    the previous set.  Host PCM is staged into a device buffer; device PCM is read in place
+    //    (utterance u at pcm_dev + u * stride, n[u] <= stride).
+    void load_utterances(const float* const* pcm_host, const int* n, int U);
+    void load_utterances_device(const float* pcm_dev, int64_t stride, const int* n, int U);
+    // 2. encoder rows e < E (<= max_batch): mel frames [seek[e], seek[e] + 3000) of utterance utt[e]
+    //    -> conv stem -> encoder -> cross K/V of every decoder layer; kept until the next call
+    void encode_windows(const int* utt, const int* seek, int E);
+    int encoded_windows() const { return enc_E_; }
+    // 3. decode B rows (<= max_batch) over the encoded windows (rq.kv_row).  tokens/top1/top2:
+    //    host [B][n_steps]; lang_out (optional, [B]): the language token each row was decoded with
+    //    (-1: none); ts_state_out (optional, [B][4], whisper_full mode): has_ts, seek_delta,
+    //    result_len, status (0 running, 1 completed, 2 failed) of each row's decoder
+    void decode(int B, const DecodeRequest& rq, int* tokens, float* top1, float* top2, int* lang_out = nullptr,
+                int* ts_state_out = nullptr);
+
+    // the three stages for B utterances that are one window each (seek 0), decoder row b on window b
+    // pcm_dev: B windows at pcm_dev + b * stride (device memory)
     void transcribe_device(const float* pcm_dev, int64_t stride, const int* n_samples, int B, const DecodeRequest& rq,
                            int* tokens, float* top1, float* top2, int* lang_out = nullptr, int* ts_state_out = nullptr);
-    // host PCM convenience (stages into the engine's pcm buffer)
     void transcribe_host(const float* const* pcm, const int* n_samples, int B, const DecodeRequest& rq, int* tokens,
                          float* top1, float* top2, int* lang_out = nullptr, int* ts_state_out = nullptr);
 
-    // beam search (whisper_full, beam strategy): mel, encoder, cross K/V, prefix and prompt pass
-    // of B decoder rows (rq.beam_k candidates each) -> the first step's candidates; then one
-    // step per call: row b continues row src[b]'s sequence with tokens[b]; rowstate [B][4] =
-    // last token, previous token, has_ts, seek_delta; step = index of the token being chosen
-    void beam_begin(const float* const* pcm, const int* n_samples, int B, const DecodeRequest& rq, BeamCands* out,
-                    int* lang_out);
+    // beam search (whisper_full, beam strategy) over the encoded windows: prefix and prompt pass of
+    // B decoder rows (rq.beam_k candidates each, rq.kv_row their windows) -> the first step's
+    // candidates; then one step per call: row b continues row src[b]'s sequence with tokens[b];
+    // rowstate [B][4] = last token, previous token, has_ts, seek_delta; step = index of the token
+    // being chosen
+    void beam_begin(int B, const DecodeRequest& rq, BeamCands* out, int* lang_out);
     void beam_next(const int* src, const int* tokens, const int* rowstate, int step, BeamCands* out);
 
-    void debug_mel(const float* pcm_host, int n, float* out_host);
+    // the normalised log-mel [n_mels][3000] of the window at frame `seek` of one utterance
+    void debug_mel(const float* pcm_host, int n, int seek, float* out_host);
     void debug_encode(const float* mel_host, float* out_host);
     bool debug_weight_checksum(int tid, double* out2);
     // re-launch one hot-path kernel on the last call's buffers; returns avg us per launch
@@ -126,9 +148,11 @@ private:
         int B, B_total, b0, out_cap, n_forced;
         uint32_t flags;
         bool full;
+        int share = 0;  // rows per window (0: identity rows, no window map)
         bool operator<(const GraphKey& o) const {
             if (full != o.full) return full < o.full;
             if (B != o.B) return B < o.B;
+            if (share != o.share) return share < o.share;
             if (B_total != o.B_total) return B_total < o.B_total;
             if (b0 != o.b0) return b0 < o.b0;
             if (out_cap != o.out_cap) return out_cap < o.out_cap;
@@ -159,6 +183,8 @@ private:
         int *beam_row = nullptr, *beam_step = nullptr, *beam_src = nullptr, *beam_ident = nullptr;  // beam search
         int *cand_id = nullptr, *beam_tid = nullptr;
         float* cand_lp = nullptr;
+        int* kvrow = nullptr;         // [B] encoded window of each row (window map)
+        int share = 0;                // rows per window of this call (0: identity, no map)
         std::map<GraphKey, hipGraphExec_t> graphs;
         std::vector<int> host_tok;    // host sources of the call's token uploads
         size_t host_used = 0;
@@ -171,15 +197,17 @@ private:
     void load_ggml(const GgmlFile& f);
     void alloc_workspace();
     void upload_tables(const std::vector<float>* filters);
-    void stage_pcm(const float* const* pcm, const int* n, int B);
-    void run_mel(const float* pcm_dev, int64_t stride, int B, float* dbg);
+    void run_mel_utts(const float* pcm, const std::vector<int64_t>& pcm_off, const int* n, int U);
+    void upload_windows(const int* utt, const int* seek, int E);
+    void finish_call_timing();
     void run_encoder(int B);
     void enqueue_encoder(int B);  // run_encoder, replayed from a per-B graph after the first call
     void run_cross_kv(int B);
     void run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1, float* top2, int* lang_out,
                     int* ts_state_out);
-    void enqueue_decoder_pass(DecGroup& g, int B_total, int Tq, const DecodeRequest& rq, int out_cap);
-    float* enqueue_layers(DecGroup& g, int B_total, int Tq);
+    // E: encoded windows (the cross K/V layout); g.share / g.kvrow: the rows' window map
+    void enqueue_decoder_pass(DecGroup& g, int E, int Tq, const DecodeRequest& rq, int out_cap);
+    float* enqueue_layers(DecGroup& g, int E, int Tq);
     void enqueue_head(DecGroup& g, int Tq, const DecodeRequest& rq, int out_cap, float* xc, const uint32_t* sup,
                       bool blank);
 
@@ -221,10 +249,7 @@ private:
     // ---- workspace (one arena)
     char* aarena_ = nullptr;
     int64_t abytes_ = 0;
-    float* pcm_ = nullptr;
-    int* nsamp_ = nullptr;
-    float* mel_raw_ = nullptr;
-    unsigned* mel_max_ = nullptr;
+    int *win_utt_ = nullptr, *win_seek_ = nullptr;  // [max_batch] encoder windows
     void* mel_in_ = nullptr;
     void* y1p_ = nullptr;
     float* x_ = nullptr;
@@ -246,6 +271,24 @@ private:
     void* kvtmp_ = nullptr;      // self-K/V reorder scratch (allocated on first beam search)
     std::vector<int> beam_host_;  // host sources of the per-step uploads
     void read_cands(int B, BeamCands* out);
+
+    // ---- utterances of load_utterances (grown on demand, outside the arenas)
+    float* upcm_ = nullptr;      // staged host PCM
+    int64_t upcm_cap_ = 0;       // samples
+    float* umel_ = nullptr;      // log10-mel rows of every utterance [rows][n_mels]
+    int64_t umel_cap_ = 0;       // rows
+    char* uinfo_ = nullptr;      // [U] pcm_off (int64), row_off (int64), n (int), max key (unsigned)
+    int uinfo_cap_ = 0;
+    MelUtts mu_{};
+    unsigned* umax_ = nullptr;
+    std::vector<int> un_;        // samples per utterance (host)
+    std::vector<int64_t> uhost_; // pcm / row offsets (host)
+    std::vector<char> mel_img_;  // host source of the descriptor upload
+    std::vector<int> whost_;     // host source of the window upload
+    std::vector<int> kvrow_host_;  // host source of the rows' window map upload
+    int enc_E_ = 0;              // windows encoded by the last encode_windows
+    bool mel_pending_ = false, enc_pending_ = false;  // stages whose events the next decode reads
+    void ensure_capacity(void** p, int64_t* cap, int64_t need, size_t esz, const char* what);
 
     Timings tm_;
     CallStats cs_;

@@ -2,6 +2,7 @@
 #include "full.h"
 
 #include <math.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <map>
@@ -14,7 +15,6 @@ namespace spt {
 
 namespace {
 
-constexpr int kWin = 480000;  // samples per 30 s window
 constexpr int kHop = 160;     // samples per 10 ms frame
 
 // whisper_n_len of an input: log_mel_spectrogram's n_len_org = 1 + (n + 200 - 400) / 160
@@ -79,9 +79,9 @@ void bookkeep(DecOut& d, int tok, int i, int seek, int seek_end, const FullParam
 // (ties: lower decoder index), each live decoder takes the next one (from the second step on,
 // skipping candidates whose sum equals the one just taken), its self-K/V row follows the source
 // decoder, and the per-decoder bookkeeping runs on the new last token
-void run_beam(Engine& e, const DecodeRequest& rq, const std::vector<const float*>& ptr, const std::vector<int>& ns,
-              int nj, int K, const std::vector<int>& seek, const std::vector<int>& seek_end, const FullParams& p,
-              const Specials& sp, int n_max, std::vector<std::vector<DecOut>>* outs, std::vector<int>* lang) {
+void run_beam(Engine& e, const DecodeRequest& rq, int nj, int K, const std::vector<int>& seek,
+              const std::vector<int>& seek_end, const FullParams& p, const Specials& sp, int n_max,
+              std::vector<std::vector<DecOut>>* outs, std::vector<int>* lang) {
     const int B = nj * K;
     struct Dec {
         DecOut o;
@@ -92,7 +92,7 @@ void run_beam(Engine& e, const DecodeRequest& rq, const std::vector<const float*
     for (Dec& d : dec) d.o.seek_delta = 3000;
     BeamCands c;
     lang->assign(B, -1);
-    e.beam_begin(ptr.data(), ns.data(), B, rq, &c, lang->data());
+    e.beam_begin(B, rq, &c, lang->data());
     struct Cand {
         int src;
         Dec d;
@@ -235,17 +235,15 @@ void whisper_full_batch(Engine& e, const Vocab* vocab, const std::vector<const f
         (*out)[u].lang_tok = us[u].lang;
     }
     uint64_t call = 0;
-    while (true) {
-        std::vector<int> act;
-        for (int u = 0; u < U; ++u) {
-            if (us[u].done) continue;
-            if (us[u].seek + 100 >= us[u].seek_end) { us[u].done = true; continue; }  // < 1 s left
-            act.push_back(u);
-        }
-        if (act.empty()) break;
-        for (int u : act)  // a short tail: drop the past prompt (it makes the decoder repeat itself)
-            if (us[u].seek > 0 && us[u].seek + 500 >= us[u].seek_end) us[u].past.clear();
-        std::vector<int> pending = act;
+    // one window of each utterance in `chunk` (encoded as window win_of[u]): the temperature
+    // loop of whisper_full_with_state, each temperature's decoders batched over the utterances
+    // SPT_NO_WINDOW_SHARE=1 (tests): each decoder row encodes its own copy of its window, as every
+    // engine call did before ABI 11 -- the outputs must be bitwise the same as with shared windows
+    const char* ns_env = getenv("SPT_NO_WINDOW_SHARE");
+    const bool no_share = ns_env && atoi(ns_env) != 0;
+    std::map<int, int> chunk_utt;  // utterance -> its index in the loaded set
+    auto window_pass = [&](const std::vector<int>& chunk, const std::map<int, int>& win_of) {
+        std::vector<int> pending = chunk;
         for (size_t it = 0; it < temps.size() && !pending.empty(); ++it) {
             const float t_cur = temps[it];
             const bool beam = p.beam_size > 1 && t_cur == 0.0f;  // WHISPER_SAMPLING_BEAM_SEARCH
@@ -290,27 +288,31 @@ void whisper_full_batch(Engine& e, const Vocab* vocab, const std::vector<const f
                     rq.extra_suppress = nst;
                     rq.blank_tok = blank;
                     rq.n_steps = std::min(n_max, dm.n_text_ctx + 1 - P - Tq);
-                    std::vector<const float*> ptr(B);
-                    std::vector<int> ns(B);
                     for (int j = 0; j < nj; ++j) {
                         const int u = grp[g0 + j];
-                        const int64_t off = (int64_t)us[u].seek * kHop;
-                        const int avail = (int)std::max<int64_t>(0, std::min<int64_t>(kWin, n[u] - off));
                         for (int d = 0; d < nd; ++d) {
-                            const int r = j * nd + d;
-                            ptr[r] = pcm[u] + std::min<int64_t>(off, n[u]);
-                            ns[r] = avail;
+                            rq.kv_row.push_back(win_of.at(u));  // the utterance's encoded window
                             rq.seek.push_back(us[u].seek);
                             rq.seek_end.push_back(us[u].seek_end);
                             if (P > 0) rq.row_prefix.push_back(prefix[u]);
                             if (multi) rq.lang_tok.push_back(us[u].lang >= 0 ? us[u].lang : -(j * nd + 1));
                         }
                     }
+                    if (no_share) {  // test hook: every row its own copy of its window (ABI <= 10)
+                        std::vector<int> wu, ws;
+                        for (int j = 0; j < nj; ++j)
+                            for (int d = 0; d < nd; ++d) {
+                                wu.push_back(chunk_utt.at(grp[g0 + j]));
+                                ws.push_back(us[grp[g0 + j]].seek);
+                            }
+                        e.encode_windows(wu.data(), ws.data(), B);
+                        rq.kv_row.clear();
+                    }
                     if (beam) {
                         rq.beam_k = ndec;
                         std::vector<std::vector<DecOut>> bo;
                         std::vector<int> lang;
-                        run_beam(e, rq, ptr, ns, nj, nd, rq.seek, rq.seek_end, p, sp, n_max, &bo, &lang);
+                        run_beam(e, rq, nj, nd, rq.seek, rq.seek_end, p, sp, n_max, &bo, &lang);
                         for (int j = 0; j < nj; ++j) {
                             const int u = grp[g0 + j];
                             if (multi && us[u].lang < 0) {
@@ -324,8 +326,7 @@ void whisper_full_batch(Engine& e, const Vocab* vocab, const std::vector<const f
                     const int S = rq.n_steps;
                     std::vector<int> tok((size_t)B * S), lang(B, -1), state((size_t)B * 4);
                     std::vector<float> plog((size_t)B * S), tid((size_t)B * S);
-                    e.transcribe_host(ptr.data(), ns.data(), B, rq, tok.data(), plog.data(), tid.data(), lang.data(),
-                                      state.data());
+                    e.decode(B, rq, tok.data(), plog.data(), tid.data(), lang.data(), state.data());
                     for (int j = 0; j < nj; ++j) {
                         const int u = grp[g0 + j];
                         if (multi && us[u].lang < 0) {  // detected once, on the utterance's first window
@@ -412,6 +413,45 @@ void whisper_full_batch(Engine& e, const Vocab* vocab, const std::vector<const f
             }
             pending.swap(again);
         }
+    };
+    // utterances in sets whose PCM and log-mel stay resident together (an hour of audio per set;
+    // a longer utterance is a set of its own): each set's log-mel is computed once, whole
+    constexpr int64_t kSetSamples = 16000LL * 3600;
+    for (int u0 = 0; u0 < U;) {
+        int u1 = u0;
+        int64_t tot = 0;
+        while (u1 < U && (u1 == u0 || tot + n[u1] <= kSetSamples)) tot += n[u1++];
+        bool any = false;
+        for (int u = u0; u < u1; ++u) any = any || us[u].seek + 100 < us[u].seek_end;
+        if (any) e.load_utterances(pcm.data() + u0, n.data() + u0, u1 - u0);
+        while (any) {
+            std::vector<int> act;
+            for (int u = u0; u < u1; ++u) {
+                if (us[u].done) continue;
+                if (us[u].seek + 100 >= us[u].seek_end) { us[u].done = true; continue; }  // < 1 s left
+                act.push_back(u);
+            }
+            if (act.empty()) break;
+            for (int u : act)  // a short tail: drop the past prompt (it makes the decoder repeat itself)
+                if (us[u].seek > 0 && us[u].seek + 500 >= us[u].seek_end) us[u].past.clear();
+            // one encoder run per window (whisper_encode_internal at `seek`), shared by every
+            // temperature and every decoder of the utterance
+            for (size_t c0 = 0; c0 < act.size(); c0 += cap) {
+                const std::vector<int> chunk(act.begin() + c0, act.begin() + std::min(act.size(), c0 + cap));
+                const int E = (int)chunk.size();
+                std::vector<int> wu(E), ws(E);
+                std::map<int, int> win_of;
+                for (int i = 0; i < E; ++i) {
+                    wu[i] = chunk[i] - u0;
+                    chunk_utt[chunk[i]] = wu[i];
+                    ws[i] = us[chunk[i]].seek;
+                    win_of[chunk[i]] = i;
+                }
+                e.encode_windows(wu.data(), ws.data(), E);
+                window_pass(chunk, win_of);
+            }
+        }
+        u0 = u1;
     }
     for (FullResult& r : *out)
         for (const FullSegment& s : r.segments) r.text += s.text;

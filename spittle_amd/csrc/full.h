@@ -8,9 +8,11 @@
 // The per-token rules run on the device (k_sample.hip); this file owns what whisper.cpp does
 // between decoder passes: the seek loop, decoder ranking and fallback, segment assembly.
 //
-// Differences: a window's log-mel is computed from its own 30 s of samples (the
-// reference takes frames [seek, seek + 3000) of one log-mel of the whole input, normalised
-// by its global maximum); temperature draws come from a counter-based stream, not mt19937.
+// As whisper.cpp: ONE log-mel of each whole utterance (global max - 8 clamp), each window's
+// encoder input = frames [seek, seek + 3000) of it, one encoder run per window shared by every
+// temperature and every decoder of the utterance (Engine::load_utterances / encode_windows /
+// decode).  Difference: temperature draws come from a
+// counter-based stream, not mt19937.
 #pragma once
 #include <stdint.h>
 

@@ -220,6 +220,12 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_q64_kernel(const bf16* __res
         const bf16* qp = base + (size_t)min(q_abs, T - 1) * ld + h * 64;
 #pragma unroll
         for (int s = 0; s < 4; ++s) qf[qb][s] = *(const bf16x8*)(qp + 16 * s + 8 * hf);
+        if constexpr (SUM == 4) {  // scores come out of the MFMA in log2 units: s = (q * c) . k
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) qf[qb][s][e] = (short)f2bf(bf2f((bf16)qf[qb][s][e]) * kScaleLog2);
+        }
     }
 
     auto lds_k = [&](int buf) -> SPT_LDS char* { return (SPT_LDS char*)smem + (buf * 2 + 0) * 8192; };
@@ -263,8 +269,11 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_q64_kernel(const bf16* __res
         f32x16 s[2][2];
 #pragma unroll
         for (int kt2 = 0; kt2 < 2; ++kt2) {
+            // SUM == 4: the accumulator starts at -m (the query's running maximum, log2 units, a
+            // lane constant), so the MFMA chain leaves s - m and p = exp2(s - m) needs no FMA
+            const float i0 = (SUM == 4 && kt > 0) ? -m_run[0] : 0.f, i1 = (SUM == 4 && kt > 0) ? -m_run[1] : 0.f;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) { s[0][kt2][i] = 0.f; s[1][kt2][i] = 0.f; }
+            for (int i = 0; i < 16; ++i) { s[0][kt2][i] = i0; s[1][kt2][i] = i1; }
             const int row = 32 * kt2 + l32;
 #pragma unroll
             for (int st = 0; st < 4; ++st) {
@@ -284,7 +293,71 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_q64_kernel(const bf16* __res
                         if (kt * 64 + key_of(kt2, r, hf) >= T) s[qb][kt2][r] = -INFINITY;
         }
         bf16x8 pf[2][2][2];
-        if constexpr (SUM == 3) {
+        if constexpr (SUM == 4) {
+            // Optimistic softmax as SUM == 3, on scores already relative to the running maximum:
+            // one v_exp and one scalar add per score (no packed f32 VALU beside the MFMAs); the
+            // first tile, or a lane whose tile sum leaves [0, 2^12], re-bases: m += max(0, tile max)
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb) {
+                union { bf16x8 v; uint32_t w[4]; } pu[2][2];
+                auto expo = [&](float sub) {
+                    float l0 = 0.f, l1 = 0.f;
+#pragma unroll
+                    for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+                        for (int r = 0; r < 16; r += 2) {
+                            const float p0 = __builtin_amdgcn_exp2f(s[qb][kt2][r] - sub);
+                            const float p1 = __builtin_amdgcn_exp2f(s[qb][kt2][r + 1] - sub);
+                            l0 += p0;
+                            l1 += p1;
+                            const f32x2 pv = {p0, p1};
+                            pu[kt2][r >> 3].w[(r & 7) >> 1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pv, bf16x2v));
+                        }
+                    return l0 + l1;
+                };
+                auto expo0 = [&]() {  // the common path: s is already s - m
+                    float l0 = 0.f, l1 = 0.f;
+#pragma unroll
+                    for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+                        for (int r = 0; r < 16; r += 2) {
+                            const float p0 = __builtin_amdgcn_exp2f(s[qb][kt2][r]);
+                            const float p1 = __builtin_amdgcn_exp2f(s[qb][kt2][r + 1]);
+                            l0 += p0;
+                            l1 += p1;
+                            const f32x2 pv = {p0, p1};
+                            pu[kt2][r >> 3].w[(r & 7) >> 1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pv, bf16x2v));
+                        }
+                    return l0 + l1;
+                };
+                float lt = kt > 0 ? expo0() : INFINITY;
+                if (__any(!(lt <= 4096.0f))) {
+                    float mloc = -INFINITY;  // tile maximum of s - m (kt == 0: of s, m = -inf)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) mloc = max3f(mloc, s[qb][0][r], s[qb][1][r]);
+                    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+                    float delta, alpha;
+                    if (kt == 0) {
+                        delta = mloc;
+                        alpha = 0.f;
+                        m_run[qb] = mloc;
+                    } else {
+                        delta = fmaxf(mloc, 0.f);
+                        alpha = __builtin_amdgcn_exp2f(-delta);
+                        m_run[qb] += delta;
+                    }
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) { o[qb][0][i] *= alpha; o[qb][1][i] *= alpha; }
+                    lsum[qb] *= alpha;
+                    lt = expo(delta);
+                }
+                lsum[qb] += lt;
+#pragma unroll
+                for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+                    for (int sp = 0; sp < 2; ++sp) pf[qb][kt2][sp] = pu[kt2][sp].v;
+            }
+        } else if constexpr (SUM == 3) {
             // Optimistic softmax: exponentiate against the running maximum first and re-base only
             // when a lane's tile row-sum leaves [0, 2^12] (or is not finite -- always on the first
             // tile, where m_run = -inf).  Probabilities stay <= 2^12 (exact range in f32 / bf16,
@@ -560,6 +633,7 @@ void enc_attention(int dtype, const void* qkv, int B, int T, int H, void* out, h
         if (sum == 1) hipLaunchKernelGGL(attn_bf16_q64_kernel<1>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
         else if (sum == 2) hipLaunchKernelGGL(attn_bf16_q64_kernel<2>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
         else if (sum == 3 && swz == 3) hipLaunchKernelGGL((attn_bf16_q64_kernel<3, 3>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
+        else if (sum == 4) hipLaunchKernelGGL(attn_bf16_q64_kernel<4>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
         else if (sum == 3) hipLaunchKernelGGL(attn_bf16_q64_kernel<3>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
         else if (swz == 0) hipLaunchKernelGGL((attn_bf16_q64_kernel<0, 0>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
         else if (swz == 1) hipLaunchKernelGGL((attn_bf16_q64_kernel<0, 1>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);

@@ -760,29 +760,38 @@ __global__ __launch_bounds__(64 * AW) void self_attn_kernel(const T* __restrict_
     }
 }
 
-// Cross-attention over the cached encoder K/V (all T_enc keys), one workgroup per (b, h).
-// kv: [2][B_layout][H][T_enc][64] at the group's first sequence.  (A fused LayerNorm + cross-Q
-// projection prologue and key-chunk splits were measured slower on MI355X: r1
-// exp_fused_xattn_pending_slabs.txt.)
+// Cross-attention over the cached encoder K/V (all T_enc keys), one workgroup per (row run, h).
+// kv: one layer in the kv_offset layout of B_layout windows, at the group's first window (no map)
+// or at the layer (kvrow: the window of each run of `share` rows).  A workgroup takes queries
+// [blockIdx.y * NQ, + NQ) of its run's share * Tq query rows (rows j * share .. + share - 1, Tq
+// each), so the decoders of one utterance (beam / best_of) read its window's K/V once per chunk.
+// (A fused LayerNorm + cross-Q projection prologue and key-chunk splits were measured slower on
+// MI355X: r1 exp_fused_xattn_pending_slabs.txt.)
 template <typename T, int NQ, bool SPLIT, int NW = AW, int NIX = 0>
 __global__ __launch_bounds__(64 * NW) void cross_attn_kernel(const T* __restrict__ q, const T* __restrict__ kv,
                                                              int B_layout, int H, int T_enc, int Tq,
-                                                             T* __restrict__ out, float* __restrict__ part) {
+                                                             T* __restrict__ out, float* __restrict__ part,
+                                                             const int* __restrict__ kvrow, int share) {
     typedef AttnWave<T, NQ, NIX, NW> W;
     XA_STAMP(0);
     __shared__ float s_m[NW][NQ], s_l[NW][NQ];
     __shared__ float s_o[NW][NQ][64];
-    const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+    const int bh = blockIdx.x, j = bh / H, h = bh - j * H;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane & 7;
+    const int nq_all = share * Tq;                          // query rows of this run
+    const int c0 = SPLIT ? 0 : (int)blockIdx.y * NQ;        // first query of this workgroup
+    const int nq = min(NQ, nq_all - c0);
+    const int kb = kvrow ? kvrow[j * share] : j;            // the run's window
     W aw;  // kv_offset layout: 32-key blocks [T/32][B][H][2][32][64]
-    const size_t kvo = ((size_t)b * H + h) * 4096 + 8 * g;
+    const size_t kvo = ((size_t)kb * H + h) * 4096 + 8 * g;
     aw.init(kv + kvo, kv + kvo + 2048, T_enc, lane, (int64_t)B_layout * H * 4096);
+    const size_t qrow0 = (size_t)j * nq_all + c0;           // = (j * share) * Tq + c0
     float qv[NQ][8];
     int lim[NQ];
 #pragma unroll
     for (int t = 0; t < NQ; ++t) {
-        const int tt = t < Tq ? t : Tq - 1;
-        const T* qr = q + (size_t)(b * Tq + tt) * (H * 64) + h * 64 + 8 * g;
+        const int tt = t < nq ? t : nq - 1;
+        const T* qr = q + (qrow0 + tt) * (H * 64) + h * 64 + 8 * g;
 #pragma unroll
         for (int e = 0; e < 8; ++e) qv[t][e] = to_f<T>(qr[e]) * kLog2Scale;
         lim[t] = T_enc;
@@ -791,24 +800,24 @@ __global__ __launch_bounds__(64 * NW) void cross_attn_kernel(const T* __restrict
     const int nblk_all = cdiv(T_enc, W::KB);
     const int S = SPLIT ? (int)gridDim.y : 1, sp = SPLIT ? (int)blockIdx.y : 0;
     const int per = cdiv(nblk_all, S), blk0 = sp * per, nblk = min(nblk_all, blk0 + per);
-    aw.run(blk0 + wid, nblk, false, qv, lim, Tq);
+    aw.run(blk0 + wid, nblk, false, qv, lim, nq);
     if (wid == 0) XA_STAMP(1);
     aw.to_lds(s_m, s_l, s_o, wid, lane);
     __syncthreads();
     XA_STAMP(2);
-    if (tid < 64 * Tq) {
-        const int t = tid >> 6, e = tid & 63;
+    for (int i = tid; i < 64 * nq; i += 64 * NW) {
+        const int t = i >> 6, e = i & 63;
         float M, L, O;
         attn_merge<NQ, NW>(s_m, s_l, s_o, t, e, M, L, O);
         if constexpr (SPLIT) {  // partial {o[64], m, l} for the output projection's merge prologue
-            float* pp = part + ((((size_t)(b * Tq + t)) * H + h) * S + sp) * 66;
+            float* pp = part + (((qrow0 + t) * H + h) * S + sp) * 66;
             pp[e] = O;
             if (e == 0) {
                 pp[64] = M;
                 pp[65] = L;
             }
         } else {
-            out[(size_t)(b * Tq + t) * (H * 64) + h * 64 + e] = from_f<T>(O / L);
+            out[(qrow0 + t) * (H * 64) + h * 64 + e] = from_f<T>(O / L);
         }
     }
 }
@@ -952,20 +961,32 @@ void dec_self_attn(int dtype, const void* q, const void* cache, int B, int H, in
 }
 
 void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int B_layout, int H, int T_enc, int Tq, void* out,
-                    hipStream_t st, int splits, float* part) {
+                    hipStream_t st, int splits, float* part, const int* kvrow, int share) {
     if (Tq < 1 || Tq > 4) throw std::runtime_error("dec_cross_attn: 1..4 queries per sequence");
     if (splits < 1 || splits > 4 || (splits > 1 && !part)) throw std::runtime_error("dec_cross_attn: 1..4 key chunks");
-    const dim3 grid(B * H, splits), blk(64 * AW);
-#define SPT_XA(T, NQ, SP)                                                                                   \
-    hipLaunchKernelGGL((cross_attn_kernel<T, NQ, SP>), grid, blk, 0, st, (const T*)q, (const T*)kv, B_layout, H, \
-                       T_enc, Tq, (T*)out, part)
-    if (dtype == DT_BF16) {
-        if (Tq == 1) { if (splits > 1) SPT_XA(bf16, 1, true); else SPT_XA(bf16, 1, false); }
-        else { if (splits > 1) SPT_XA(bf16, 4, true); else SPT_XA(bf16, 4, false); }
-    } else {
-        if (Tq == 1) { if (splits > 1) SPT_XA(float, 1, true); else SPT_XA(float, 1, false); }
-        else { if (splits > 1) SPT_XA(float, 4, true); else SPT_XA(float, 4, false); }
-    }
+    if (share < 1 || share > 8 || B % share) throw std::runtime_error("dec_cross_attn: rows per window 1..8, dividing B");
+    if (share > 1 && !kvrow) throw std::runtime_error("dec_cross_attn: shared windows need the window map");
+    const int nq = share * Tq;
+    // queries per workgroup: 1 or 4 as without a window map; a decode step of several rows per
+    // window takes 5 (bf16: beam 5 / best_of 5 in one workgroup; 8 would spill) or 4 (f32) of
+    // them.  Every variant gives each lane the
+    // same keys as the one-row kernel of the same Tq (NI: keys per lane), so a row's result is
+    // bitwise the same whether or not its window is shared.
+    const int NQ = nq == 1 ? 1 : Tq > 1 ? 4 : (dtype == DT_BF16 ? 5 : 4);
+    if (splits > 1 && nq > NQ) throw std::runtime_error("dec_cross_attn: key chunks need one query chunk per window");
+    const dim3 grid((B / share) * H, splits > 1 ? splits : cdiv(nq, NQ)), blk(64 * AW);
+#define SPT_XA(T, NQ_, SP, NI)                                                                                  \
+    hipLaunchKernelGGL((cross_attn_kernel<T, NQ_, SP, AW, NI>), grid, blk, 0, st, (const T*)q, (const T*)kv,      \
+                       B_layout, H, T_enc, Tq, (T*)out, part, kvrow, share)
+    // NI = 4 for the step kernels of both dtypes (AttnWave's default at NQ = 1)
+#define SPT_XA_T(T)                                                                       \
+    if (NQ == 1) { if (splits > 1) SPT_XA(T, 1, true, 0); else SPT_XA(T, 1, false, 0); }  \
+    else if (NQ == 4 && Tq > 1) { if (splits > 1) SPT_XA(T, 4, true, 0); else SPT_XA(T, 4, false, 0); } \
+    else if (NQ == 4) { if (splits > 1) SPT_XA(T, 4, true, 4); else SPT_XA(T, 4, false, 4); } \
+    else { if (splits > 1) SPT_XA(T, 5, true, 4); else SPT_XA(T, 5, false, 4); }
+    if (dtype == DT_BF16) { SPT_XA_T(bf16); }
+    else { SPT_XA_T(float); }
+#undef SPT_XA_T
 #undef SPT_XA
     SPT_LAUNCH_CHECK();
 }

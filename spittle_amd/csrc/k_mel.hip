@@ -13,9 +13,16 @@
 // output matches the CPU restatement (oracle/wo_mel.c) bit-for-bit up to libm's
 // last-ulp differences in log10.  The mel filterbank is walked only over its
 // nonzero groups of four (a zero group adds exactly +0.0 to the double sum).
-// A per-chunk maximum is reduced with one atomicMax per workgroup on an
+// A per-utterance maximum is reduced with one atomicMax per workgroup on an
 // order-preserving integer key; mel_norm then clamps at max - 8, applies
-// (x + 4) / 4 and writes the zero-padded, time-major conv1 input.
+// (x + 4) / 4 and writes the zero-padded, time-major conv1 input of each
+// encoder window: frames [seek, seek + 3000) of its utterance.
+//
+// The log-mel is computed once over each WHOLE utterance, as whisper.cpp's
+// whisper_pcm_to_mel does before whisper_full's seek loop: the reflective head
+// is the utterance's own first samples, frames run to (n + 480000) / 160, and
+// the clamp uses the utterance's global maximum.  Each window then takes its
+// slice (whisper_encode_internal's mel_offset = seek).
 #include "common.h"
 #include "kernels.h"
 
@@ -55,21 +62,21 @@ __device__ __forceinline__ void butterfly(const float* E, const float* O, float*
     }
 }
 
-__global__ __launch_bounds__(256) void mel_frames_kernel(const float* __restrict__ pcm, int64_t stride,
-                                                         const int* __restrict__ nsamp, int n_mels, MelTables tb,
-                                                         float* __restrict__ mel_raw, unsigned* __restrict__ mel_max) {
+__global__ __launch_bounds__(256) void mel_frames_kernel(const float* __restrict__ pcm, MelUtts ut, int n_mels,
+                                                         MelTables tb, float* __restrict__ mel_raw,
+                                                         unsigned* __restrict__ mel_max) {
     __shared__ float s_smp[FB * HOP + NFFT - HOP];
     __shared__ float s_tab[3][NFFT];
     __shared__ float s_buf[2][FB][2 * NFFT];
     __shared__ unsigned s_max;
     const int b = blockIdx.y, tid = threadIdx.x;
-    const int n = nsamp[b];
+    const int n = ut.n[b];
     const int n_comp = frames_computed(n);
     const int f0 = blockIdx.x * FB;
     if (f0 >= n_comp) return;
     const int nf = min(FB, n_comp - f0);
     const int n_sig = n + NFFT / 2;
-    const float* x = pcm + (size_t)b * stride;
+    const float* x = pcm + ut.pcm_off[b];
     if (tid == 0) s_max = 0u;
     for (int i = tid; i < NFFT; i += 256) {
         s_tab[0][i] = tb.hann[i];
@@ -155,7 +162,7 @@ __global__ __launch_bounds__(256) void mel_frames_kernel(const float* __restrict
             }
         }
         const float v = (float)log10(sum > 1e-10 ? sum : 1e-10);
-        mel_raw[((size_t)b * MEL_ROWS + f0 + f) * n_mels + j] = v;
+        mel_raw[(size_t)(ut.row_off[b] + f0 + f) * n_mels + j] = v;
         lmax = fmaxf(lmax, v);
     }
     lmax = wave_max(lmax);
@@ -165,20 +172,21 @@ __global__ __launch_bounds__(256) void mel_frames_kernel(const float* __restrict
 }
 
 template <typename T>
-__global__ void mel_norm_kernel(const float* __restrict__ mel_raw, const unsigned* __restrict__ mel_max,
-                                const int* __restrict__ nsamp, int n_mels, int Cp, T* __restrict__ out,
-                                float* __restrict__ dbg) {
-    const int b = blockIdx.y;
+__global__ void mel_norm_kernel(const float* __restrict__ mel_raw, const unsigned* __restrict__ mel_max, MelUtts ut,
+                                const int* __restrict__ win_utt, const int* __restrict__ win_seek, int n_mels, int Cp,
+                                T* __restrict__ out, float* __restrict__ dbg) {
+    const int b = blockIdx.y;  // encoder row (window)
     const int r = blockIdx.x;  // padded row 0..3001
-    const int n_comp = frames_computed(nsamp[b]);
-    float gmax = fkey_inv(mel_max[b]);
+    const int u = win_utt[b], seek = win_seek[b];
+    const int n_comp = frames_computed(ut.n[u]);
+    float gmax = fkey_inv(mel_max[u]);
     if (!(gmax > -10.0f)) gmax = -10.0f;  // frames past the signal are log10(1e-10)
     const double mmax = (double)gmax - 8.0;
-    const int t = r - 1;
+    const int t = r - 1, f = seek + t;  // f < n_len = n / 160 + 3000 whenever seek < n_len_org
     for (int c = threadIdx.x; c < Cp; c += blockDim.x) {
         float o = 0.0f;
         if (t >= 0 && t < 3000 && c < n_mels) {
-            float v = t < n_comp ? mel_raw[((size_t)b * MEL_ROWS + t) * n_mels + c] : -10.0f;
+            float v = f < n_comp ? mel_raw[(size_t)(ut.row_off[u] + f) * n_mels + c] : -10.0f;
             if ((double)v < mmax) v = (float)mmax;
             o = (float)(((double)v + 4.0) / 4.0);
             if (dbg) dbg[((size_t)b * n_mels + c) * 3000 + t] = o;
@@ -189,23 +197,30 @@ __global__ void mel_norm_kernel(const float* __restrict__ mel_raw, const unsigne
 
 }  // namespace
 
-void mel_frames(const float* pcm, int64_t pcm_stride, const int* n_samples, int B, int n_mels, MelTables t,
-                float* mel_raw, unsigned* mel_max, hipStream_t st) {
-    HIP_CHECK(hipMemsetAsync(mel_max, 0, sizeof(unsigned) * B, st));
-    dim3 grid(cdiv(MEL_ROWS, FB), B);
-    hipLaunchKernelGGL(mel_frames_kernel, grid, dim3(256), 0, st, pcm, pcm_stride, n_samples, n_mels, t, mel_raw,
-                       mel_max);
+int mel_rows(int n) {
+    const int n_sig = n + NFFT / 2, n_len = (int)(((int64_t)n + 480000) / HOP);
+    return std::min(n_sig / HOP + 1, n_len);
 }
 
-void mel_norm(int dtype, const float* mel_raw, const unsigned* mel_max, const int* n_samples, int B, int n_mels,
-              int Cp, void* mel_in, float* dbg, hipStream_t st) {
-    dim3 grid(MEL_ROWS, B);
+void mel_frames(const float* pcm, MelUtts u, int U, int max_rows, int n_mels, MelTables t, float* mel_raw,
+                unsigned* mel_max, hipStream_t st) {
+    HIP_CHECK(hipMemsetAsync(mel_max, 0, sizeof(unsigned) * U, st));
+    if (U < 1 || max_rows < 1) return;
+    dim3 grid(cdiv(max_rows, FB), U);
+    hipLaunchKernelGGL(mel_frames_kernel, grid, dim3(256), 0, st, pcm, u, n_mels, t, mel_raw, mel_max);
+    SPT_LAUNCH_CHECK();
+}
+
+void mel_norm(int dtype, const float* mel_raw, const unsigned* mel_max, MelUtts u, const int* win_utt,
+              const int* win_seek, int E, int n_mels, int Cp, void* mel_in, float* dbg, hipStream_t st) {
+    dim3 grid(MEL_ROWS, E);
     if (dtype == DT_BF16)
-        hipLaunchKernelGGL(mel_norm_kernel<bf16>, grid, dim3(128), 0, st, mel_raw, mel_max, n_samples, n_mels, Cp,
-                           (bf16*)mel_in, dbg);
+        hipLaunchKernelGGL(mel_norm_kernel<bf16>, grid, dim3(128), 0, st, mel_raw, mel_max, u, win_utt, win_seek,
+                           n_mels, Cp, (bf16*)mel_in, dbg);
     else
-        hipLaunchKernelGGL(mel_norm_kernel<float>, grid, dim3(128), 0, st, mel_raw, mel_max, n_samples, n_mels, Cp,
-                           (float*)mel_in, dbg);
+        hipLaunchKernelGGL(mel_norm_kernel<float>, grid, dim3(128), 0, st, mel_raw, mel_max, u, win_utt, win_seek,
+                           n_mels, Cp, (float*)mel_in, dbg);
+    SPT_LAUNCH_CHECK();
 }
 
 }  // namespace spt

@@ -75,13 +75,26 @@ struct MelTables {
     const float* filt;   // [n_mels][201]
     const int* grp;      // [n_mels][2] first / last+1 group of 4 bins with a nonzero weight
 };
-constexpr int MEL_ROWS = 3002;  // padded time-major rows: [zero][3000 frames][zero]
-// log10 mel of every computed frame of each chunk; mel_raw [B][3002][n_mels]; max key per chunk
-void mel_frames(const float* pcm, int64_t pcm_stride, const int* n_samples, int B, int n_mels,
-                MelTables t, float* mel_raw, unsigned* mel_max, hipStream_t st);
-// clamp / normalise -> conv1 input [B][3002][Cp] (row 0 and 3001 zero); optional f32 [B][n_mels][3000]
-void mel_norm(int dtype, const float* mel_raw, const unsigned* mel_max, const int* n_samples, int B,
-              int n_mels, int Cp, void* mel_in, float* dbg, hipStream_t st);
+constexpr int MEL_ROWS = 3002;  // padded time-major rows of a window: [zero][3000 frames][zero]
+// whole utterances (device arrays, one entry each): samples pcm[pcm_off[u] .. + n[u]), their
+// mel_rows(n[u]) computed log10-mel rows at mel_raw[row_off[u]] ([rows][n_mels])
+struct MelUtts {
+    const int64_t* pcm_off;
+    const int64_t* row_off;
+    const int* n;
+};
+// frames whisper.cpp computes for n samples: min((n + 200) / 160 + 1, (n + 480000) / 160); later
+// frames of the (n + 480000) / 160 are log10(1e-10)
+int mel_rows(int n);
+// log10 mel of every computed frame of each of U utterances (max_rows >= every mel_rows(n[u]));
+// the maximum of each utterance as an order-preserving key in mel_max[u]
+void mel_frames(const float* pcm, MelUtts u, int U, int max_rows, int n_mels, MelTables t, float* mel_raw,
+                unsigned* mel_max, hipStream_t st);
+// encoder windows e < E: frames [win_seek[e], + 3000) of utterance win_utt[e], clamped at that
+// utterance's max - 8 and normalised -> conv1 input [E][3002][Cp] (rows 0 and 3001 zero); optional
+// f32 copy [E][n_mels][3000]
+void mel_norm(int dtype, const float* mel_raw, const unsigned* mel_max, MelUtts u, const int* win_utt,
+              const int* win_seek, int E, int n_mels, int Cp, void* mel_in, float* dbg, hipStream_t st);
 
 // ------------------------------------------------------------------ norm (k_norm.hip)
 // y[m] = LN(x[m]) * w + b ; x f32 [M][d], y f32/bf16 [M][d]
@@ -154,8 +167,12 @@ void dec_self_attn(int dtype, const void* q, const void* cache, int B, int H, in
 // partials [R][H][splits][66] = {o[64], m, l} to `part` instead (merged by an A_ATTN GEMV)
 // kv: one layer of the cross K/V cache (kv_offset layout with B_layout sequences), advanced to
 // the first of the B sequences (+ b0 * H * 4096)
+// kvrow (device [B], optional): rows j * share .. + share - 1 all attend to window kvrow[j * share]
+// (kv then points at the layer, not at the first sequence); one workgroup per (window run, head)
+// reads that window's K/V once for its share * Tq queries (the decoders of one utterance)
 void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int B_layout, int H, int T_enc, int Tq,
-                    void* out, hipStream_t st, int splits = 1, float* part = nullptr);
+                    void* out, hipStream_t st, int splits = 1, float* part = nullptr, const int* kvrow = nullptr,
+                    int share = 1);
 
 struct FinalizeArgs {
     const void* part; int n_tiles;        // logits top-2 partials [B][n_tiles]

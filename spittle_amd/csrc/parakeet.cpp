@@ -80,6 +80,10 @@ bool parse_parakeet_spec(const std::string& spec, PkDims* dm, uint64_t* seed, st
     d.name = parts[0];
     if (d.name == "parakeet-tdt-0.6b-v3") {
         // defaults
+    } else if (d.name == "parakeet-tdt-0.6b-v2") {
+        // the catalog's English-only model (model_catalog.json:214-217): v3's network with a
+        // 1024-piece SentencePiece vocabulary [upstream, recalled]
+        d.n_vocab = 1024;
     } else if (d.name == "parakeet-test-small") {
         d.d = 256; d.n_layers = 2; d.n_heads = 4; d.ff = 1024; d.sub_ch = 128; d.pred = 128; d.n_vocab = 1024;
     } else {

@@ -265,12 +265,14 @@ class WhisperEngine:
         self._check(self._lib.spt_get_call_stats(self._ctx, C.byref(t)))
         return {k: getattr(t, k) for k, _ in t._fields_ if k != "reserved0"}
 
-    def debug_mel(self, samples) -> np.ndarray:
+    def debug_mel(self, samples, seek: int = 0) -> np.ndarray:
+        """The normalised log-mel [n_mels][3000] the encoder takes for the window at frame `seek`
+        (frames seek .. seek + 2999 of the whole utterance's log-mel)."""
         self._need()
         x = np.ascontiguousarray(np.asarray(samples, np.float32).reshape(-1))
         out = np.empty((self.info()["n_mels"], 3000), np.float32)
-        self._check(self._lib.spt_debug_mel(self._ctx, x.ctypes.data_as(C.POINTER(C.c_float)), x.size,
-                                            out.ctypes.data_as(C.POINTER(C.c_float))))
+        self._check(self._lib.spt_debug_mel_at(self._ctx, x.ctypes.data_as(C.POINTER(C.c_float)), x.size, int(seek),
+                                               out.ctypes.data_as(C.POINTER(C.c_float))))
         return out
 
     def debug_encode(self, mel) -> np.ndarray:

@@ -193,3 +193,64 @@ def test_full_language_autodetect():
     for a, b in zip(full, fast):
         assert a.language is not None and a.language == b.language
     e.unload_model()
+
+
+def _loud_then_quiet(seconds, seed):
+    n = int(seconds * 16000)
+    x = np.concatenate([O.synth_audio(seed + k) for k in range((n + 479999) // 480000)])[:n].copy()
+    x[n // 2:] *= np.float32(0.03)  # the second half 30 dB quieter
+    return x
+
+
+@pytest.mark.parametrize("seconds,seed", [(45, 300), (75, 302)])
+def test_loud_then_quiet_whole_input_mel(tiny, seconds, seed):
+    """whisper.cpp's whisper_full takes every window's frames from ONE log-mel of the whole input
+    (global max - 8 clamp, real preceding samples at each window start; transcription.rs:494-503
+    hands it the whole utterance).  A loud-then-quiet dictation over 30 s makes the later windows'
+    mel differ from a per-window mel; the oracle restates the whole-input mel, and the device must
+    match it window by window."""
+    e, om = tiny
+    x = _loud_then_quiet(seconds, seed)
+    p = W.Params(max_tokens=16)
+    r = e.transcribe_samples(x, _params(max_new_tokens=16))
+    wins, segs, toks, _ = W.transcribe(om, x, p)
+    assert len(wins) >= 2
+    if _compare(r, wins, segs, toks):
+        assert r.n_windows == len(wins)
+    assert r.n_windows >= 2
+    cs = e.call_stats()
+    assert cs["encoder_windows"] == r.n_windows, cs  # one encoder run per window
+
+
+def test_one_encoder_run_per_window_with_fallback(tiny):
+    """Temperature fallback re-decodes a window at each temperature (best_of 5 sampled decoders
+    at t > 0) over the SAME encoded window: one encoder run per window, several decoder runs."""
+    e, _ = tiny
+    x = O.synth_audio(84, 30 * 16000)
+    r = e.transcribe_samples(x, _params(temperature_inc=0.2, logprob_thold=10.0, best_of=5, max_new_tokens=8, seed=3))
+    cs = e.call_stats()
+    assert r.n_fallbacks == 5 * r.n_windows
+    assert cs["encoder_windows"] == r.n_windows, cs
+    assert cs["engine_calls"] >= 6 * r.n_windows, cs
+
+
+@pytest.mark.parametrize("kind", ["beam5", "fallback_best_of5"])
+def test_shared_window_bitwise_equal_to_copies(tiny, kind, monkeypatch):
+    """The decoders of one utterance (beam 5, best_of 5) read one shared encoded window; the
+    result is bitwise the one they get when each decoder row encodes its own copy (every engine
+    call before ABI 11; SPT_NO_WINDOW_SHARE=1)."""
+    e, _ = tiny
+    xs = [O.synth_audio(85, 12 * 16000), O.synth_audio(86, 40 * 16000)]
+    kw = dict(beam_size=5, max_new_tokens=12) if kind == "beam5" else \
+        dict(temperature_inc=0.2, logprob_thold=10.0, best_of=5, max_new_tokens=12, seed=11)
+    shared = e.transcribe_batch(xs, _params(**kw))
+    cs = e.call_stats()
+    monkeypatch.setenv("SPT_NO_WINDOW_SHARE", "1")
+    copies = e.transcribe_batch(xs, _params(**kw))
+    cs2 = e.call_stats()
+    monkeypatch.delenv("SPT_NO_WINDOW_SHARE")
+    for a, b in zip(shared, copies):
+        assert a.tokens == b.tokens and a.text == b.text
+        assert np.array_equal(np.asarray(a.top1), np.asarray(b.top1))
+        assert [(s.start, s.end, s.text) for s in a.segments] == [(s.start, s.end, s.text) for s in b.segments]
+    assert cs["encoder_windows"] < cs2["encoder_windows"], (cs, cs2)

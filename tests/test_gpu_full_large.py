@@ -121,3 +121,34 @@ def test_large_v3_beam5(large, seconds, seed):
     x = _audio(seconds, seed)
     r = e.transcribe_samples(x, _params(beam_size=5, max_new_tokens=16))
     _check(f"beam5_{seconds}s", r, om, x, W.Params(max_tokens=16, beam_size=5))
+
+
+def _loud_then_quiet(seconds, seed):
+    x = _audio(seconds, seed).copy()
+    x[x.size // 2:] *= np.float32(0.03)  # the second half 30 dB quieter
+    return x
+
+
+@pytest.mark.parametrize("seconds,seed", [(45, 310), (75, 312)])
+def test_large_v3_loud_then_quiet(large, seconds, seed):
+    """The app's call on a loud-then-quiet dictation over 30 s: every window's frames come from one
+    log-mel of the whole utterance (whisper_pcm_to_mel's global max - 8 clamp), at large-v3 width,
+    against the oracle's whole-input restatement."""
+    e, om = large
+    x = _loud_then_quiet(seconds, seed)
+    r = e.transcribe_samples(x, _params(max_new_tokens=24))
+    rec = _check(f"loud_quiet_{seconds}s", r, om, x, W.Params(max_tokens=24))
+    assert r.n_windows >= 2 and rec["oracle_windows"] >= 2
+    assert e.call_stats()["encoder_windows"] == r.n_windows
+
+
+def test_large_v3_beam5_shared_window_bitwise(large, monkeypatch):
+    """Beam 5 at large-v3 width in bf16: the five decoders read one shared window (one workgroup
+    per (window, head) for all five queries), bitwise the result of five private copies."""
+    e, _ = large
+    x = _audio(20, 191)
+    a = e.transcribe_samples(x, _params(beam_size=5, max_new_tokens=16))
+    monkeypatch.setenv("SPT_NO_WINDOW_SHARE", "1")
+    b = e.transcribe_samples(x, _params(beam_size=5, max_new_tokens=16))
+    monkeypatch.delenv("SPT_NO_WINDOW_SHARE")
+    assert a.tokens == b.tokens and np.array_equal(np.asarray(a.top1), np.asarray(b.top1))

@@ -244,3 +244,58 @@ def test_whisper_full_with_vocabulary(tiny_f32):
         assert s.text == b"".join(tiny_f32.full_vocab[t] for t in toks if t < eot).decode("utf-8", "replace")
     assert a.text == "".join(s.text for s in a.segments).strip()
     e.unload_model()
+
+
+@pytest.fixture(scope="module")
+def turbo(tmp_path_factory):
+    """ggml-large-v3-turbo.bin's geometry (/root/reference/src-tauri/resources/model_catalog.json:
+    169-173): large-v3 width (d 1280, 20 heads, 128 mels, 51866 tokens) with 4 decoder layers, as
+    an f16 file; 2 encoder layers here (turbo's encoder is large-v3's 32, covered at full depth by
+    test_gpu_fullsize)."""
+    O.set_threads(16)
+    mf = ModelFile(tmp_path_factory.mktemp("turbo"), "large-v3", G.F16, 2, 4)
+    e = _engine(mf.path, "bf16", max_batch=8)
+    om = mf.oracle("bf16")
+    yield mf, e, om
+    e.unload_model()
+    om.close()
+
+
+def _long_audio(seconds, seed):
+    n = int(seconds * 16000)
+    return np.concatenate([O.synth_audio(seed + k) for k in range((n + 479999) // 480000)])[:n]
+
+
+@pytest.mark.parametrize("seconds,seed", [(20, 400), (45, 404)])
+def test_turbo_file_whisper_full(turbo, seconds, seed):
+    """The app's call (whisper_full, timestamps on, fallback off) on the turbo geometry: tokens,
+    timestamp ids and segments equal to the oracle's whisper_full on the file's values rounded as
+    the bf16 engine holds them (bars of test_gpu_full_large: decisions over 0.1, log-probabilities
+    within 0.05; the seeds' oracle decisions all clear 0.1)."""
+    from oracle import whisper_full as W
+    from spittle_amd import WhisperInferenceParams
+    from tests.test_gpu_full_large import _check
+    mf, e, om = turbo
+    assert e.info()["n_dec"] == 4 and e.info()["n_enc"] == 2
+    x = _long_audio(seconds, seed)
+    r = e.transcribe_samples(x, WhisperInferenceParams(language="en", temperature_inc=0.0, max_new_tokens=24))
+    rec = _check(f"turbo_{seconds}s", r, om, x, W.Params(max_tokens=24))
+    assert rec["exact"] and r.n_windows == rec["oracle_windows"]
+
+
+def test_turbo_file_fast_path_batch(turbo):
+    """The benchmark protocol on the turbo geometry (B = 8 windows, greedy, no timestamps):
+    teacher-forced on the oracle's tokens, top-1 logits within 0.1; batch-invariant (bitwise)."""
+    mf, e, om = turbo
+    xs = [O.synth_audio(410 + i) for i in range(8)]
+    n = 12
+    rs = e.transcribe_batch(xs, _params(ignore_eot=True, max_new_tokens=n))
+    for i in (0, 5):
+        enc = om.encode(O.mel(xs[i], 128))
+        tk, t1, t2 = om.decode(enc, O.default_prompt(mf.dims.n_vocab), n, FLAGS)
+        got = np.array(rs[i].tokens)
+        k = next((s for s in range(n) if (t1 - t2)[s] < 0.2), n)
+        assert list(got[:k]) == list(tk[:k]), (i, got, tk)
+        assert np.abs(np.asarray(rs[i].top1[:k]) - t1[:k]).max() < 0.1
+        alone = e.transcribe_samples(xs[i], _params(ignore_eot=True, max_new_tokens=n))
+        assert alone.tokens == rs[i].tokens and np.array_equal(alone.top1, rs[i].top1)

@@ -385,14 +385,17 @@ def test_c5_streaming_b64_full_size():
     om.close()
 
 
-def test_full_size_fp16():
-    """parakeet-tdt-0.6b-v3 shape (24 layers, d 1024), fp16 encoder, 4 s: encoder vs the oracle
+@pytest.mark.parametrize("model,record", [("parakeet-tdt-0.6b-v3", "parakeet_fullsize.json"),
+                                          ("parakeet-tdt-0.6b-v2", "parakeet_v2_fullsize.json")])
+def test_full_size_fp16(model, record):
+    """parakeet-tdt-0.6b-v3 shape (24 layers, d 1024), and the catalog's English-only v2 (its
+    1024-token vocabulary; model_catalog.json:214-217), fp16 encoder, 4 s: encoder vs the oracle
     on identically rounded weights; the decoder exact on a given encoder output; end-to-end
-    agreement recorded in gpurun_out/parakeet_fullsize.json."""
+    agreement recorded in gpurun_out/<record>."""
     from spittle_amd import ParakeetInferenceParams, TimestampGranularity
     P.set_threads(16)
-    e = _engine("synthetic:parakeet-tdt-0.6b-v3", "f16", max_batch=2, max_seconds=8.0)
-    om = P.Model(P.dims_for("parakeet-tdt-0.6b-v3"), seed=SEED, wdtype=P.W_F16)
+    e = _engine("synthetic:" + model, "f16", max_batch=2, max_seconds=8.0)
+    om = P.Model(P.dims_for(model), seed=SEED, wdtype=P.W_F16)
     pcm = synth_audio(14, 16000 * 4)
     mel = P.mel(pcm)
     g = e.debug_encode(mel)
@@ -404,10 +407,44 @@ def test_full_size_fp16():
     r = e.transcribe_samples(pcm, ParakeetInferenceParams(timestamp_granularity=TimestampGranularity.Token))
     first, _, gap = _agree(r, om, o, F16_GAP)
     os.makedirs(OUT, exist_ok=True)
-    json.dump({"config": "parakeet-tdt-0.6b-v3 synthetic seed 7, fp16 encoder, 4 s", "encoder_rel_rms": rel,
+    json.dump({"config": f"{model} synthetic seed 7, fp16 encoder, 4 s", "encoder_rel_rms": rel,
                "encoder_max_abs": float(np.abs(g - o).max()), "oracle_tokens": len(t), "gpu_tokens": len(r.tokens),
                "prefix_agreement": first, "margin_at_departure": None if gap == float("inf") else gap,
                "decoder_exact_on_oracle_encoder": True},
-              open(os.path.join(OUT, "parakeet_fullsize.json"), "w"), indent=1)
+              open(os.path.join(OUT, record), "w"), indent=1)
     assert rel < 4e-3, rel
+    e.unload_model()
+
+
+def test_v2_english_model_dir_full_size(tmp_path):
+    """The catalog's parakeet-tdt-0.6b-v2-int8 directory (English only, 1024-token vocabulary;
+    /root/reference/src-tauri/resources/model_catalog.json:214-217) in the int8 export's layout at
+    its full shape (24 layers, d 1024): dimensions inferred from the tensors, the f32 engine's
+    tokens and frames against the oracle on the same dequantised weights, text from its vocab.txt,
+    and the app's int8() params (fp16 encoder) running on it."""
+    from spittle_amd import ParakeetEngine, ParakeetModelParams
+    from spittle_amd.parakeet import OnnxModelDir
+    from tests import onnx_parakeet
+    P.set_threads(16)
+    d = P.dims_for("parakeet-tdt-0.6b-v2")
+    om = P.Model(d, seed=SEED)
+    path = str(tmp_path / "parakeet-tdt-0.6b-v2-int8")
+    exp = onnx_parakeet.write_dir(path, om, d, quant="int8")
+    h = OnnxModelDir(path)
+    assert h.dims()["n_vocab"] == 1024 and h.dims()["n_layers"] == 24
+    for tid in exp:
+        om.set_tensor(tid, h.tensor(tid))
+    h.close()
+    e = ParakeetEngine()
+    e.load_model_with_params(path, ParakeetModelParams(dtype="f32", max_batch=2, max_seconds=8.0))
+    assert e.info()["n_vocab"] == 1024 and e.info()["n_layers"] == 24
+    pcm = synth_audio(42, 16000 * 3)
+    r = e.transcribe_samples(pcm, _tok_params())
+    i, n_or, gap = _agree(r, om, om.encode(P.mel(pcm)), F32_GAP)
+    assert len(r.tokens) > 0 and all(0 <= t < 1024 for t in r.tokens)
+    assert r.text == "".join(onnx_parakeet.vocab_piece(t) for t in r.tokens).replace("▁", " ").strip()
+    e.unload_model()
+    e.load_model_with_params(path, ParakeetModelParams.int8())
+    r16 = e.transcribe_samples(pcm)
+    assert r16.text and all(0 <= t < 1024 for t in r16.tokens)
     e.unload_model()
