@@ -224,6 +224,19 @@ def decode_window_beam(m: O.Model, enc: np.ndarray, prompt: list, seek: int, see
         if not cands:
             break
         cands.sort(key=lambda c: (-c[1], c[0]))
+        # the cut across decoders: the distinct cumulative scores the live decoders take (step 0:
+        # every decoder takes the single best, later steps skip exact repeats) and the first one
+        # left out.  Exact repeats (identical decoder rows) are deduplicated by equality, which the
+        # GPU reproduces bitwise; a near-tie between different scores is an uncertain decision.
+        live = sum(1 for w in decs if not w.status)
+        distinct = []
+        for c in cands:
+            if not distinct or c[1] != distinct[-1]:
+                distinct.append(c[1])
+            if len(distinct) > (1 if i == 0 else live):
+                break
+        for a, b in zip(distinct, distinct[1:]):
+            gap = min(gap, a - b)
         new, new_sums, cur = list(decs), list(sums), 0
         for d in range(K):
             if decs[d].status:

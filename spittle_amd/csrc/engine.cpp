@@ -579,7 +579,7 @@ void Engine::alloc_workspace() {
             g.ds = (DecState*)c.take(sizeof(DecState));
             g.dx2 = (float*)c.take(R * d * 4);
             g.pend = (float*)c.take((int64_t)kMaxPend * R * d * 4);
-            g.xpart = (float*)c.take((int64_t)R * dm_.n_head * 4 * 66 * 4);
+            g.xpart = (float*)c.take((int64_t)R * dm_.n_head * 8 * 66 * 4);
             g.seek = (int*)c.take(B * 4);
             g.seek_end = (int*)c.take(B * 4);
             g.ts_state = (int*)c.take(B * 16);
@@ -843,7 +843,15 @@ float* Engine::enqueue_layers(DecGroup& g, int E, int Tq) {
     // window map: rows j * share .. + share - 1 attend to window g.kvrow[j * share]; without one,
     // row b attends to window g.b0 + b (the cross-attention key split applies there only)
     const bool mapped = g.share > 0;
-    const int xs = mapped ? 1 : xsplit_;
+    const int runs = B / std::max(1, g.share);
+    // a small grid of unshared rows (B = 1: 20 workgroups) streams each window's K/V through few
+    // CUs: run its 8 waves as 8 workgroups, merged in the output projection (bitwise the same
+    // result).  r4 (profiles/r4/exp_xattn_vw.txt): B = 1 pass 1.609 -> 1.562 ms; slower for the
+    // 5 rows of a beam on one window (2.61 -> 2.66) and for B = 8 (1.81 -> 2.21), so only there.
+    // SPT_XATTN_VW=0: never, 2: always (measurements)
+    static const int vw_env = getenv("SPT_XATTN_VW") ? atoi(getenv("SPT_XATTN_VW")) : 1;
+    const bool vw = vw_env == 2 || (vw_env != 0 && g.share <= 1 && runs * H < 96);
+    const int xs = vw ? 8 : mapped ? 1 : xsplit_;
     const int ks = dt_ == DT_BF16 ? 128 : 64;
     hipStream_t st = g.st;
     float* xc = g.dx;   // current residual rows (dec_embed / dec_finalize wrote this pass's input here)
@@ -893,8 +901,12 @@ float* Engine::enqueue_layers(DecGroup& g, int E, int Tq) {
         a.W = e.cq_w; a.N = d; a.K = d; a.bias = e.cq_b; a.C = g.dq; a.ldc = d;
         gemv(dt_, GV_BIAS, A_LN, a, st);
         consumed();
-        dec_cross_attn(dt_, g.dq, ckv_l, B, E, H, T, Tq, g.dao, st, xs, g.xpart, mapped ? g.kvrow : nullptr,
-                       mapped ? g.share : 1);
+        if (vw)
+            dec_cross_attn_vw(dt_, g.dq, ckv_l, B, E, H, T, Tq, g.xpart, st, mapped ? g.kvrow : nullptr,
+                              mapped ? g.share : 1);
+        else
+            dec_cross_attn(dt_, g.dq, ckv_l, B, E, H, T, Tq, g.dao, st, xs, g.xpart, mapped ? g.kvrow : nullptr,
+                           mapped ? g.share : 1);
         // cross output projection (merging the key chunks in its prologue), residual add in place
         a = GemvArgs{};
         a.A = g.dao; a.lda = d; a.R = R; a.W = e.co_w; a.N = d; a.K = d; a.bias = e.co_b; a.C = xc; a.ldc = d;

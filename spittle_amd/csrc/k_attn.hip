@@ -626,7 +626,7 @@ __global__ __launch_bounds__(256, 1) void attn_f32_kernel(const float* __restric
 
 void enc_attention(int dtype, const void* qkv, int B, int T, int H, void* out, hipStream_t st) {
     static const bool q32 = getenv("SPT_ATTN_Q32") != nullptr;  // A/B switch: 32 queries per wave
-    static const int sum = getenv("SPT_ATTN_SUM") ? atoi(getenv("SPT_ATTN_SUM")) : 3;  // 3: optimistic softmax (r2: 129 -> 124 us)
+    static const int sum = getenv("SPT_ATTN_SUM") ? atoi(getenv("SPT_ATTN_SUM")) : 4;  // 4: scores relative to the running max (r4: 133 -> 127 us); 3: r2-r3 optimistic softmax
     static const int swz = getenv("SPT_ATTN_SWZ") ? atoi(getenv("SPT_ATTN_SWZ")) : 1;
     if (dtype == DT_BF16 && !q32) {
         dim3 g(cdiv(T, 256), H, B);

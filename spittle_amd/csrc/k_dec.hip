@@ -317,10 +317,11 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
             for (int c = 1; c < S; ++c) M = fmaxf(M, mc[c]);
             float L = 0.f, O = 0.f;
 #pragma unroll
-            for (int c = 0; c < S; ++c) {
-                const float f = mc[c] == -INFINITY ? 0.f : exp2f(mc[c] - M);
-                L += lc[c] * f;
-                O += oc[c] * f;
+            for (int c = 0; c < S; ++c) {  // attn_merge's operations (bitwise): skip empty chunks
+                if (mc[c] == -INFINITY) continue;
+                const float f = exp2f(mc[c] - M);
+                L = __builtin_fmaf(lc[c], f, L);
+                O = __builtin_fmaf(oc[c], f, O);
             }
             img[(size_t)r * lds_ld + h * 64 + e] = from_f<T>(O / L);
         }
@@ -494,7 +495,8 @@ void gemv_launch_cfg(const GemvArgs& a, hipStream_t st) {
     X(GV_BIAS_RESID, A_DIRECT)          \
     X(GV_BIAS_RESID, ATTN_SRC(2))       \
     X(GV_BIAS_RESID, ATTN_SRC(3))       \
-    X(GV_BIAS_RESID, ATTN_SRC(4))
+    X(GV_BIAS_RESID, ATTN_SRC(4))       \
+    X(GV_BIAS_RESID, ATTN_SRC(8))
 
 // > 64 KiB of dynamic LDS must be enabled per kernel, outside any stream capture
 template <typename T, int MODE, int ASRC>
@@ -505,7 +507,7 @@ void gemv_attr_all() {
     gemv_attr<T, MODE, ASRC, 4, NWV, CT, MAXJ>();
     if constexpr (MODE == GV_LOGITS) {
         SPT_ATTR(4, 4, 4)
-    } else if constexpr (ASRC == A_DIRECT) {
+    } else if constexpr (ASRC == A_DIRECT || is_attn(ASRC)) {
         SPT_GV_CONFIGS(SPT_ATTR)
     } else {
         SPT_ATTR(4, 1, 2)
@@ -536,7 +538,10 @@ void gemv_launch_rg(const GemvArgs& a, hipStream_t st) {
         // Wide LayerNorm-prologue GEMVs (fc1, N = 4d >= 4096): two column tiles per workgroup,
         // so half as many workgroups re-read the residual rows for their LayerNorm image (r1
         // exp23: fc1 9.4 -> 8.6 us, RTFx +1.2 %; the QKV and cross-Q projections lose with it)
-        if constexpr (ASRC != A_DIRECT) {
+        // an attention-merge prologue (A_ATTN) takes A_DIRECT's geometry: the same waves and K
+        // slices, so the cross output projection of merged key partials is bitwise the projection
+        // of the 8-wave kernel's output (dec_cross_attn_vw)
+        if constexpr (is_ln(ASRC)) {
             // K = 10 super-steps (large-v3's d = 1280 in bf16): 10 waves, each an exact slice, so
             // the LayerNorm does not wait for the weight stream (GV_EXACT_LN=0 restores r1's shapes)
             static const bool exact_ln = !getenv("GV_EXACT_LN") || atoi(getenv("GV_EXACT_LN")) != 0;
@@ -552,7 +557,7 @@ void gemv_launch_rg(const GemvArgs& a, hipStream_t st) {
         }
         if (nss <= 8) gemv_launch_cfg<T, MODE, ASRC, RG, 4, 1, 2>(a, st);
         else if (nss <= 16) gemv_launch_cfg<T, MODE, ASRC, RG, 8, 1, 2>(a, st);
-        else if constexpr (ASRC == A_DIRECT) {  // 16 waves: no room for a staged A image's registers
+        else if constexpr (!is_ln(ASRC)) {  // 16 waves: no room for a staged A image's registers
             if (nss <= 48) gemv_launch_cfg<T, MODE, ASRC, RG, 16, 1, 3>(a, st);
             else throw std::runtime_error("gemv: K too large");
         } else throw std::runtime_error("gemv: K too large for a staged A operand");
@@ -587,23 +592,26 @@ template <> struct KVChunk<float> {
 // space; raw K/V chunks ping-pong so the next block streams in during the current one.
 // qv is pre-scaled by log2(e)/8.  Leaves (m, l, o) per query in the calling lanes.
 // keys per lane: 4 for bf16 (r1 exp10 / exp11: lower register pressure and more resident waves
-// beat deeper per-lane prefetch for both the cross- and the self-attention step), 2 for f32 prompts
-template <typename T, int NQ, int NI_ = 0, int NW = AW>
+// beat more keys per lane for both the cross- and the self-attention step), 2 for f32 prompts.
+// PF: key blocks in the register ring (PF - 1 in flight while one is processed); the blocks are
+// processed in the same order whatever PF is, so PF changes no result bit.
+template <typename T, int NQ, int NI_ = 0, int NW = AW, int PF = 2>
 struct AttnWave {
     static constexpr int NI = NI_ > 0 ? NI_ : (sizeof(T) == 2) ? 4 : (NQ == 1 ? 4 : 2);
     static constexpr int KB = 8 * NI;  // keys per block
-    KVChunk<T> kA[NI], vA[NI], kB[NI], vB[NI];
+    static_assert(PF >= 2 && PF <= 4, "AttnWave: 2..4 ring slots");
+    KVChunk<T> kc_[PF][NI], vc_[PF][NI];
     float m[NQ], l[NQ], o[NQ][8];
     const T *Kb, *Vb;
     int n_keys, slot;
-    int64_t bstride = 0;  // 0: key rows contiguous ([T][64]); else 32-key blocks this far apart
+    int64_t bstride = 2048;  // 32-key blocks this far apart (2048: key rows contiguous, [T][64])
 
     __device__ __forceinline__ void init(const T* K, const T* V, int nk, int lane, int64_t blk_stride = 0) {
         slot = lane >> 3;
         Kb = K;
         Vb = V;
         n_keys = nk;
-        bstride = blk_stride;
+        bstride = blk_stride ? blk_stride : 32 * 64;  // one branch-free offset formula for both layouts
 #pragma unroll
         for (int t = 0; t < NQ; ++t) {
             m[t] = -INFINITY;
@@ -616,13 +624,19 @@ struct AttnWave {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             const int key = min(blk * KB + 8 * i + slot, n_keys - 1);
-            const size_t off = bstride ? (size_t)(key >> 5) * bstride + (size_t)(key & 31) * 64 : (size_t)key * 64;
+            const size_t off = (size_t)(key >> 5) * bstride + (size_t)(key & 31) * 64;
             kc[i].load(Kb + off);
             vc[i].load(Vb + off);
         }
     }
+    // The arithmetic is spelled out (contraction off, explicit fmaf): every inlined instance of this
+    // step -- per query t, per key block, per kernel (8-wave, single-wave, chunked queries) -- then
+    // computes the same bits.  r4: left to the compiler, the fully unrolled schedule contracted
+    // some instances differently, so identical decoder rows (a beam's first steps) in different
+    // query chunks differed in the last bit and whisper.cpp's exact-equality candidate dedup failed.
     __device__ __forceinline__ void process(const KVChunk<T> (&kc)[NI], const KVChunk<T> (&vc)[NI], int kbase,
                                             const float (&qv)[NQ][8], const int (&lim)[NQ], int Tq) {
+#pragma clang fp contract(off)
 #pragma unroll
         for (int t = 0; t < NQ; ++t) {
             if (t >= Tq) break;
@@ -632,7 +646,7 @@ struct AttnWave {
             for (int i = 0; i < NI; ++i) {
                 float v = 0.f;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) v += qv[t][e] * kc[i].at(e);
+                for (int e = 0; e < 8; ++e) v = __builtin_fmaf(qv[t][e], kc[i].at(e), v);
                 v += __shfl_xor(v, 1, 64);
                 v += __shfl_xor(v, 2, 64);
                 v += __shfl_xor(v, 4, 64);
@@ -654,26 +668,44 @@ struct AttnWave {
                 const float p = exp2f(s[i] - mn);
                 ls += p;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) o[t][e] += p * vc[i].at(e);
+                for (int e = 0; e < 8; ++e) o[t][e] = __builtin_fmaf(p, vc[i].at(e), o[t][e]);
             }
-            l[t] = l[t] * alpha + ls;
+            l[t] = __builtin_fmaf(l[t], alpha, ls);
             m[t] = mn;
         }
     }
-    // blocks blk0 + w, blk0 + w + NW, ... below nblk; the first block may already be in flight
-    __device__ __forceinline__ void run(int blk, int nblk, bool first_loaded, const float (&qv)[NQ][8],
-                                        const int (&lim)[NQ], int Tq) {
-        if (blk < nblk && !first_loaded) load_blk(kA, vA, blk);
+    // blocks blk0 + w, blk0 + w + NW, ... below nblk, PF - 1 of them loading ahead.  MAXB bounds the
+    // blocks one wave takes (a fully unrolled, straight-line schedule with unconditional loads:
+    // past the wave's last block they repeat it, L1/L2 hits, never processed).  r4: in a rolled loop
+    // whose ring registers rotate, the compiler drained every load in flight (vmcnt(0)) at the
+    // loop head, so no block was ever in flight while another was processed.  More blocks than
+    // MAXB (never for Whisper's 1500 keys / 448 positions) take the rolled loop.
+    template <int MAXB>
+    __device__ __forceinline__ void run(int blk, int nblk, const float (&qv)[NQ][8], const int (&lim)[NQ], int Tq) {
+        if (blk >= nblk) return;
+        const int cnt = (nblk - 1 - blk) / NW + 1;  // this wave's blocks
+        const int mine = blk + (cnt - 1) * NW;      // its last one
+        if (MAXB <= 8 && cnt <= MAXB) {  // (longer schedules are not unrolled: the f32 prompt kernels)
+#pragma unroll
+            for (int d = 0; d < PF - 1 && d < MAXB; ++d) load_blk(kc_[d], vc_[d], min(blk + d * NW, mine));
+#pragma unroll
+            for (int i = 0; i < (MAXB <= 8 ? MAXB : 1); ++i) {
+                if (i >= cnt) break;
+                if (i + PF - 1 < (MAXB <= 8 ? MAXB : 1))
+                    load_blk(kc_[(i + PF - 1) % PF], vc_[(i + PF - 1) % PF], min(blk + (i + PF - 1) * NW, mine));
+                process(kc_[i % PF], vc_[i % PF], (blk + i * NW) * KB, qv, lim, Tq);
+            }
+            return;
+        }
+        load_blk(kc_[0], vc_[0], blk);
         while (blk < nblk) {
-            int nb = blk + NW;
-            if (nb < nblk) load_blk(kB, vB, nb);
-            process(kA, vA, blk * KB, qv, lim, Tq);
-            blk = nb;
+            load_blk(kc_[1], vc_[1], min(blk + NW, mine));
+            process(kc_[0], vc_[0], blk * KB, qv, lim, Tq);
+            blk += NW;
             if (blk >= nblk) break;
-            nb = blk + NW;
-            if (nb < nblk) load_blk(kA, vA, nb);
-            process(kB, vB, blk * KB, qv, lim, Tq);
-            blk = nb;
+            load_blk(kc_[0], vc_[0], min(blk + NW, mine));
+            process(kc_[1], vc_[1], blk * KB, qv, lim, Tq);
+            blk += NW;
         }
     }
     // sum l and o over the 8 key slots of the wave (m is wave-uniform) into LDS
@@ -710,17 +742,18 @@ struct AttnWave {
 template <int NQ, int NW = AW>
 __device__ __forceinline__ void attn_merge(const float (*s_m)[NQ], const float (*s_l)[NQ], const float (*s_o)[NQ][64],
                                            int t, int e, float& M, float& L, float& O) {
+#pragma clang fp contract(off)
     M = -INFINITY;
 #pragma unroll
     for (int w = 0; w < NW; ++w) M = fmaxf(M, s_m[w][t]);
     L = 0.f;
     O = 0.f;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) {
+    for (int w = 0; w < NW; ++w) {  // the same operations as the GEMV's A_ATTN merge (bitwise)
         if (s_m[w][t] == -INFINITY) continue;
         const float f = exp2f(s_m[w][t] - M);
-        L += s_l[w][t] * f;
-        O += s_o[w][t][e] * f;
+        L = __builtin_fmaf(s_l[w][t], f, L);
+        O = __builtin_fmaf(s_o[w][t][e], f, O);
     }
 }
 
@@ -749,7 +782,7 @@ __global__ __launch_bounds__(64 * AW) void self_attn_kernel(const T* __restrict_
         for (int e = 0; e < 8; ++e) qv[t][e] = to_f<T>(qr[e]) * kLog2Scale;
         lim[t] = pos0 + tt + 1;
     }
-    aw.run(wid, cdiv(n_keys, AttnWave<T, NQ, NIX>::KB), false, qv, lim, Tq);
+    aw.template run<(448 / AttnWave<T, NQ, NIX>::KB + 1 + AW - 1) / AW>(wid, cdiv(n_keys, AttnWave<T, NQ, NIX>::KB), qv, lim, Tq);
     aw.to_lds(s_m, s_l, s_o, wid, lane);
     __syncthreads();
     if (tid < 64 * Tq) {
@@ -767,12 +800,12 @@ __global__ __launch_bounds__(64 * AW) void self_attn_kernel(const T* __restrict_
 // each), so the decoders of one utterance (beam / best_of) read its window's K/V once per chunk.
 // (A fused LayerNorm + cross-Q projection prologue and key-chunk splits were measured slower on
 // MI355X: r1 exp_fused_xattn_pending_slabs.txt.)
-template <typename T, int NQ, bool SPLIT, int NW = AW, int NIX = 0>
+template <typename T, int NQ, bool SPLIT, int NW = AW, int NIX = 0, int PF = 2>
 __global__ __launch_bounds__(64 * NW) void cross_attn_kernel(const T* __restrict__ q, const T* __restrict__ kv,
                                                              int B_layout, int H, int T_enc, int Tq,
                                                              T* __restrict__ out, float* __restrict__ part,
                                                              const int* __restrict__ kvrow, int share) {
-    typedef AttnWave<T, NQ, NIX, NW> W;
+    typedef AttnWave<T, NQ, NIX, NW, PF> W;
     XA_STAMP(0);
     __shared__ float s_m[NW][NQ], s_l[NW][NQ];
     __shared__ float s_o[NW][NQ][64];
@@ -800,7 +833,7 @@ __global__ __launch_bounds__(64 * NW) void cross_attn_kernel(const T* __restrict
     const int nblk_all = cdiv(T_enc, W::KB);
     const int S = SPLIT ? (int)gridDim.y : 1, sp = SPLIT ? (int)blockIdx.y : 0;
     const int per = cdiv(nblk_all, S), blk0 = sp * per, nblk = min(nblk_all, blk0 + per);
-    aw.run(blk0 + wid, nblk, false, qv, lim, nq);
+    aw.template run<(1500 / W::KB + 1 + NW - 1) / NW>(blk0 + wid, nblk, qv, lim, nq);
     if (wid == 0) XA_STAMP(1);
     aw.to_lds(s_m, s_l, s_o, wid, lane);
     __syncthreads();
@@ -818,6 +851,57 @@ __global__ __launch_bounds__(64 * NW) void cross_attn_kernel(const T* __restrict
             }
         } else {
             out[(qrow0 + t) * (H * 64) + h * 64 + e] = from_f<T>(O / L);
+        }
+    }
+}
+
+// The same cross-attention with each of the 8 waves of a (row run, h) workgroup as a workgroup
+// of its own (grid.y = the wave index w, grid.z = the query chunk): wave w of the 8-wave kernel
+// and workgroup w here run the same AttnWave over the same key blocks (w, w + 8, ...), and each
+// writes its {o[64], m, l} as partial w of [rows][H][8][66]; the cross output projection's A_ATTN
+// prologue merges the 8 partials in order w = 0..7 with attn_merge's arithmetic.  A row's result
+// is therefore bitwise the 8-wave kernel's, and the choice between the two is free: this one runs
+// when the 8-wave grid is small (B = 1, or the decoders of one utterance sharing a window), where
+// 20 workgroups would stream 7.7 MB per layer through 20 CUs.
+template <typename T, int NQ, int NIX = 0, int PF = 2>
+__global__ __launch_bounds__(64) void cross_attn_vw_kernel(const T* __restrict__ q, const T* __restrict__ kv,
+                                                           int B_layout, int H, int T_enc, int Tq,
+                                                           float* __restrict__ part, const int* __restrict__ kvrow,
+                                                           int share) {
+    typedef AttnWave<T, NQ, NIX, AW, PF> W;  // block stride AW = the 8-wave kernel's waves
+    __shared__ float s_m[1][NQ], s_l[1][NQ];
+    __shared__ float s_o[1][NQ][64];
+    const int bh = blockIdx.x, j = bh / H, h = bh - j * H;
+    const int vw = blockIdx.y;                              // the 8-wave kernel's wave index
+    const int lane = threadIdx.x, g = lane & 7;
+    const int nq_all = share * Tq;
+    const int c0 = (int)blockIdx.z * NQ;
+    const int nq = min(NQ, nq_all - c0);
+    const int kb = kvrow ? kvrow[j * share] : j;
+    W aw;
+    const size_t kvo = ((size_t)kb * H + h) * 4096 + 8 * g;
+    aw.init(kv + kvo, kv + kvo + 2048, T_enc, lane, (int64_t)B_layout * H * 4096);
+    const size_t qrow0 = (size_t)j * nq_all + c0;
+    float qv[NQ][8];
+    int lim[NQ];
+#pragma unroll
+    for (int t = 0; t < NQ; ++t) {
+        const int tt = t < nq ? t : nq - 1;
+        const T* qr = q + (qrow0 + tt) * (H * 64) + h * 64 + 8 * g;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qv[t][e] = to_f<T>(qr[e]) * kLog2Scale;
+        lim[t] = T_enc;
+    }
+    aw.template run<(1500 / W::KB + 1 + AW - 1) / AW>(vw, cdiv(T_enc, W::KB), qv, lim, nq);
+    aw.to_lds(s_m, s_l, s_o, 0, lane);
+    __syncthreads();
+    for (int i = lane; i < 64 * nq; i += 64) {
+        const int t = i >> 6, e = i & 63;
+        float* pp = part + (((qrow0 + t) * H + h) * AW + vw) * 66;
+        pp[e] = s_o[0][t][e];
+        if (e == 0) {
+            pp[64] = s_m[0][t];
+            pp[65] = s_l[0][t];
         }
     }
 }
@@ -923,8 +1007,8 @@ void gemv(int dtype, int mode, int asrc, const GemvArgs& a_in, hipStream_t st) {
     if (asrc == A_LN)
         for (int p = 0; p < 4; ++p)
             if (!a.pend[p]) throw std::runtime_error("gemv: LayerNorm prologue needs 4 pending slabs (zero slab if none)");
-    if (asrc == A_ATTN && (!a.apart || a.a_splits < 2 || a.a_splits > 4 || a.a_heads * 64 != a.K))
-        throw std::runtime_error("gemv: attention-merge prologue needs 2..4 chunks over all heads");
+    if (asrc == A_ATTN && (!a.apart || a.a_splits < 2 || (a.a_splits > 4 && a.a_splits != 8) || a.a_heads * 64 != a.K))
+        throw std::runtime_error("gemv: attention-merge prologue needs 2..4 or 8 chunks over all heads");
     const int code = asrc == A_LN ? LN_SRC(a.n_pend) : asrc == A_ATTN ? ATTN_SRC(a.a_splits) : asrc;
 #define SPT_GV(M, S)                                                      \
     if (mode == M && code == S) {                                         \
@@ -960,6 +1044,12 @@ void dec_self_attn(int dtype, const void* q, const void* cache, int B, int H, in
     SPT_LAUNCH_CHECK();
 }
 
+// key blocks in each cross-attention wave's register ring (SPT_XATTN_PF = 2..4; no result changes)
+static int xattn_pf() {
+    static const int pf = getenv("SPT_XATTN_PF") ? std::max(2, std::min(4, atoi(getenv("SPT_XATTN_PF")))) : 2;
+    return pf;
+}
+
 void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int B_layout, int H, int T_enc, int Tq, void* out,
                     hipStream_t st, int splits, float* part, const int* kvrow, int share) {
     if (Tq < 1 || Tq > 4) throw std::runtime_error("dec_cross_attn: 1..4 queries per sequence");
@@ -975,12 +1065,17 @@ void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int B_layou
     const int NQ = nq == 1 ? 1 : Tq > 1 ? 4 : (dtype == DT_BF16 ? 5 : 4);
     if (splits > 1 && nq > NQ) throw std::runtime_error("dec_cross_attn: key chunks need one query chunk per window");
     const dim3 grid((B / share) * H, splits > 1 ? splits : cdiv(nq, NQ)), blk(64 * AW);
-#define SPT_XA(T, NQ_, SP, NI)                                                                                  \
-    hipLaunchKernelGGL((cross_attn_kernel<T, NQ_, SP, AW, NI>), grid, blk, 0, st, (const T*)q, (const T*)kv,      \
-                       B_layout, H, T_enc, Tq, (T*)out, part, kvrow, share)
+#define SPT_XA(T, NQ_, SP, NI, ...)                                                                             \
+    hipLaunchKernelGGL((cross_attn_kernel<T, NQ_, SP, AW, NI __VA_ARGS__>), grid, blk, 0, st, (const T*)q,        \
+                       (const T*)kv, B_layout, H, T_enc, Tq, (T*)out, part, kvrow, share)
     // NI = 4 for the step kernels of both dtypes (AttnWave's default at NQ = 1)
 #define SPT_XA_T(T)                                                                       \
-    if (NQ == 1) { if (splits > 1) SPT_XA(T, 1, true, 0); else SPT_XA(T, 1, false, 0); }  \
+    if (NQ == 1) {                                                                        \
+        if (splits > 1) SPT_XA(T, 1, true, 0);                                            \
+        else if (xattn_pf() == 4) SPT_XA(T, 1, false, 0, , 4);                            \
+        else if (xattn_pf() == 3) SPT_XA(T, 1, false, 0, , 3);                            \
+        else SPT_XA(T, 1, false, 0);                                                      \
+    }                                                                                     \
     else if (NQ == 4 && Tq > 1) { if (splits > 1) SPT_XA(T, 4, true, 0); else SPT_XA(T, 4, false, 0); } \
     else if (NQ == 4) { if (splits > 1) SPT_XA(T, 4, true, 4); else SPT_XA(T, 4, false, 4); } \
     else { if (splits > 1) SPT_XA(T, 5, true, 4); else SPT_XA(T, 5, false, 4); }
@@ -988,6 +1083,36 @@ void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int B_layou
     else { SPT_XA_T(float); }
 #undef SPT_XA_T
 #undef SPT_XA
+    SPT_LAUNCH_CHECK();
+}
+
+void dec_cross_attn_vw(int dtype, const void* q, const void* kv, int B, int B_layout, int H, int T_enc, int Tq,
+                       float* part, hipStream_t st, const int* kvrow, int share) {
+    if (Tq < 1 || Tq > 4) throw std::runtime_error("dec_cross_attn_vw: 1..4 queries per sequence");
+    if (share < 1 || share > 8 || B % share) throw std::runtime_error("dec_cross_attn_vw: rows per window 1..8, dividing B");
+    if (share > 1 && !kvrow) throw std::runtime_error("dec_cross_attn_vw: shared windows need the window map");
+    if (!part) throw std::runtime_error("dec_cross_attn_vw: needs the partials buffer");
+    const int nq = share * Tq;
+    // the same query chunks and keys per lane as dec_cross_attn (bitwise the same partials)
+    const int NQ = nq == 1 ? 1 : Tq > 1 ? 4 : (dtype == DT_BF16 ? 5 : 4);
+    const dim3 grid((B / share) * H, AW, cdiv(nq, NQ)), blk(64);
+#define SPT_XV(T, NQ_, NI, PF)                                                                               \
+    hipLaunchKernelGGL((cross_attn_vw_kernel<T, NQ_, NI, PF>), grid, blk, 0, st, (const T*)q, (const T*)kv,      \
+                       B_layout, H, T_enc, Tq, part, kvrow, share)
+#define SPT_XV_PF(T, NQ_, NI)                                    \
+    if (xattn_pf() == 4) SPT_XV(T, NQ_, NI, 4);                  \
+    else if (xattn_pf() == 3) SPT_XV(T, NQ_, NI, 3);             \
+    else SPT_XV(T, NQ_, NI, 2);
+#define SPT_XV_T(T)                                         \
+    if (NQ == 1) { SPT_XV_PF(T, 1, 0) }                     \
+    else if (NQ == 4 && Tq > 1) SPT_XV(T, 4, 0, 2);         \
+    else if (NQ == 4) SPT_XV(T, 4, 4, 2);                   \
+    else { SPT_XV_PF(T, 5, 4) }
+    if (dtype == DT_BF16) { SPT_XV_T(bf16); }
+    else { SPT_XV_T(float); }
+#undef SPT_XV_T
+#undef SPT_XV_PF
+#undef SPT_XV
     SPT_LAUNCH_CHECK();
 }
 

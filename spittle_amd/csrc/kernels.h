@@ -131,7 +131,7 @@ struct GemvArgs {
     const float* ln_w; const float* ln_b; // A_LN: LayerNorm of x + pend[0] + .. + pend[3]
     const float* pend[4]; int n_pend;     // A_LN: pending partial slabs (same layout as A): n_pend = 0, 2 or 4
     float* x_out;                         // A_LN: combined rows written here by workgroup (0, 0) (or nullptr)
-    const float* apart; int a_splits, a_heads;  // A_ATTN: cross-attention chunk partials [R][H][S][66]
+    const float* apart; int a_splits, a_heads;  // A_ATTN: cross-attention chunk partials [R][H][S][66] (S = 2..4, 8)
     int R;                                // rows (<= 64)
     const void* W; int N, K;              // W [N][K]
     const float* bias;
@@ -173,6 +173,11 @@ void dec_self_attn(int dtype, const void* q, const void* cache, int B, int H, in
 void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int B_layout, int H, int T_enc, int Tq,
                     void* out, hipStream_t st, int splits = 1, float* part = nullptr, const int* kvrow = nullptr,
                     int share = 1);
+// the same attention with each of the 8 waves of a (row run, head) workgroup as a workgroup of its
+// own: writes partial w of [rows][H][8][66] = {o[64], m, l} (merged by an A_ATTN GEMV with 8
+// chunks); bitwise the 8-wave kernel's result once merged, for small grids (B / share * H small)
+void dec_cross_attn_vw(int dtype, const void* q, const void* kv, int B, int B_layout, int H, int T_enc, int Tq,
+                       float* part, hipStream_t st, const int* kvrow = nullptr, int share = 1);
 
 struct FinalizeArgs {
     const void* part; int n_tiles;        // logits top-2 partials [B][n_tiles]
