@@ -4,6 +4,8 @@ import os
 import sys
 import time
 
+import torch  # noqa: F401  (as bench.py: rocprofv3 crashed at start-up in a process that loaded the HIP runtime first)
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from spittle_amd import WhisperEngine, WhisperInferenceParams, WhisperModelParams  # noqa: E402
 from spittle_amd.synth import synth_audio  # noqa: E402

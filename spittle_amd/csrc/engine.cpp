@@ -587,7 +587,6 @@ void Engine::alloc_workspace() {
             g.beam_row = (int*)c.take(B * 16);
             g.beam_step = (int*)c.take(64);
             g.beam_src = (int*)c.take(B * 4);
-            g.beam_ident = (int*)c.take(B * 4);
             g.cand_id = (int*)c.take(B * 8 * 4);
             g.cand_lp = (float*)c.take(B * 8 * 4);
             g.beam_tid = (int*)c.take(B * 4);
@@ -844,13 +843,16 @@ float* Engine::enqueue_layers(DecGroup& g, int E, int Tq) {
     // row b attends to window g.b0 + b (the cross-attention key split applies there only)
     const bool mapped = g.share > 0;
     const int runs = B / std::max(1, g.share);
-    // a small grid of unshared rows (B = 1: 20 workgroups) streams each window's K/V through few
-    // CUs: run its 8 waves as 8 workgroups, merged in the output projection (bitwise the same
-    // result).  r4 (profiles/r4/exp_xattn_vw.txt): B = 1 pass 1.609 -> 1.562 ms; slower for the
-    // 5 rows of a beam on one window (2.61 -> 2.66) and for B = 8 (1.81 -> 2.21), so only there.
-    // SPT_XATTN_VW=0: never, 2: always (measurements)
+    // a small grid (B = 1: 20 workgroups; a beam's 5 rows on one window: 20) streams each window's
+    // K/V through few CUs: run its 8 waves as 8 workgroups, merged in the output projection, and
+    // for one-token steps of shared rows one query per workgroup (the 8 x 5 workgroups per head
+    // re-read the window's 384 KB from L2) -- all bitwise the same result.  r4
+    // (profiles/r4/exp_xattn_vw.txt, exp_beam_step.txt): B = 1 pass 1.609 -> 1.562 ms; the 5-query
+    // workgroups of a beam took 29 us per layer; B = 8 (160 workgroups) stays on the 8-wave kernel.
+    // SPT_XATTN_VW=0: never, 2: always, 3: small grids without the per-query split (measurements)
     static const int vw_env = getenv("SPT_XATTN_VW") ? atoi(getenv("SPT_XATTN_VW")) : 1;
-    const bool vw = vw_env == 2 || (vw_env != 0 && g.share <= 1 && runs * H < 96);
+    const bool vw = vw_env == 2 || (vw_env != 0 && runs * H < 96);
+    const bool per_query = vw && Tq == 1 && vw_env != 3;
     const int xs = vw ? 8 : mapped ? 1 : xsplit_;
     const int ks = dt_ == DT_BF16 ? 128 : 64;
     hipStream_t st = g.st;
@@ -903,7 +905,7 @@ float* Engine::enqueue_layers(DecGroup& g, int E, int Tq) {
         consumed();
         if (vw)
             dec_cross_attn_vw(dt_, g.dq, ckv_l, B, E, H, T, Tq, g.xpart, st, mapped ? g.kvrow : nullptr,
-                              mapped ? g.share : 1);
+                              mapped ? g.share : 1, per_query);
         else
             dec_cross_attn(dt_, g.dq, ckv_l, B, E, H, T, Tq, g.dao, st, xs, g.xpart, mapped ? g.kvrow : nullptr,
                            mapped ? g.share : 1);
@@ -1349,11 +1351,9 @@ void Engine::beam_begin(int B, const DecodeRequest& rq, BeamCands* out, int* lan
     }
     beam_rq_ = rq;
     beam_B_ = B;
+    beam_side_ = 0;  // the prompt pass writes the group's own cache
     std::vector<int> tok((size_t)B * rq.n_steps);
     decode(B, rq, tok.data(), nullptr, nullptr, lang_out, nullptr);
-    std::vector<int> ident(B);
-    for (int b = 0; b < B; ++b) ident[b] = b;
-    HIP_CHECK(hipMemcpy(groups_[0].beam_ident, ident.data(), B * 4, hipMemcpyHostToDevice));
     read_cands(B, out);
 }
 
@@ -1375,14 +1375,22 @@ void Engine::beam_next(const int* src, const int* tokens, const int* rowstate, i
     HIP_CHECK(hipMemcpyAsync(g.tok_in, h + B, B * 4, hipMemcpyHostToDevice, g.st));
     HIP_CHECK(hipMemcpyAsync(g.beam_row, h + 2 * B, (size_t)B * 16, hipMemcpyHostToDevice, g.st));
     HIP_CHECK(hipMemcpyAsync(g.beam_step, h + 6 * B, 4, hipMemcpyHostToDevice, g.st));
-    // one captured graph per (rows, candidates, flags, length): reorder the self-K/V rows
-    // (positions < pos0) through the scratch, feed the tokens, the decoder pass and the
-    // candidates kernel.  The uploads above stay outside: the graph reads them in place.
+    // one captured graph per (rows, candidates, flags, length, cache side): gather the self-K/V
+    // rows (positions < pos0) from the side holding them into the other side, which this step's
+    // layers then append to and read (the two sides alternate: one gather per step, not a gather
+    // into the scratch and a copy back), feed the tokens, the decoder pass and the candidates
+    // kernel.  The uploads above stay outside: the graph reads them in place.  (The next window's
+    // prompt pass writes the group's own cache from position 0, so either side may end a search.)
+    const int side = beam_side_;
+    void* const own = g.skv;
+    void* const kv_from = side ? kvtmp_ : own;
+    void* const kv_to = side ? own : kvtmp_;
     auto beam_pass = [&] {
-        dec_kv_gather(dt_, g.skv, kvtmp_, g.beam_src, dm_.n_dec, B, dm_.n_head, dm_.n_text_ctx, g.ds, g.st);
-        dec_kv_gather(dt_, kvtmp_, g.skv, g.beam_ident, dm_.n_dec, B, dm_.n_head, dm_.n_text_ctx, g.ds, g.st);
+        dec_kv_gather(dt_, kv_from, kv_to, g.beam_src, dm_.n_dec, B, dm_.n_head, dm_.n_text_ctx, g.ds, g.st);
         dec_embed(dt_, g.tok_in, B, 1, dm_.d, tok_emb_, dec_pos_, g.ds, g.dx, g.st);
+        g.skv = kv_to;
         float* x = enqueue_layers(g, enc_E_, 1);
+        g.skv = own;
         enqueue_head(g, 1, beam_rq_, beam_rq_.n_steps, x, suppress_, (beam_rq_.flags & 1u) != 0);
     };
     static const bool no_graph = getenv("SPT_NO_GRAPH") != nullptr;
@@ -1391,7 +1399,7 @@ void Engine::beam_next(const int* src, const int* tokens, const int* rowstate, i
         beam_pass();
     } else {
         // n_forced = -beam_k marks a beam-step graph (a real n_forced is >= 0)
-        GraphKey key{B, enc_E_, 0, beam_rq_.n_steps, -beam_rq_.beam_k, beam_rq_.flags, beam_rq_.full};
+        GraphKey key{B, enc_E_, side, beam_rq_.n_steps, -beam_rq_.beam_k, beam_rq_.flags, beam_rq_.full};  // b0: cache side
         key.share = g.share;
         auto it = g.graphs.find(key);
         if (it == g.graphs.end()) {
@@ -1407,6 +1415,7 @@ void Engine::beam_next(const int* src, const int* tokens, const int* rowstate, i
         HIP_CHECK(hipGraphLaunch(it->second, g.st));
     }
     HIP_CHECK(hipEventRecord(ev_[9], g.st));
+    beam_side_ ^= 1;
     read_cands(B, out);  // synchronises g.st
     float ms = 0.0f;
     HIP_CHECK(hipEventElapsedTime(&ms, ev_[8], ev_[9]));

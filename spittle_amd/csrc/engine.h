@@ -180,7 +180,7 @@ private:
         float* xpart = nullptr;       // cross-attention chunk partials [R][H][<=4][66]
         int *seek = nullptr, *seek_end = nullptr, *ts_state = nullptr;  // whisper_full decoding
         TsParams* prm = nullptr;
-        int *beam_row = nullptr, *beam_step = nullptr, *beam_src = nullptr, *beam_ident = nullptr;  // beam search
+        int *beam_row = nullptr, *beam_step = nullptr, *beam_src = nullptr;  // beam search
         int *cand_id = nullptr, *beam_tid = nullptr;
         float* cand_lp = nullptr;
         int* kvrow = nullptr;         // [B] encoded window of each row (window map)
@@ -268,6 +268,7 @@ private:
     std::vector<int> ts_init_;
     DecodeRequest beam_rq_;      // the request of the beam search in progress
     int beam_B_ = 0;
+    int beam_side_ = 0;          // the self-K/V side holding the search's rows: 0 the group's cache, 1 kvtmp_
     void* kvtmp_ = nullptr;      // self-K/V reorder scratch (allocated on first beam search)
     std::vector<int> beam_host_;  // host sources of the per-step uploads
     void read_cands(int B, BeamCands* out);

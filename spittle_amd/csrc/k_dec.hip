@@ -297,33 +297,49 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
         // flash-decoding merge of the S chunks: heads covering this workgroup's K range;
         // thread <-> (row r, head h, element e)
         constexpr int S = attn_s(ASRC);
-        T* img = (T*)smem;
+        SPT_LDS T* img = (SPT_LDS T*)smem;  // LDS-typed: the stores cannot alias the partials' loads
         const int H = a.a_heads;
         const int h0 = (ss0 * KS) >> 6, h1 = min(H, (ss1 * KS + 63) >> 6);
         const int nh = h1 - h0;
-        for (int idx = tid; idx < a.R * nh * 64; idx += 64 * NWV) {
-            const int r = idx / (nh * 64), rem = idx - r * nh * 64;
-            const int h = h0 + (rem >> 6), e = rem & 63;
-            const float* pp = a.apart + ((size_t)r * H + h) * S * 66;
-            float mc[S], lc[S], oc[S];
+        const int total = a.R * nh * 64;
+        // four elements per thread per round, every partial load of the round issued before any
+        // merge (r4: one element per round waited a full L2 round trip each -- 16 us for the 5 x 20
+        // heads of a beam step, profiles/r4/exp_beam_step.txt)
+        constexpr int U = 4;
+        for (int base = tid; base < total; base += U * 64 * NWV) {
+            float mc[U][S], lc[U][S], oc[U][S];
 #pragma unroll
-            for (int c = 0; c < S; ++c) {
-                mc[c] = pp[c * 66 + 64];
-                lc[c] = pp[c * 66 + 65];
-                oc[c] = pp[c * 66 + e];
+            for (int u = 0; u < U; ++u) {
+                const int idx = min(base + u * 64 * NWV, total - 1);
+                const int r = idx / (nh * 64), rem = idx - r * nh * 64;
+                const int h = h0 + (rem >> 6), e = rem & 63;
+                const float* pp = a.apart + ((size_t)r * H + h) * S * 66;
+#pragma unroll
+                for (int c = 0; c < S; ++c) {
+                    mc[u][c] = pp[c * 66 + 64];
+                    lc[u][c] = pp[c * 66 + 65];
+                    oc[u][c] = pp[c * 66 + e];
+                }
             }
-            float M = mc[0];
 #pragma unroll
-            for (int c = 1; c < S; ++c) M = fmaxf(M, mc[c]);
-            float L = 0.f, O = 0.f;
+            for (int u = 0; u < U; ++u) {
+                const int idx = base + u * 64 * NWV;
+                if (idx >= total) break;
+                const int r = idx / (nh * 64), rem = idx - r * nh * 64;
+                const int h = h0 + (rem >> 6), e = rem & 63;
+                float M = mc[u][0];
 #pragma unroll
-            for (int c = 0; c < S; ++c) {  // attn_merge's operations (bitwise): skip empty chunks
-                if (mc[c] == -INFINITY) continue;
-                const float f = exp2f(mc[c] - M);
-                L = __builtin_fmaf(lc[c], f, L);
-                O = __builtin_fmaf(oc[c], f, O);
+                for (int c = 1; c < S; ++c) M = fmaxf(M, mc[u][c]);
+                float L = 0.f, O = 0.f;
+#pragma unroll
+                for (int c = 0; c < S; ++c) {  // attn_merge's operations (bitwise): skip empty chunks
+                    if (mc[u][c] == -INFINITY) continue;
+                    const float f = exp2f(mc[u][c] - M);
+                    L = __builtin_fmaf(lc[u][c], f, L);
+                    O = __builtin_fmaf(oc[u][c], f, O);
+                }
+                img[(size_t)r * lds_ld + h * 64 + e] = from_f<T>(O / L);
             }
-            img[(size_t)r * lds_ld + h * 64 + e] = from_f<T>(O / L);
         }
         __syncthreads();
     }
@@ -1087,14 +1103,16 @@ void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int B_layou
 }
 
 void dec_cross_attn_vw(int dtype, const void* q, const void* kv, int B, int B_layout, int H, int T_enc, int Tq,
-                       float* part, hipStream_t st, const int* kvrow, int share) {
+                       float* part, hipStream_t st, const int* kvrow, int share, bool per_query) {
     if (Tq < 1 || Tq > 4) throw std::runtime_error("dec_cross_attn_vw: 1..4 queries per sequence");
     if (share < 1 || share > 8 || B % share) throw std::runtime_error("dec_cross_attn_vw: rows per window 1..8, dividing B");
     if (share > 1 && !kvrow) throw std::runtime_error("dec_cross_attn_vw: shared windows need the window map");
     if (!part) throw std::runtime_error("dec_cross_attn_vw: needs the partials buffer");
     const int nq = share * Tq;
-    // the same query chunks and keys per lane as dec_cross_attn (bitwise the same partials)
-    const int NQ = nq == 1 ? 1 : Tq > 1 ? 4 : (dtype == DT_BF16 ? 5 : 4);
+    // the same query chunks and keys per lane as dec_cross_attn (bitwise the same partials); per_query
+    // (one-token steps): one query per workgroup, the window's K/V re-read per query from L2 -- the
+    // same 4 keys per lane as the shared kernels' NIX = 4, so still bitwise the same partials
+    const int NQ = (nq == 1 || (per_query && Tq == 1)) ? 1 : Tq > 1 ? 4 : (dtype == DT_BF16 ? 5 : 4);
     const dim3 grid((B / share) * H, AW, cdiv(nq, NQ)), blk(64);
 #define SPT_XV(T, NQ_, NI, PF)                                                                               \
     hipLaunchKernelGGL((cross_attn_vw_kernel<T, NQ_, NI, PF>), grid, blk, 0, st, (const T*)q, (const T*)kv,      \

@@ -45,6 +45,16 @@ __device__ __forceinline__ MaxI max_merge(MaxI a, MaxI b) {
     return (b.v > a.v || (b.v == a.v && b.i < a.i)) ? b : a;
 }
 
+// The per-row vocabulary kernels below hold a thread's logits in registers: VJ per thread, strided
+// n = tid + j * TW (V <= VJ * TW = 53248 covers Whisper's 51864..51866; checked at launch), every
+// load issued before the first use.  r4: a loop that loaded one logit per iteration waited a full
+// memory round trip per iteration (the beam candidate kernel took 214 us per step,
+// profiles/r4/exp_beam_step.txt).  The suppress bitmask is staged in LDS for the same reason.
+constexpr int VJ = 52;
+__device__ __forceinline__ void stage_suppress(uint32_t* s_sup, const uint32_t* __restrict__ sup, int V) {
+    for (int w = threadIdx.x; w < (V + 31) / 32; w += TW) s_sup[w] = sup[w];
+}
+
 template <typename T>
 __global__ __launch_bounds__(TW) void finalize_ts_kernel(TsArgs a) {
     __shared__ MaxI s_m[2][TW / 64];
@@ -59,6 +69,9 @@ __global__ __launch_bounds__(TW) void finalize_ts_kernel(TsArgs a) {
     const float* lg = a.logits + (size_t)b * a.ldl;
     int* S = a.state + 4 * b;  // has_ts, seek_delta, result_len, status (0 run, 1 done, 2 failed)
     const bool live = step < a.out_cap && !a.done[b];
+    __shared__ uint32_t s_sup[VJ * TW / 32];
+    if (live) stage_suppress(s_sup, a.suppress, V);
+    __syncthreads();
     if (live) {
         const int oi0 = b * a.out_cap;
         const int last = step > 0 ? a.out_tok[oi0 + step - 1] : -1;
@@ -67,7 +80,7 @@ __global__ __launch_bounds__(TW) void finalize_ts_kernel(TsArgs a) {
         const bool pen_ts = step < 2 || pen >= beg;
         const int has_ts = S[0], seek_delta = S[1];
         auto masked = [&](int n) -> bool {
-            if ((a.suppress[n >> 5] >> (n & 31)) & 1u) return true;
+            if ((s_sup[n >> 5] >> (n & 31)) & 1u) return true;
             if (step == 0 && P.suppress_blank && (n == eot || n == a.blank)) return true;
             if (n >= beg) {
                 if (P.no_ts) return true;
@@ -79,12 +92,29 @@ __global__ __launch_bounds__(TW) void finalize_ts_kernel(TsArgs a) {
             }
             return false;
         };
-        auto val = [&](int n) { return P.temperature > 0.0f ? lg[n] / P.temperature : lg[n]; };
+        const float temp = P.temperature;
+        auto val = [&](int n) { return temp > 0.0f ? lg[n] / temp : lg[n]; };
+        // this thread's logits (strided) and their mask bits, all loads up front
+        float lv[VJ];
+#pragma unroll
+        for (int j = 0; j < VJ; ++j) {
+            const int n = tid + j * TW;
+            lv[j] = lg[min(n, V - 1)];
+        }
+        uint64_t keep = 0;
+#pragma unroll
+        for (int j = 0; j < VJ; ++j) {
+            const int n = tid + j * TW;
+            if (n < V && !masked(n)) keep |= 1ull << j;
+            if (temp > 0.0f) lv[j] = lv[j] / temp;
+        }
         // pass 1: maxima (first index on ties) of the text [0, beg) and timestamp [beg, V) ranges
         MaxI mt{-INFINITY, 0x7fffffff}, ms{-INFINITY, 0x7fffffff};
-        for (int n = tid; n < V; n += TW) {
-            if (masked(n)) continue;
-            const MaxI c{val(n), n};
+#pragma unroll
+        for (int j = 0; j < VJ; ++j) {
+            if (!((keep >> j) & 1)) continue;
+            const int n = tid + j * TW;
+            const MaxI c{lv[j], n};
             if (n < beg) mt = max_merge(mt, c);
             else ms = max_merge(ms, c);
         }
@@ -101,13 +131,15 @@ __global__ __launch_bounds__(TW) void finalize_ts_kernel(TsArgs a) {
         const float M = fmaxf(mt.v, ms.v);
         // pass 2: sum exp over everything unmasked (log-softmax) and over the timestamps
         float sa = 0.0f, st = 0.0f;
-        if (M > -INFINITY)
-            for (int n = tid; n < V; n += TW) {
-                if (masked(n)) continue;
-                const float v = val(n);
+        if (M > -INFINITY) {
+#pragma unroll
+            for (int j = 0; j < VJ; ++j) {
+                if (!((keep >> j) & 1)) continue;
+                const float v = lv[j];
                 sa += expf(v - M);
-                if (n >= beg) st += expf(v - ms.v);
+                if (tid + j * TW >= beg) st += expf(v - ms.v);
             }
+        }
         sa = wave_sum(sa);
         st = wave_sum(st);
         if (lane == 0) { s_s[0][wv] = sa; s_s[1][wv] = st; }
@@ -136,9 +168,15 @@ __global__ __launch_bounds__(TW) void finalize_ts_kernel(TsArgs a) {
             const bool rule = s_bc[3] != 0.0f;
             const float M2 = s_bc[2];
             const int C = (V + TW - 1) / TW, n0 = tid * C, n1 = min(V, n0 + C);
+            float cv[VJ];  // this thread's contiguous chunk (C <= VJ), loaded up front
+#pragma unroll
+            for (int i = 0; i < VJ; ++i) cv[i] = i < C ? val(min(n0 + i, V - 1)) : 0.0f;
             float z = 0.0f;
-            for (int n = n0; n < n1; ++n)
-                if (!masked(n) && !(rule && n < beg)) z += expf(val(n) - M2);
+#pragma unroll
+            for (int i = 0; i < VJ; ++i) {
+                const int n = n0 + i;
+                if (i < C && n < n1 && !masked(n) && !(rule && n < beg)) z += expf(cv[i] - M2);
+            }
             s_scan[tid] = z;
             __syncthreads();
             for (int o = 1; o < TW; o <<= 1) {  // inclusive Hillis-Steele scan
@@ -153,10 +191,13 @@ __global__ __launch_bounds__(TW) void finalize_ts_kernel(TsArgs a) {
             if (total > 0.0f && u >= lo && (u < hi || tid == TW - 1)) {
                 float c = lo;
                 int last_ok = -1;
-                for (int n = n0; n < n1; ++n) {
+#pragma unroll
+                for (int i = 0; i < VJ; ++i) {
+                    const int n = n0 + i;
+                    if (i >= C || n >= n1) break;
                     if (masked(n) || (rule && n < beg)) continue;
                     last_ok = n;
-                    c += expf(val(n) - M2);
+                    c += expf(cv[i] - M2);
                     if (u < c) break;
                 }
                 if (last_ok >= 0) s_pick = last_ok;
@@ -243,7 +284,6 @@ __global__ __launch_bounds__(TW) void beam_topk_kernel(BeamArgs a) {
     __shared__ MaxI s_m[2][TW / 64];
     __shared__ float s_s[TW / 64];
     __shared__ MaxI s_k[TW / 64];
-    __shared__ int s_ids[8];
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int step = a.step[0];
     const TsParams& P = *a.prm;
@@ -252,8 +292,11 @@ __global__ __launch_bounds__(TW) void beam_topk_kernel(BeamArgs a) {
     const int last = a.row[4 * b + 0], pen = a.row[4 * b + 1], has_ts = a.row[4 * b + 2], seek_delta = a.row[4 * b + 3];
     const bool last_ts = step > 0 && last >= beg;
     const bool pen_ts = step < 2 || pen >= beg;
+    __shared__ uint32_t s_sup[VJ * TW / 32];
+    stage_suppress(s_sup, a.suppress, V);
+    __syncthreads();
     auto masked = [&](int n) -> bool {
-        if ((a.suppress[n >> 5] >> (n & 31)) & 1u) return true;
+        if ((s_sup[n >> 5] >> (n & 31)) & 1u) return true;
         if (step == 0 && P.suppress_blank && (n == eot || n == a.blank)) return true;
         if (n >= beg) {
             if (P.no_ts) return true;
@@ -265,10 +308,26 @@ __global__ __launch_bounds__(TW) void beam_topk_kernel(BeamArgs a) {
         }
         return false;
     };
+    // the row's logits stay in registers (VJ per thread): the maxima, the exp sums and the k
+    // candidate rounds all read them there (the r3 kernel re-read the row from memory in each of
+    // its k + 2 sweeps, one round trip per element: 214 us per step at beam 5,
+    // profiles/r4/exp_beam_step.txt).  Same candidates, same order, same bits.
+    float lv[VJ];  // this thread's logits (strided), all loads up front
+#pragma unroll
+    for (int j = 0; j < VJ; ++j) lv[j] = lg[min(tid + j * TW, V - 1)];
+    uint64_t keep = 0;
+#pragma unroll
+    for (int j = 0; j < VJ; ++j) {
+        const int n = tid + j * TW;
+        if (n < V && !masked(n)) keep |= 1ull << j;
+    }
     MaxI mt{-INFINITY, 0x7fffffff}, ms{-INFINITY, 0x7fffffff};
-    for (int n = tid; n < V; n += TW) {
-        if (masked(n)) continue;
-        const MaxI c{lg[n], n};
+#pragma unroll
+    for (int j = 0; j < VJ; ++j) {
+        if (!((keep >> j) & 1)) continue;
+        const int n = tid + j * TW;
+        const float v = lv[j];
+        const MaxI c{v, n};
         if (n < beg) mt = max_merge(mt, c);
         else ms = max_merge(ms, c);
     }
@@ -284,15 +343,18 @@ __global__ __launch_bounds__(TW) void beam_topk_kernel(BeamArgs a) {
     for (int w = 1; w < TW / 64; ++w) { mt = max_merge(mt, s_m[0][w]); ms = max_merge(ms, s_m[1][w]); }
     const float M = fmaxf(mt.v, ms.v);
     float sa = 0.0f, st = 0.0f;
-    if (M > -INFINITY)
-        for (int n = tid; n < V; n += TW) {
-            if (masked(n)) continue;
-            sa += expf(lg[n] - M);
-            if (n >= beg) st += expf(lg[n] - ms.v);
+    if (M > -INFINITY) {
+#pragma unroll
+        for (int j = 0; j < VJ; ++j) {
+            if (!((keep >> j) & 1)) continue;
+            sa += expf(lv[j] - M);
+            if (tid + j * TW >= beg) st += expf(lv[j] - ms.v);
         }
+    }
     sa = wave_sum(sa);
     st = wave_sum(st);
     __shared__ float s_t[TW / 64];
+    __shared__ MaxI s_win;
     if (lane == 0) { s_s[wv] = sa; s_t[wv] = st; }
     __syncthreads();
     float za = 0.0f, zt = 0.0f;
@@ -300,16 +362,19 @@ __global__ __launch_bounds__(TW) void beam_topk_kernel(BeamArgs a) {
     const float lse = logf(za) + M;
     const float ts_lp = zt > 0.0f ? logf(zt) + ms.v - lse : -INFINITY;
     const bool rule = ms.v > -INFINITY && ts_lp > mt.v - lse;
-    // k rounds of a block argmax over the candidates not taken yet
+    // k rounds of a block argmax over the candidates not taken yet (the rule: timestamps only);
+    // the winner's owner drops it from its mask
+    if (rule) {
+#pragma unroll
+        for (int j = 0; j < VJ; ++j)
+            if (tid + j * TW < beg) keep &= ~(1ull << j);
+    }
     const int k = a.k;
     for (int r = 0; r < k; ++r) {
         MaxI c{-INFINITY, 0x7fffffff};
-        for (int n = tid; n < V; n += TW) {
-            if (masked(n) || (rule && n < beg)) continue;
-            bool taken = false;
-            for (int q = 0; q < r; ++q) taken = taken || s_ids[q] == n;
-            if (!taken) c = max_merge(c, MaxI{lg[n], n});
-        }
+#pragma unroll
+        for (int j = 0; j < VJ; ++j)
+            if ((keep >> j) & 1) c = max_merge(c, MaxI{lv[j], tid + j * TW});
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) c = max_merge(c, MaxI{__shfl_xor(c.v, o, 64), __shfl_xor(c.i, o, 64)});
         if (lane == 0) s_k[wv] = c;
@@ -318,11 +383,13 @@ __global__ __launch_bounds__(TW) void beam_topk_kernel(BeamArgs a) {
             MaxI m = s_k[0];
             for (int w = 1; w < TW / 64; ++w) m = max_merge(m, s_k[w]);
             const bool ok = m.v > -INFINITY && m.i < V;
-            s_ids[r] = ok ? m.i : -1;
+            s_win = m;
             a.cand_id[b * 8 + r] = ok ? m.i : -1;
-            a.cand_lp[b * 8 + r] = ok ? lg[m.i] - lse : -INFINITY;
+            a.cand_lp[b * 8 + r] = ok ? m.v - lse : -INFINITY;  // m.v is lg[m.i]
         }
         __syncthreads();
+        const MaxI w = s_win;
+        if (w.v > -INFINITY && w.i % TW == tid) keep &= ~(1ull << (w.i / TW));
     }
     if (tid == 0) a.tid[b] = ms.v > -INFINITY ? ms.i : 0;
 }
@@ -350,6 +417,7 @@ __global__ __launch_bounds__(256) void kv_gather_kernel(const T* __restrict__ sr
 
 void dec_beam_topk(const BeamArgs& a, int B, hipStream_t st) {
     if (a.k < 1 || a.k > 8) throw std::runtime_error("beam_topk: 1..8 candidates");
+    if (a.n_vocab < 1 || a.n_vocab > VJ * TW) throw std::runtime_error("beam_topk: vocabulary above 53248 tokens");
     hipLaunchKernelGGL(beam_topk_kernel, dim3(B), dim3(TW), 0, st, a);
     SPT_LAUNCH_CHECK();
 }
@@ -366,6 +434,7 @@ void dec_kv_gather(int dtype, const void* src, void* dst, const int* rows, int L
 }
 
 void dec_finalize_ts(int dtype, const TsArgs& a, int B, hipStream_t st) {
+    if (a.n_vocab < 1 || a.n_vocab > VJ * TW) throw std::runtime_error("finalize_ts: vocabulary above 53248 tokens");
     if (dtype == DT_BF16) hipLaunchKernelGGL(finalize_ts_kernel<bf16>, dim3(B), dim3(TW), 0, st, a);
     else hipLaunchKernelGGL(finalize_ts_kernel<float>, dim3(B), dim3(TW), 0, st, a);
     SPT_LAUNCH_CHECK();

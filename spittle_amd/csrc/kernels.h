@@ -176,8 +176,10 @@ void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int B_layou
 // the same attention with each of the 8 waves of a (row run, head) workgroup as a workgroup of its
 // own: writes partial w of [rows][H][8][66] = {o[64], m, l} (merged by an A_ATTN GEMV with 8
 // chunks); bitwise the 8-wave kernel's result once merged, for small grids (B / share * H small)
+// per_query (Tq = 1): one query row per workgroup (a beam's rows on one window: 8 x share
+// workgroups per head instead of 8, each re-reading the window's K/V, mostly from L2)
 void dec_cross_attn_vw(int dtype, const void* q, const void* kv, int B, int B_layout, int H, int T_enc, int Tq,
-                       float* part, hipStream_t st, const int* kvrow = nullptr, int share = 1);
+                       float* part, hipStream_t st, const int* kvrow = nullptr, int share = 1, bool per_query = false);
 
 struct FinalizeArgs {
     const void* part; int n_tiles;        // logits top-2 partials [B][n_tiles]
