@@ -853,7 +853,11 @@ float* Engine::enqueue_layers(DecGroup& g, int E, int Tq) {
     static const int vw_env = getenv("SPT_XATTN_VW") ? atoi(getenv("SPT_XATTN_VW")) : 1;
     const bool vw = vw_env == 2 || (vw_env != 0 && runs * H < 96);
     const bool per_query = vw && Tq == 1 && vw_env != 3;
-    const int xs = vw ? 8 : mapped ? 1 : xsplit_;
+    // the 8 partials merged by the cross output projection's prologue for one row (B = 1: cheaper
+    // than a launch), by a merge kernel for more (the prologue repeats the merge in each of its
+    // 80 workgroups: 15 us at a beam's 5 rows)
+    const bool vw_merge = vw && R > 1;
+    const int xs = vw ? (vw_merge ? 1 : 8) : mapped ? 1 : xsplit_;
     const int ks = dt_ == DT_BF16 ? 128 : 64;
     hipStream_t st = g.st;
     float* xc = g.dx;   // current residual rows (dec_embed / dec_finalize wrote this pass's input here)
@@ -904,8 +908,11 @@ float* Engine::enqueue_layers(DecGroup& g, int E, int Tq) {
         gemv(dt_, GV_BIAS, A_LN, a, st);
         consumed();
         if (vw)
+        {
             dec_cross_attn_vw(dt_, g.dq, ckv_l, B, E, H, T, Tq, g.xpart, st, mapped ? g.kvrow : nullptr,
                               mapped ? g.share : 1, per_query);
+            if (vw_merge) dec_attn_part_merge(dt_, g.xpart, R, H, g.dao, st);
+        }
         else
             dec_cross_attn(dt_, g.dq, ckv_l, B, E, H, T, Tq, g.dao, st, xs, g.xpart, mapped ? g.kvrow : nullptr,
                            mapped ? g.share : 1);

@@ -922,6 +922,37 @@ __global__ __launch_bounds__(64) void cross_attn_vw_kernel(const T* __restrict__
     }
 }
 
+// The 8 partials {o[64], m, l} of each (query row, head) written by cross_attn_vw_kernel, merged
+// once into the bf16 / f32 attention output: attn_merge's operations in the same order, so the
+// result is bitwise the 8-wave kernel's.  Used when the cross output projection has several rows:
+// its A_ATTN prologue would merge every row and head in each of its 80 workgroups (15 us at a
+// beam's 5 rows, profiles/r4/exp_beam_step.txt).
+template <typename T>
+__global__ __launch_bounds__(64) void attn_part_merge_kernel(const float* __restrict__ part, int H, T* __restrict__ out) {
+#pragma clang fp contract(off)
+    const int rh = blockIdx.x, e = threadIdx.x;
+    const float* pp = part + (size_t)rh * AW * 66;
+    float mw[AW], lw[AW], ow[AW];
+#pragma unroll
+    for (int w = 0; w < AW; ++w) {
+        mw[w] = pp[w * 66 + 64];
+        lw[w] = pp[w * 66 + 65];
+        ow[w] = pp[w * 66 + e];
+    }
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < AW; ++w) M = fmaxf(M, mw[w]);
+    float L = 0.f, O = 0.f;
+#pragma unroll
+    for (int w = 0; w < AW; ++w) {
+        if (mw[w] == -INFINITY) continue;
+        const float f = exp2f(mw[w] - M);
+        L = __builtin_fmaf(lw[w], f, L);
+        O = __builtin_fmaf(ow[w], f, O);
+    }
+    out[(size_t)rh * 64 + e] = from_f<T>(O / L);  // row r, head h: out[r][h * 64 + e], rh = r * H + h
+}
+
 // ------------------------------------------------------------------ finalize
 // Per sequence: reduce the logits tiles' top-2, record the token, choose the next
 // input (argmax or forced), embed it for the next pass; the last block advances
@@ -1131,6 +1162,13 @@ void dec_cross_attn_vw(int dtype, const void* q, const void* kv, int B, int B_la
 #undef SPT_XV_T
 #undef SPT_XV_PF
 #undef SPT_XV
+    SPT_LAUNCH_CHECK();
+}
+
+void dec_attn_part_merge(int dtype, const float* part, int R, int H, void* out, hipStream_t st) {
+    if (R < 1 || H < 1) throw std::runtime_error("dec_attn_part_merge: empty");
+    if (dtype == DT_BF16) hipLaunchKernelGGL(attn_part_merge_kernel<bf16>, dim3(R * H), dim3(64), 0, st, part, H, (bf16*)out);
+    else hipLaunchKernelGGL(attn_part_merge_kernel<float>, dim3(R * H), dim3(64), 0, st, part, H, (float*)out);
     SPT_LAUNCH_CHECK();
 }
 

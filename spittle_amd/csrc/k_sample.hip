@@ -51,6 +51,32 @@ __device__ __forceinline__ MaxI max_merge(MaxI a, MaxI b) {
 // memory round trip per iteration (the beam candidate kernel took 214 us per step,
 // profiles/r4/exp_beam_step.txt).  The suppress bitmask is staged in LDS for the same reason.
 constexpr int VJ = 52;
+
+// whisper_process_logits' masks for one decoder row at one step, folded into per-row constants
+// read once (the P fields were re-loaded inside every unrolled test) and a branch-free test:
+//   suppressed token; blank / EOT at step 0; a timestamp when timestamps are off, after two
+//   timestamps in a row, beyond max_initial_ts at step 0, or before the last timestamp; a text
+//   token other than EOT right after a single timestamp
+struct MaskRule {
+    int eot, beg, blank, mi_lim, sd_lim;
+    bool blank0, ts_all, tx_all;
+    __device__ MaskRule(const TsParams& P, int step, int eot_, int beg_, int blank_, bool last_ts, bool pen_ts,
+                        int has_ts, int seek_delta)
+        : eot(eot_), beg(beg_), blank(blank_) {
+        blank0 = step == 0 && P.suppress_blank;
+        ts_all = P.no_ts || (last_ts && pen_ts);
+        tx_all = last_ts && !pen_ts;
+        mi_lim = (step == 0 && P.max_initial >= 0) ? beg + P.max_initial : 0x7fffffff;
+        sd_lim = has_ts ? beg + seek_delta / 2 : -0x7fffffff;
+    }
+    __device__ __forceinline__ bool masked(const uint32_t* s_sup, int n) const {
+        const bool sup = (s_sup[n >> 5] >> (n & 31)) & 1u;
+        const bool b0 = blank0 & ((n == eot) | (n == blank));
+        const bool ts = (n >= beg) & (ts_all | (n > mi_lim) | (n < sd_lim));
+        const bool tx = (n < eot) & tx_all;
+        return sup | b0 | ts | tx;
+    }
+};
 __device__ __forceinline__ void stage_suppress(uint32_t* s_sup, const uint32_t* __restrict__ sup, int V) {
     for (int w = threadIdx.x; w < (V + 31) / 32; w += TW) s_sup[w] = sup[w];
 }
@@ -79,19 +105,8 @@ __global__ __launch_bounds__(TW) void finalize_ts_kernel(TsArgs a) {
         const bool last_ts = step > 0 && last >= beg;
         const bool pen_ts = step < 2 || pen >= beg;
         const int has_ts = S[0], seek_delta = S[1];
-        auto masked = [&](int n) -> bool {
-            if ((s_sup[n >> 5] >> (n & 31)) & 1u) return true;
-            if (step == 0 && P.suppress_blank && (n == eot || n == a.blank)) return true;
-            if (n >= beg) {
-                if (P.no_ts) return true;
-                if (last_ts && pen_ts) return true;
-                if (step == 0 && P.max_initial >= 0 && n > beg + P.max_initial) return true;
-                if (has_ts && n < beg + seek_delta / 2) return true;
-            } else if (n < eot && last_ts && !pen_ts) {
-                return true;
-            }
-            return false;
-        };
+        const MaskRule mr(P, step, eot, beg, a.blank, last_ts, pen_ts, has_ts, seek_delta);
+        auto masked = [&](int n) -> bool { return mr.masked(s_sup, n); };
         const float temp = P.temperature;
         auto val = [&](int n) { return temp > 0.0f ? lg[n] / temp : lg[n]; };
         // this thread's logits (strided) and their mask bits, all loads up front
@@ -109,14 +124,15 @@ __global__ __launch_bounds__(TW) void finalize_ts_kernel(TsArgs a) {
             if (temp > 0.0f) lv[j] = lv[j] / temp;
         }
         // pass 1: maxima (first index on ties) of the text [0, beg) and timestamp [beg, V) ranges
-        MaxI mt{-INFINITY, 0x7fffffff}, ms{-INFINITY, 0x7fffffff};
+        const MaxI none{-INFINITY, 0x7fffffff};  // branch-free as in beam_topk_kernel (same bits)
+        MaxI mt = none, ms = none;
 #pragma unroll
         for (int j = 0; j < VJ; ++j) {
-            if (!((keep >> j) & 1)) continue;
             const int n = tid + j * TW;
-            const MaxI c{lv[j], n};
-            if (n < beg) mt = max_merge(mt, c);
-            else ms = max_merge(ms, c);
+            const MaxI c = ((keep >> j) & 1) ? MaxI{lv[j], n} : none;
+            const bool t = n < beg;
+            mt = max_merge(mt, t ? c : none);
+            ms = max_merge(ms, t ? none : c);
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
@@ -134,10 +150,10 @@ __global__ __launch_bounds__(TW) void finalize_ts_kernel(TsArgs a) {
         if (M > -INFINITY) {
 #pragma unroll
             for (int j = 0; j < VJ; ++j) {
-                if (!((keep >> j) & 1)) continue;
-                const float v = lv[j];
-                sa += expf(v - M);
-                if (tid + j * TW >= beg) st += expf(v - ms.v);
+                const bool k_ = (keep >> j) & 1;
+                const float ea = expf(lv[j] - M), et = expf(lv[j] - ms.v);
+                sa += k_ ? ea : 0.0f;
+                st += (k_ && tid + j * TW >= beg) ? et : 0.0f;
             }
         }
         sa = wave_sum(sa);
@@ -295,19 +311,8 @@ __global__ __launch_bounds__(TW) void beam_topk_kernel(BeamArgs a) {
     __shared__ uint32_t s_sup[VJ * TW / 32];
     stage_suppress(s_sup, a.suppress, V);
     __syncthreads();
-    auto masked = [&](int n) -> bool {
-        if ((s_sup[n >> 5] >> (n & 31)) & 1u) return true;
-        if (step == 0 && P.suppress_blank && (n == eot || n == a.blank)) return true;
-        if (n >= beg) {
-            if (P.no_ts) return true;
-            if (last_ts && pen_ts) return true;
-            if (step == 0 && P.max_initial >= 0 && n > beg + P.max_initial) return true;
-            if (has_ts && n < beg + seek_delta / 2) return true;
-        } else if (n < eot && last_ts && !pen_ts) {
-            return true;
-        }
-        return false;
-    };
+    const MaskRule mr(P, step, eot, beg, a.blank, last_ts, pen_ts, has_ts, seek_delta);
+    auto masked = [&](int n) -> bool { return mr.masked(s_sup, n); };
     // the row's logits stay in registers (VJ per thread): the maxima, the exp sums and the k
     // candidate rounds all read them there (the r3 kernel re-read the row from memory in each of
     // its k + 2 sweeps, one round trip per element: 214 us per step at beam 5,
@@ -321,15 +326,18 @@ __global__ __launch_bounds__(TW) void beam_topk_kernel(BeamArgs a) {
         const int n = tid + j * TW;
         if (n < V && !masked(n)) keep |= 1ull << j;
     }
-    MaxI mt{-INFINITY, 0x7fffffff}, ms{-INFINITY, 0x7fffffff};
+    // branch-free over the unrolled entries (a skipped entry offers {-inf, INT_MAX}, which never
+    // wins a merge; a skipped exp adds +0.0f to a positive sum): the same maxima and sums, bit for
+    // bit, without an exec-mask branch per entry
+    const MaxI none{-INFINITY, 0x7fffffff};
+    MaxI mt = none, ms = none;
 #pragma unroll
     for (int j = 0; j < VJ; ++j) {
-        if (!((keep >> j) & 1)) continue;
         const int n = tid + j * TW;
-        const float v = lv[j];
-        const MaxI c{v, n};
-        if (n < beg) mt = max_merge(mt, c);
-        else ms = max_merge(ms, c);
+        const MaxI c = ((keep >> j) & 1) ? MaxI{lv[j], n} : none;
+        const bool t = n < beg;
+        mt = max_merge(mt, t ? c : none);
+        ms = max_merge(ms, t ? none : c);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -346,9 +354,10 @@ __global__ __launch_bounds__(TW) void beam_topk_kernel(BeamArgs a) {
     if (M > -INFINITY) {
 #pragma unroll
         for (int j = 0; j < VJ; ++j) {
-            if (!((keep >> j) & 1)) continue;
-            sa += expf(lv[j] - M);
-            if (tid + j * TW >= beg) st += expf(lv[j] - ms.v);
+            const bool k_ = (keep >> j) & 1;
+            const float ea = expf(lv[j] - M), et = expf(lv[j] - ms.v);
+            sa += k_ ? ea : 0.0f;
+            st += (k_ && tid + j * TW >= beg) ? et : 0.0f;
         }
     }
     sa = wave_sum(sa);
@@ -371,10 +380,9 @@ __global__ __launch_bounds__(TW) void beam_topk_kernel(BeamArgs a) {
     }
     const int k = a.k;
     for (int r = 0; r < k; ++r) {
-        MaxI c{-INFINITY, 0x7fffffff};
+        MaxI c = none;
 #pragma unroll
-        for (int j = 0; j < VJ; ++j)
-            if ((keep >> j) & 1) c = max_merge(c, MaxI{lv[j], tid + j * TW});
+        for (int j = 0; j < VJ; ++j) c = max_merge(c, ((keep >> j) & 1) ? MaxI{lv[j], tid + j * TW} : none);
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) c = max_merge(c, MaxI{__shfl_xor(c.v, o, 64), __shfl_xor(c.i, o, 64)});
         if (lane == 0) s_k[wv] = c;

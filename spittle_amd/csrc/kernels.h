@@ -180,6 +180,9 @@ void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int B_layou
 // workgroups per head instead of 8, each re-reading the window's K/V, mostly from L2)
 void dec_cross_attn_vw(int dtype, const void* q, const void* kv, int B, int B_layout, int H, int T_enc, int Tq,
                        float* part, hipStream_t st, const int* kvrow = nullptr, int share = 1, bool per_query = false);
+// the 8 partials of each of R query rows x H heads merged into out [R][H * 64] (bitwise the 8-wave
+// kernel's output), for a plain (A_DIRECT) cross output projection
+void dec_attn_part_merge(int dtype, const float* part, int R, int H, void* out, hipStream_t st);
 
 struct FinalizeArgs {
     const void* part; int n_tiles;        // logits top-2 partials [B][n_tiles]
