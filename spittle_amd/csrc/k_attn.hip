@@ -255,14 +255,18 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_q64_kernel(const bf16* __res
 #pragma unroll
         for (int i = 0; i < 16; ++i) { o[qb][0][i] = 0.f; o[qb][1][i] = 0.f; }
 
+    f32x16 cinit[2];  // the QK^T chains' start: 0, or (SUM == 4, after the first tile) -m_run
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { cinit[0][i] = 0.f; cinit[1][i] = 0.f; }
     // double-buffered K/V: the DMA of tile kt + 1 is issued before tile kt's products (a third
     // buffer with two tiles in flight measured slower: 149 vs 144 us on large-v3)
     const int nkt = cdiv(T, 64);
     stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    for (int kt = 0; kt < nkt; ++kt) {
-        const int cur = kt & 1;
+    // one K/V tile; called with a literal buffer index (the loop below is unrolled by two), so every
+    // LDS address is a constant offset from one base: no per-tile address VALU beside the MFMAs (r4)
+    auto tile = [&](const int kt, const int cur) __attribute__((always_inline)) {
         if (kt + 1 < nkt) stage(cur ^ 1, kt + 1);
         const SPT_LDS char* lk = lds_k(cur);
         const SPT_LDS char* lv = lds_v(cur);
@@ -270,17 +274,16 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_q64_kernel(const bf16* __res
 #pragma unroll
         for (int kt2 = 0; kt2 < 2; ++kt2) {
             // SUM == 4: the accumulator starts at -m (the query's running maximum, log2 units, a
-            // lane constant), so the MFMA chain leaves s - m and p = exp2(s - m) needs no FMA
-            const float i0 = (SUM == 4 && kt > 0) ? -m_run[0] : 0.f, i1 = (SUM == 4 && kt > 0) ? -m_run[1] : 0.f;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) { s[0][kt2][i] = i0; s[1][kt2][i] = i1; }
+            // lane constant), so the MFMA chain leaves s - m and p = exp2(s - m) needs no FMA.  The
+            // chain's first MFMA reads that start from cinit (set only when m moves) as its C
+            // operand: no 64 register moves per tile (r4)
             const int row = 32 * kt2 + l32;
 #pragma unroll
             for (int st = 0; st < 4; ++st) {
                 const int c = 2 * st + hf;
                 const bf16x8 a = *(const SPT_LDS bf16x8*)(lk + row * 128 + ((c ^ kswz<SW>(row)) << 4));
-                s[0][kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[0][st], s[0][kt2], 0, 0, 0);
-                s[1][kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[1][st], s[1][kt2], 0, 0, 0);
+                s[0][kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[0][st], st == 0 ? cinit[0] : s[0][kt2], 0, 0, 0);
+                s[1][kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[1][st], st == 0 ? cinit[1] : s[1][kt2], 0, 0, 0);
             }
         }
         if (kt * 64 + 64 > T) {
@@ -346,6 +349,8 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_q64_kernel(const bf16* __res
                         alpha = __builtin_amdgcn_exp2f(-delta);
                         m_run[qb] += delta;
                     }
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) cinit[qb][i] = -m_run[qb];
 #pragma unroll
                     for (int i = 0; i < 16; ++i) { o[qb][0][i] *= alpha; o[qb][1][i] *= alpha; }
                     lsum[qb] *= alpha;
@@ -471,9 +476,9 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_q64_kernel(const bf16* __res
                         (SPT_LDS bf16x4v*)(lv + key0 * 128 + ((((cb >> 4) ^ vswz<SW>(key0)) << 4) | (cb & 15))));
                     const bf16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                         (SPT_LDS bf16x4v*)(lv + (key0 + 8) * 128 + ((((cb >> 4) ^ vswz<SW>(key0 + 8)) << 4) | (cb & 15))));
-                    bf16x8 va;
-                    va[0] = lo[0]; va[1] = lo[1]; va[2] = lo[2]; va[3] = lo[3];
-                    va[4] = hi[0]; va[5] = hi[1]; va[6] = hi[2]; va[7] = hi[3];
+                    // a concatenation, not eight element inserts (which cost ~120 shift / or /
+                    // and VALU per tile beside 32 MFMAs, r4)
+                    const bf16x8 va = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
                     o[0][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pf[0][kt2][sp], o[0][dt], 0, 0, 0);
                     o[1][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pf[1][kt2][sp], o[1][dt], 0, 0, 0);
                 }
@@ -489,6 +494,10 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_q64_kernel(const bf16* __res
             }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+    for (int kt = 0; kt < nkt; kt += 2) {
+        tile(kt, 0);
+        if (kt + 1 < nkt) tile(kt + 1, 1);
     }
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
