@@ -118,9 +118,9 @@ __global__ __launch_bounds__(TW) void finalize_ts_kernel(TsArgs a) {
         }
         uint64_t keep = 0;
 #pragma unroll
-        for (int j = 0; j < VJ; ++j) {
+        for (int j = 0; j < VJ; ++j) {  // branch-free (as beam_topk_kernel)
             const int n = tid + j * TW;
-            if (n < V && !masked(n)) keep |= 1ull << j;
+            keep |= (uint64_t)((n < V) & !masked(min(n, V - 1))) << j;
             if (temp > 0.0f) lv[j] = lv[j] / temp;
         }
         // pass 1: maxima (first index on ties) of the text [0, beg) and timestamp [beg, V) ranges
@@ -322,9 +322,9 @@ __global__ __launch_bounds__(TW) void beam_topk_kernel(BeamArgs a) {
     for (int j = 0; j < VJ; ++j) lv[j] = lg[min(tid + j * TW, V - 1)];
     uint64_t keep = 0;
 #pragma unroll
-    for (int j = 0; j < VJ; ++j) {
+    for (int j = 0; j < VJ; ++j) {  // branch-free: the LDS mask reads can all be in flight
         const int n = tid + j * TW;
-        if (n < V && !masked(n)) keep |= 1ull << j;
+        keep |= (uint64_t)((n < V) & !masked(min(n, V - 1))) << j;
     }
     // branch-free over the unrolled entries (a skipped entry offers {-inf, INT_MAX}, which never
     // wins a merge; a skipped exp adds +0.0f to a positive sum): the same maxima and sums, bit for
@@ -378,6 +378,11 @@ __global__ __launch_bounds__(TW) void beam_topk_kernel(BeamArgs a) {
         for (int j = 0; j < VJ; ++j)
             if (tid + j * TW < beg) keep &= ~(1ull << j);
     }
+    // the winners stay in LDS until the rounds are over: a global store by thread 0 before a
+    // __syncthreads() would hold every round's barrier until the store had completed (the
+    // barrier's release waits on vmcnt)
+    __shared__ int s_cid[8];
+    __shared__ float s_clp[8];
     const int k = a.k;
     for (int r = 0; r < k; ++r) {
         MaxI c = none;
@@ -392,12 +397,16 @@ __global__ __launch_bounds__(TW) void beam_topk_kernel(BeamArgs a) {
             for (int w = 1; w < TW / 64; ++w) m = max_merge(m, s_k[w]);
             const bool ok = m.v > -INFINITY && m.i < V;
             s_win = m;
-            a.cand_id[b * 8 + r] = ok ? m.i : -1;
-            a.cand_lp[b * 8 + r] = ok ? m.v - lse : -INFINITY;  // m.v is lg[m.i]
+            s_cid[r] = ok ? m.i : -1;
+            s_clp[r] = ok ? m.v - lse : -INFINITY;  // m.v is lg[m.i]
         }
         __syncthreads();
         const MaxI w = s_win;
         if (w.v > -INFINITY && w.i % TW == tid) keep &= ~(1ull << (w.i / TW));
+    }
+    if (tid < k) {
+        a.cand_id[b * 8 + tid] = s_cid[tid];
+        a.cand_lp[b * 8 + tid] = s_clp[tid];
     }
     if (tid == 0) a.tid[b] = ms.v > -INFINITY ? ms.i : 0;
 }

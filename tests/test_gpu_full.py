@@ -234,6 +234,32 @@ def test_one_encoder_run_per_window_with_fallback(tiny):
     assert cs["engine_calls"] >= 6 * r.n_windows, cs
 
 
+@pytest.mark.parametrize("vw", ["0", "3"])
+@pytest.mark.parametrize("kind", ["beam5", "fallback_best_of5"])
+def test_cross_attention_strategies_bitwise(tiny, kind, vw, monkeypatch):
+    """The decoders of one utterance on one shared window run, by default, one query per
+    single-wave workgroup with the 8 partials merged by attn_part_merge_kernel (r4).  The 8-wave
+    kernel with five queries per workgroup (SPT_XATTN_VW=0) and the single-wave kernel with five
+    queries per workgroup (SPT_XATTN_VW=3) must give bitwise the same result: every strategy runs
+    the same per-lane keys, block order and pinned arithmetic (contraction off, explicit fmaf)."""
+    from spittle_amd import WhisperEngine, WhisperModelParams
+    e, _ = tiny
+    xs = [O.synth_audio(87, 12 * 16000), O.synth_audio(88, 35 * 16000)]
+    kw = dict(beam_size=5, max_new_tokens=10) if kind == "beam5" else \
+        dict(temperature_inc=0.2, logprob_thold=10.0, best_of=5, max_new_tokens=10, seed=13)
+    ref = e.transcribe_batch(xs, _params(**kw))
+    monkeypatch.setenv("SPT_XATTN_VW", vw)
+    e2 = WhisperEngine(WhisperModelParams(dtype="f32", max_batch=8, seed=SEED))  # captures under vw
+    try:
+        e2.load_model("synthetic:tiny.en")
+        got = e2.transcribe_batch(xs, _params(**kw))
+    finally:
+        e2.unload_model()
+    for a, b in zip(ref, got):
+        assert a.tokens == b.tokens and a.text == b.text
+        assert np.array_equal(np.asarray(a.top1), np.asarray(b.top1))
+
+
 @pytest.mark.parametrize("kind", ["beam5", "fallback_best_of5"])
 def test_shared_window_bitwise_equal_to_copies(tiny, kind, monkeypatch):
     """The decoders of one utterance (beam 5, best_of 5) read one shared encoded window; the

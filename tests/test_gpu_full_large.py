@@ -152,3 +152,23 @@ def test_large_v3_beam5_shared_window_bitwise(large, monkeypatch):
     b = e.transcribe_samples(x, _params(beam_size=5, max_new_tokens=16))
     monkeypatch.delenv("SPT_NO_WINDOW_SHARE")
     assert a.tokens == b.tokens and np.array_equal(np.asarray(a.top1), np.asarray(b.top1))
+
+
+@pytest.mark.parametrize("vw", ["0", "3"])
+def test_large_v3_beam5_cross_attention_strategies_bitwise(large, vw, monkeypatch):
+    """Beam 5 at large-v3 width in bf16: the default one-query single-wave workgroups with the
+    partial merge, the 8-wave kernel with five queries per workgroup (SPT_XATTN_VW=0) and the
+    single-wave five-query kernel (3) give bitwise the same result (a new engine captures its
+    passes under the switch)."""
+    from spittle_amd import WhisperEngine, WhisperModelParams
+    e, _ = large
+    x = _audio(20, 193)
+    a = e.transcribe_samples(x, _params(beam_size=5, max_new_tokens=12))
+    monkeypatch.setenv("SPT_XATTN_VW", vw)
+    e2 = WhisperEngine(WhisperModelParams(dtype="bf16", max_batch=8, seed=SEED))
+    try:
+        e2.load_model(SPEC)
+        b = e2.transcribe_samples(x, _params(beam_size=5, max_new_tokens=12))
+    finally:
+        e2.unload_model()
+    assert a.tokens == b.tokens and np.array_equal(np.asarray(a.top1), np.asarray(b.top1))
