@@ -849,8 +849,9 @@ float* Engine::enqueue_layers(DecGroup& g, int E, int Tq) {
     // re-read the window's 384 KB from L2) -- all bitwise the same result.  r4
     // (profiles/r4/exp_xattn_vw.txt, exp_beam_step.txt): B = 1 pass 1.609 -> 1.562 ms; the 5-query
     // workgroups of a beam took 29 us per layer; B = 8 (160 workgroups) stays on the 8-wave kernel.
-    // SPT_XATTN_VW=0: never, 2: always, 3: small grids without the per-query split (measurements)
-    static const int vw_env = getenv("SPT_XATTN_VW") ? atoi(getenv("SPT_XATTN_VW")) : 1;
+    // SPT_XATTN_VW=0: never, 2: always, 3: small grids without the per-query split (measurements and
+    // the cross-strategy bitwise tests; read when a pass is captured, so a new engine picks it up)
+    const int vw_env = getenv("SPT_XATTN_VW") ? atoi(getenv("SPT_XATTN_VW")) : 1;
     const bool vw = vw_env == 2 || (vw_env != 0 && runs * H < 96);
     const bool per_query = vw && Tq == 1 && vw_env != 3;
     // the 8 partials merged by the cross output projection's prologue for one row (B = 1: cheaper
@@ -1335,10 +1336,15 @@ void Engine::read_cands(int B, BeamCands* out) {
     out->id.resize((size_t)B * 8);
     out->lp.resize((size_t)B * 8);
     out->tid.resize(B);
-    HIP_CHECK(hipMemcpyAsync(out->id.data(), g.cand_id, (size_t)B * 32, hipMemcpyDeviceToHost, g.st));
-    HIP_CHECK(hipMemcpyAsync(out->lp.data(), g.cand_lp, (size_t)B * 32, hipMemcpyDeviceToHost, g.st));
-    HIP_CHECK(hipMemcpyAsync(out->tid.data(), g.beam_tid, (size_t)B * 4, hipMemcpyDeviceToHost, g.st));
+    // cand_id, cand_lp and beam_tid are consecutive carvings of one workspace: one copy back
+    const char* lo = (const char*)g.cand_id;
+    const size_t o_lp = (const char*)g.cand_lp - lo, o_tid = (const char*)g.beam_tid - lo;
+    beam_rd_.resize(o_tid + (size_t)B * 4);
+    HIP_CHECK(hipMemcpyAsync(beam_rd_.data(), lo, beam_rd_.size(), hipMemcpyDeviceToHost, g.st));
     HIP_CHECK(hipStreamSynchronize(g.st));
+    memcpy(out->id.data(), beam_rd_.data(), (size_t)B * 32);
+    memcpy(out->lp.data(), beam_rd_.data() + o_lp, (size_t)B * 32);
+    memcpy(out->tid.data(), beam_rd_.data() + o_tid, (size_t)B * 4);
 }
 
 void Engine::beam_begin(int B, const DecodeRequest& rq, BeamCands* out, int* lang_out) {
@@ -1372,16 +1378,19 @@ void Engine::beam_next(const int* src, const int* tokens, const int* rowstate, i
     for (int b = 0; b < B; ++b)
         if (src[b] < 0 || src[b] >= B || tokens[b] < 0 || tokens[b] >= dm_.n_vocab)
             throw std::runtime_error("beam_next: bad source row or token");
-    // host sources stay alive until the step's results are read back (synchronous below)
-    beam_host_.assign(src, src + B);
-    beam_host_.insert(beam_host_.end(), tokens, tokens + B);
-    beam_host_.insert(beam_host_.end(), rowstate, rowstate + (size_t)B * 4);
-    beam_host_.push_back(step);
-    const int* h = beam_host_.data();
-    HIP_CHECK(hipMemcpyAsync(g.beam_src, h, B * 4, hipMemcpyHostToDevice, g.st));
-    HIP_CHECK(hipMemcpyAsync(g.tok_in, h + B, B * 4, hipMemcpyHostToDevice, g.st));
-    HIP_CHECK(hipMemcpyAsync(g.beam_row, h + 2 * B, (size_t)B * 16, hipMemcpyHostToDevice, g.st));
-    HIP_CHECK(hipMemcpyAsync(g.beam_step, h + 6 * B, 4, hipMemcpyHostToDevice, g.st));
+    // host sources stay alive until the step's results are read back (synchronous below).  beam_row,
+    // beam_step and beam_src are consecutive carvings of one workspace: one upload for the three,
+    // laid out at their device offsets, and one for the tokens
+    char* lo = (char*)g.beam_row;
+    const size_t o_step = (char*)g.beam_step - lo, o_src = (char*)g.beam_src - lo;
+    beam_host_.assign((o_src + (size_t)B * 4 + 3) / 4, 0);
+    char* hb = (char*)beam_host_.data();
+    memcpy(hb, rowstate, (size_t)B * 16);
+    memcpy(hb + o_step, &step, 4);
+    memcpy(hb + o_src, src, (size_t)B * 4);
+    beam_tok_.assign(tokens, tokens + B);
+    HIP_CHECK(hipMemcpyAsync(lo, hb, o_src + (size_t)B * 4, hipMemcpyHostToDevice, g.st));
+    HIP_CHECK(hipMemcpyAsync(g.tok_in, beam_tok_.data(), (size_t)B * 4, hipMemcpyHostToDevice, g.st));
     // one captured graph per (rows, candidates, flags, length, cache side): gather the self-K/V
     // rows (positions < pos0) from the side holding them into the other side, which this step's
     // layers then append to and read (the two sides alternate: one gather per step, not a gather
@@ -1395,6 +1404,11 @@ void Engine::beam_next(const int* src, const int* tokens, const int* rowstate, i
     auto beam_pass = [&] {
         dec_kv_gather(dt_, kv_from, kv_to, g.beam_src, dm_.n_dec, B, dm_.n_head, dm_.n_text_ctx, g.ds, g.st);
         dec_embed(dt_, g.tok_in, B, 1, dm_.d, tok_emb_, dec_pos_, g.ds, g.dx, g.st);
+        struct SkvSide {  // the layers append to / read kv_to; the group's pointer is restored on unwind
+            DecGroup& g;
+            void* own;
+            ~SkvSide() { g.skv = own; }
+        } side_guard{g, own};
         g.skv = kv_to;
         float* x = enqueue_layers(g, enc_E_, 1);
         g.skv = own;

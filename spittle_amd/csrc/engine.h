@@ -270,7 +270,9 @@ private:
     int beam_B_ = 0;
     int beam_side_ = 0;          // the self-K/V side holding the search's rows: 0 the group's cache, 1 kvtmp_
     void* kvtmp_ = nullptr;      // self-K/V reorder scratch (allocated on first beam search)
-    std::vector<int> beam_host_;  // host sources of the per-step uploads
+    std::vector<int> beam_host_;  // host image of the per-step uploads (beam_row .. beam_src)
+    std::vector<int> beam_tok_;   // host source of the step's tokens
+    std::vector<char> beam_rd_;   // host image of cand_id .. beam_tid
     void read_cands(int B, BeamCands* out);
 
     // ---- utterances of load_utterances (grown on demand, outside the arenas)

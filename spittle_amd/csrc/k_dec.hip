@@ -1166,7 +1166,7 @@ void dec_cross_attn_vw(int dtype, const void* q, const void* kv, int B, int B_la
 }
 
 void dec_attn_part_merge(int dtype, const float* part, int R, int H, void* out, hipStream_t st) {
-    if (R < 1 || H < 1) throw std::runtime_error("dec_attn_part_merge: empty");
+    if (R < 1 || H < 1 || !part || !out) throw std::runtime_error("dec_attn_part_merge: empty or missing buffers");
     if (dtype == DT_BF16) hipLaunchKernelGGL(attn_part_merge_kernel<bf16>, dim3(R * H), dim3(64), 0, st, part, H, (bf16*)out);
     else hipLaunchKernelGGL(attn_part_merge_kernel<float>, dim3(R * H), dim3(64), 0, st, part, H, (float*)out);
     SPT_LAUNCH_CHECK();
