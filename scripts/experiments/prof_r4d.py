@@ -1,5 +1,6 @@
 """r4d: what a 10 s beam-5 call and a B = 1 greedy call spend per kernel (run under
-rocprofv3 --kernel-trace --stats; MODE=beam or MODE=b1 picks the call)."""
+rocprofv3 --kernel-trace --stats; MODE=beam or MODE=b1 picks the call, CALLS the timed calls
+after the warm one)."""
 import os
 import sys
 import time
@@ -21,7 +22,7 @@ else:
                                max_new_tokens=128)
     x = synth_audio(2030)
 e.transcribe_samples(x, p)
-for _ in range(2):
+for _ in range(int(os.environ.get("CALLS", "2"))):
     t0 = time.perf_counter()
     r = e.transcribe_samples(x, p)
     ms = (time.perf_counter() - t0) * 1e3

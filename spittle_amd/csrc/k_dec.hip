@@ -302,44 +302,32 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
         const int h0 = (ss0 * KS) >> 6, h1 = min(H, (ss1 * KS + 63) >> 6);
         const int nh = h1 - h0;
         const int total = a.R * nh * 64;
-        // four elements per thread per round, every partial load of the round issued before any
-        // merge (r4: one element per round waited a full L2 round trip each -- 16 us for the 5 x 20
-        // heads of a beam step, profiles/r4/exp_beam_step.txt)
-        constexpr int U = 4;
-        for (int base = tid; base < total; base += U * 64 * NWV) {
-            float mc[U][S], lc[U][S], oc[U][S];
+        // one element per thread per round: the engine takes this prologue for one row only (B = 1:
+        // 1280 elements over 512 threads); several rows merge once in attn_part_merge_kernel (r4:
+        // batching four elements per round here cost the one-row pass 1.5 %, 189 VGPRs)
+        for (int idx = tid; idx < total; idx += 64 * NWV) {
+            const int r = idx / (nh * 64), rem = idx - r * nh * 64;
+            const int h = h0 + (rem >> 6), e = rem & 63;
+            const float* pp = a.apart + ((size_t)r * H + h) * S * 66;
+            float mc[S], lc[S], oc[S];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int idx = min(base + u * 64 * NWV, total - 1);
-                const int r = idx / (nh * 64), rem = idx - r * nh * 64;
-                const int h = h0 + (rem >> 6), e = rem & 63;
-                const float* pp = a.apart + ((size_t)r * H + h) * S * 66;
-#pragma unroll
-                for (int c = 0; c < S; ++c) {
-                    mc[u][c] = pp[c * 66 + 64];
-                    lc[u][c] = pp[c * 66 + 65];
-                    oc[u][c] = pp[c * 66 + e];
-                }
+            for (int c = 0; c < S; ++c) {
+                mc[c] = pp[c * 66 + 64];
+                lc[c] = pp[c * 66 + 65];
+                oc[c] = pp[c * 66 + e];
             }
+            float M = mc[0];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int idx = base + u * 64 * NWV;
-                if (idx >= total) break;
-                const int r = idx / (nh * 64), rem = idx - r * nh * 64;
-                const int h = h0 + (rem >> 6), e = rem & 63;
-                float M = mc[u][0];
+            for (int c = 1; c < S; ++c) M = fmaxf(M, mc[c]);
+            float L = 0.f, O = 0.f;
 #pragma unroll
-                for (int c = 1; c < S; ++c) M = fmaxf(M, mc[u][c]);
-                float L = 0.f, O = 0.f;
-#pragma unroll
-                for (int c = 0; c < S; ++c) {  // attn_merge's operations (bitwise): skip empty chunks
-                    if (mc[u][c] == -INFINITY) continue;
-                    const float f = exp2f(mc[u][c] - M);
-                    L = __builtin_fmaf(lc[u][c], f, L);
-                    O = __builtin_fmaf(oc[u][c], f, O);
-                }
-                img[(size_t)r * lds_ld + h * 64 + e] = from_f<T>(O / L);
+            for (int c = 0; c < S; ++c) {  // attn_merge's operations (bitwise): skip empty chunks
+                if (mc[c] == -INFINITY) continue;
+                const float f = exp2f(mc[c] - M);
+                L = __builtin_fmaf(lc[c], f, L);
+                O = __builtin_fmaf(oc[c], f, O);
             }
+            img[(size_t)r * lds_ld + h * 64 + e] = from_f<T>(O / L);
         }
         __syncthreads();
     }
