@@ -17,6 +17,9 @@ e.load_model("synthetic:large-v3")
 if mode == "beam":
     p = WhisperInferenceParams(language="en", beam_size=5, temperature_inc=0.0)
     x = synth_audio(2010)[:16000 * 10]
+elif mode == "full5":  # the app's default whisper_full call on 5 s (timestamps, fallback, best_of 5)
+    p = WhisperInferenceParams(language="en")
+    x = synth_audio(2005)[:16000 * 5]
 else:
     p = WhisperInferenceParams(language="en", no_timestamps=True, temperature_inc=0.0, ignore_eot=True,
                                max_new_tokens=128)

@@ -583,6 +583,8 @@ void Engine::alloc_workspace() {
             g.seek = (int*)c.take(B * 4);
             g.seek_end = (int*)c.take(B * 4);
             g.ts_state = (int*)c.take(B * 16);
+            g.ts_stat = (float*)c.take((int64_t)B * TS_CHUNKS * 6 * 4);
+            g.beam_stat = (float*)c.take((int64_t)B * TS_CHUNKS * BEAM_STAT * 4);
             g.prm = (TsParams*)c.take(sizeof(TsParams));
             g.beam_row = (int*)c.take(B * 16);
             g.beam_step = (int*)c.take(64);
@@ -964,6 +966,8 @@ void Engine::enqueue_head(DecGroup& g, int Tq, const DecodeRequest& rq, int out_
         bm.n_vocab = dm_.n_vocab; bm.eot = sp.eot; bm.beg = sp.beg; bm.blank = rq.blank_tok;
         bm.suppress = sup; bm.prm = g.prm; bm.row = g.beam_row; bm.step = g.beam_step; bm.k = rq.beam_k;
         bm.cand_id = g.cand_id; bm.cand_lp = g.cand_lp; bm.tid = g.beam_tid;
+        static const bool one_wg = getenv("SPT_BEAM_ONE_WG") != nullptr;  // the single-workgroup kernel (A/B)
+        bm.stat = one_wg ? nullptr : g.beam_stat;
         dec_beam_topk(bm, B, st);
         dec_advance(g.ds, Tq, st);
         return;
@@ -977,7 +981,8 @@ void Engine::enqueue_head(DecGroup& g, int Tq, const DecodeRequest& rq, int out_
         t.next_tok = g.tok_in; t.out_tok = g.out_tok; t.out_plog = g.out_t1; t.out_tid = g.out_t2; t.out_cap = out_cap;
         t.done = g.done;
         t.emb = tok_emb_; t.pos = dec_pos_; t.d = d; t.ctx = ctx; t.Tq = Tq; t.x = g.dx;
-        t.ds = g.ds; t.arrive = g.arrive;
+        t.ds = g.ds; t.arrive = g.arrive; t.stat = g.ts_stat;
+        dec_ts_stats(t, B, st);
         dec_finalize_ts(dt_, t, B, st);
         return;
     }

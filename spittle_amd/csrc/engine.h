@@ -179,6 +179,8 @@ private:
         float* pend = nullptr;        // pending partial slabs [kMaxPend][R][d]
         float* xpart = nullptr;       // cross-attention chunk partials [R][H][<=4][66]
         int *seek = nullptr, *seek_end = nullptr, *ts_state = nullptr;  // whisper_full decoding
+        float* ts_stat = nullptr;     // [B][TS_CHUNKS][6] per-chunk vocabulary statistics (dec_ts_stats)
+        float* beam_stat = nullptr;   // [B][TS_CHUNKS][BEAM_STAT] per-chunk statistics and beam candidates
         TsParams* prm = nullptr;
         int *beam_row = nullptr, *beam_step = nullptr, *beam_src = nullptr;  // beam search
         int *cand_id = nullptr, *beam_tid = nullptr;

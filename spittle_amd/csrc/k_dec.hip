@@ -511,6 +511,7 @@ void gemv_attr_all() {
     gemv_attr<T, MODE, ASRC, 4, NWV, CT, MAXJ>();
     if constexpr (MODE == GV_LOGITS) {
         SPT_ATTR(4, 4, 4)
+        SPT_ATTR(8, 8, 4)
     } else if constexpr (ASRC == A_DIRECT || is_attn(ASRC)) {
         SPT_GV_CONFIGS(SPT_ATTR)
     } else {
@@ -537,7 +538,11 @@ template <typename T, int MODE, int ASRC, int RG>
 void gemv_launch_rg(const GemvArgs& a, hipStream_t st) {
     const int nss = cdiv(a.K / GV<T>::KS, a.ksplit);  // super-steps per workgroup
     if constexpr (MODE == GV_LOGITS) {
-        gemv_launch_cfg<T, MODE, ASRC, RG, 4, 4, 4>(a, st);
+        // one wave per 16-column tile over all of K either way (bitwise the same logits); wider
+        // workgroups stage each LayerNorm image for more tiles (SPT_GV_LOGITS_CT = 4 / 8, r4)
+        static const int lct = getenv("SPT_GV_LOGITS_CT") ? atoi(getenv("SPT_GV_LOGITS_CT")) : 4;
+        if (lct == 8) gemv_launch_cfg<T, MODE, ASRC, RG, 8, 8, 4>(a, st);
+        else gemv_launch_cfg<T, MODE, ASRC, RG, 4, 4, 4>(a, st);
     } else {
         // Wide LayerNorm-prologue GEMVs (fc1, N = 4d >= 4096): two column tiles per workgroup,
         // so half as many workgroups re-read the residual rows for their LayerNorm image (r1

@@ -69,26 +69,123 @@ struct MaskRule {
         mi_lim = (step == 0 && P.max_initial >= 0) ? beg + P.max_initial : 0x7fffffff;
         sd_lim = has_ts ? beg + seek_delta / 2 : -0x7fffffff;
     }
-    __device__ __forceinline__ bool masked(const uint32_t* s_sup, int n) const {
-        const bool sup = (s_sup[n >> 5] >> (n & 31)) & 1u;
+    __device__ __forceinline__ bool masked_rules(int n) const {  // everything but the suppress bits
         const bool b0 = blank0 & ((n == eot) | (n == blank));
         const bool ts = (n >= beg) & (ts_all | (n > mi_lim) | (n < sd_lim));
         const bool tx = (n < eot) & tx_all;
-        return sup | b0 | ts | tx;
+        return b0 | ts | tx;
+    }
+    __device__ __forceinline__ bool masked(const uint32_t* s_sup, int n) const {
+        const bool sup = (s_sup[n >> 5] >> (n & 31)) & 1u;
+        return sup | masked_rules(n);
     }
 };
 __device__ __forceinline__ void stage_suppress(uint32_t* s_sup, const uint32_t* __restrict__ sup, int V) {
     for (int w = threadIdx.x; w < (V + 31) / 32; w += TW) s_sup[w] = sup[w];
 }
 
+// whisper_process_logits' statistics of one row, spread over TS_CHUNKS workgroups per row: each
+// workgroup takes a contiguous 1/TS_CHUNKS of the vocabulary and writes the text and timestamp
+// maxima (first index on ties) of its unmasked tokens and its exp sums relative to its own maxima
+// (sa over everything, st over the timestamps).  finalize_ts_kernel merges them in chunk order.
+// r4: one 1024-thread workgroup per row swept all 51866 logits itself -- about 7 K VALU
+// instructions per wave, 4 waves per SIMD on the one CU a row had (~50 us per step; SQ counters
+// in profiles/r4/exp_beam_step.txt).
+constexpr int TS_T = 256;   // threads per chunk
+constexpr int TS_J = 13;    // logits per thread: V <= TS_CHUNKS * TS_T * TS_J = 53248
+__global__ __launch_bounds__(TS_T) void ts_stats_kernel(TsArgs a) {
+    __shared__ uint32_t s_sup[TS_T * TS_J / 32 + 2];
+    __shared__ MaxI s_m[2][TS_T / 64];
+    __shared__ float s_s[2][TS_T / 64];
+    const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int step = a.ds->step;
+    const TsParams& P = *a.prm;
+    const int V = a.n_vocab, beg = a.beg, eot = a.eot;
+    const int CS = (V + TS_CHUNKS - 1) / TS_CHUNKS, n0 = c * CS, n1 = min(V, n0 + CS);
+    float* out = a.stat + ((size_t)b * TS_CHUNKS + c) * 6;
+    const bool live = step < a.out_cap && !a.done[b];
+    const int w0 = n0 >> 5, nw = n1 > n0 ? ((n1 - 1) >> 5) - w0 + 1 : 0;
+    for (int w = tid; w < nw; w += TS_T) s_sup[w] = a.suppress[w0 + w];
+    __syncthreads();
+    if (!live) {
+        if (tid == 0) {
+            out[0] = -INFINITY; out[1] = __int_as_float(0x7fffffff);
+            out[2] = -INFINITY; out[3] = __int_as_float(0x7fffffff);
+            out[4] = 0.0f; out[5] = 0.0f;
+        }
+        return;
+    }
+    const float* lg = a.logits + (size_t)b * a.ldl;
+    const int oi0 = b * a.out_cap;
+    const int last = step > 0 ? a.out_tok[oi0 + step - 1] : -1;
+    const int pen = step > 1 ? a.out_tok[oi0 + step - 2] : -1;
+    const bool last_ts = step > 0 && last >= beg;
+    const bool pen_ts = step < 2 || pen >= beg;
+    const int* S = a.state + 4 * b;
+    const MaskRule mr(P, step, eot, beg, a.blank, last_ts, pen_ts, S[0], S[1]);
+    const float temp = P.temperature;
+    float lv[TS_J];
+#pragma unroll
+    for (int j = 0; j < TS_J; ++j) lv[j] = lg[min(n0 + tid + j * TS_T, V - 1)];
+    uint32_t keep = 0;
+#pragma unroll
+    for (int j = 0; j < TS_J; ++j) {
+        const int n = n0 + tid + j * TS_T;
+        const int nc = min(n, V - 1);
+        const bool sup = (s_sup[(nc >> 5) - w0] >> (nc & 31)) & 1u;  // the chunk's suppress words
+        const bool m = sup | mr.masked_rules(nc);
+        keep |= (uint32_t)((n < n1) & !m) << j;
+        if (temp > 0.0f) lv[j] = lv[j] / temp;
+    }
+    const MaxI none{-INFINITY, 0x7fffffff};
+    MaxI mt = none, ms = none;
+#pragma unroll
+    for (int j = 0; j < TS_J; ++j) {
+        const int n = n0 + tid + j * TS_T;
+        const MaxI x = ((keep >> j) & 1) ? MaxI{lv[j], n} : none;
+        const bool t = n < beg;
+        mt = max_merge(mt, t ? x : none);
+        ms = max_merge(ms, t ? none : x);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mt = max_merge(mt, MaxI{__shfl_xor(mt.v, o, 64), __shfl_xor(mt.i, o, 64)});
+        ms = max_merge(ms, MaxI{__shfl_xor(ms.v, o, 64), __shfl_xor(ms.i, o, 64)});
+    }
+    if (lane == 0) { s_m[0][wv] = mt; s_m[1][wv] = ms; }
+    __syncthreads();
+    mt = s_m[0][0];
+    ms = s_m[1][0];
+    for (int w = 1; w < TS_T / 64; ++w) { mt = max_merge(mt, s_m[0][w]); ms = max_merge(ms, s_m[1][w]); }
+    const float M = fmaxf(mt.v, ms.v);
+    float sa = 0.0f, st = 0.0f;
+#pragma unroll
+    for (int j = 0; j < TS_J; ++j) {
+        const bool k_ = (keep >> j) & 1;
+        const float ea = expf(lv[j] - M), et = expf(lv[j] - ms.v);
+        sa += k_ ? ea : 0.0f;
+        st += (k_ && n0 + tid + j * TS_T >= beg) ? et : 0.0f;
+    }
+    sa = wave_sum(sa);
+    st = wave_sum(st);
+    if (lane == 0) { s_s[0][wv] = sa; s_s[1][wv] = st; }
+    __syncthreads();
+    if (tid == 0) {
+        float za = 0.0f, zt = 0.0f;
+        for (int w = 0; w < TS_T / 64; ++w) { za += s_s[0][w]; zt += s_s[1][w]; }
+        out[0] = mt.v; out[1] = __int_as_float(mt.i);
+        out[2] = ms.v; out[3] = __int_as_float(ms.i);
+        out[4] = M > -INFINITY ? za : 0.0f;
+        out[5] = ms.v > -INFINITY ? zt : 0.0f;
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(TW) void finalize_ts_kernel(TsArgs a) {
-    __shared__ MaxI s_m[2][TW / 64];
-    __shared__ float s_s[2][TW / 64];
     __shared__ float s_scan[TW];
     __shared__ int s_pick, s_tok;
     __shared__ float s_bc[4];  // M_all, LSE_all, M_after, ts_rule
-    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int b = blockIdx.x, tid = threadIdx.x;
     const int step = a.ds->step;
     const TsParams& P = *a.prm;
     const int V = a.n_vocab, beg = a.beg, eot = a.eot;
@@ -96,7 +193,7 @@ __global__ __launch_bounds__(TW) void finalize_ts_kernel(TsArgs a) {
     int* S = a.state + 4 * b;  // has_ts, seek_delta, result_len, status (0 run, 1 done, 2 failed)
     const bool live = step < a.out_cap && !a.done[b];
     __shared__ uint32_t s_sup[VJ * TW / 32];
-    if (live) stage_suppress(s_sup, a.suppress, V);
+    if (live && P.temperature > 0.0f) stage_suppress(s_sup, a.suppress, V);  // the sampling walk's masks
     __syncthreads();
     if (live) {
         const int oi0 = b * a.out_cap;
@@ -109,60 +206,23 @@ __global__ __launch_bounds__(TW) void finalize_ts_kernel(TsArgs a) {
         auto masked = [&](int n) -> bool { return mr.masked(s_sup, n); };
         const float temp = P.temperature;
         auto val = [&](int n) { return temp > 0.0f ? lg[n] / temp : lg[n]; };
-        // this thread's logits (strided) and their mask bits, all loads up front
-        float lv[VJ];
-#pragma unroll
-        for (int j = 0; j < VJ; ++j) {
-            const int n = tid + j * TW;
-            lv[j] = lg[min(n, V - 1)];
-        }
-        uint64_t keep = 0;
-#pragma unroll
-        for (int j = 0; j < VJ; ++j) {  // branch-free (as beam_topk_kernel)
-            const int n = tid + j * TW;
-            keep |= (uint64_t)((n < V) & !masked(min(n, V - 1))) << j;
-            if (temp > 0.0f) lv[j] = lv[j] / temp;
-        }
-        // pass 1: maxima (first index on ties) of the text [0, beg) and timestamp [beg, V) ranges
-        const MaxI none{-INFINITY, 0x7fffffff};  // branch-free as in beam_topk_kernel (same bits)
+        // the row's maxima and exp sums: dec_ts_stats' chunks merged in chunk order (every thread
+        // merges the maxima the same way; thread 0 the sums)
+        const MaxI none{-INFINITY, 0x7fffffff};
+        const float* sp = a.stat + (size_t)b * TS_CHUNKS * 6;
         MaxI mt = none, ms = none;
-#pragma unroll
-        for (int j = 0; j < VJ; ++j) {
-            const int n = tid + j * TW;
-            const MaxI c = ((keep >> j) & 1) ? MaxI{lv[j], n} : none;
-            const bool t = n < beg;
-            mt = max_merge(mt, t ? c : none);
-            ms = max_merge(ms, t ? none : c);
+        for (int c = 0; c < TS_CHUNKS; ++c) {
+            mt = max_merge(mt, MaxI{sp[c * 6 + 0], __float_as_int(sp[c * 6 + 1])});
+            ms = max_merge(ms, MaxI{sp[c * 6 + 2], __float_as_int(sp[c * 6 + 3])});
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            mt = max_merge(mt, MaxI{__shfl_xor(mt.v, o, 64), __shfl_xor(mt.i, o, 64)});
-            ms = max_merge(ms, MaxI{__shfl_xor(ms.v, o, 64), __shfl_xor(ms.i, o, 64)});
-        }
-        if (lane == 0) { s_m[0][wv] = mt; s_m[1][wv] = ms; }
-        __syncthreads();
-        mt = s_m[0][0];
-        ms = s_m[1][0];
-        for (int w = 1; w < TW / 64; ++w) { mt = max_merge(mt, s_m[0][w]); ms = max_merge(ms, s_m[1][w]); }
         const float M = fmaxf(mt.v, ms.v);
-        // pass 2: sum exp over everything unmasked (log-softmax) and over the timestamps
-        float sa = 0.0f, st = 0.0f;
-        if (M > -INFINITY) {
-#pragma unroll
-            for (int j = 0; j < VJ; ++j) {
-                const bool k_ = (keep >> j) & 1;
-                const float ea = expf(lv[j] - M), et = expf(lv[j] - ms.v);
-                sa += k_ ? ea : 0.0f;
-                st += (k_ && tid + j * TW >= beg) ? et : 0.0f;
-            }
-        }
-        sa = wave_sum(sa);
-        st = wave_sum(st);
-        if (lane == 0) { s_s[0][wv] = sa; s_s[1][wv] = st; }
-        __syncthreads();
         if (tid == 0) {
             float za = 0.0f, zt = 0.0f;
-            for (int w = 0; w < TW / 64; ++w) { za += s_s[0][w]; zt += s_s[1][w]; }
+            for (int c = 0; c < TS_CHUNKS; ++c) {
+                const float mc = fmaxf(sp[c * 6 + 0], sp[c * 6 + 2]);
+                if (mc > -INFINITY) za += sp[c * 6 + 4] * expf(mc - M);
+                if (sp[c * 6 + 2] > -INFINITY) zt += sp[c * 6 + 5] * expf(sp[c * 6 + 2] - ms.v);
+            }
             const float lse = logf(za) + M;
             // timestamp_logprob > max_text_token_logprob (both relative to the same LSE)
             const float ts_lp = zt > 0.0f ? logf(zt) + ms.v - lse : -INFINITY;
@@ -432,10 +492,172 @@ __global__ __launch_bounds__(256) void kv_gather_kernel(const T* __restrict__ sr
 
 }  // namespace
 
+// The beam candidates over TS_CHUNKS workgroups per row (as ts_stats_kernel): each chunk writes
+// its maxima, its exp sums relative to its own maxima, and its k best tokens by (logit desc, id
+// asc) twice -- over every unmasked token and over the unmasked timestamps, since which set the
+// row draws from (the timestamp rule) depends on the whole row.  beam_merge_kernel merges them.
+static __global__ __launch_bounds__(TS_T) void beam_chunk_kernel(BeamArgs a) {
+    __shared__ uint32_t s_sup[TS_T * TS_J / 32 + 2];
+    __shared__ MaxI s_m[2][TS_T / 64];
+    __shared__ float s_s[2][TS_T / 64];
+    __shared__ MaxI s_k[TS_T / 64];
+    __shared__ MaxI s_win;
+    const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int step = a.step[0];
+    const TsParams& P = *a.prm;
+    const int V = a.n_vocab, beg = a.beg, eot = a.eot;
+    const int CS = (V + TS_CHUNKS - 1) / TS_CHUNKS, n0 = c * CS, n1 = min(V, n0 + CS);
+    float* out = a.stat + ((size_t)b * TS_CHUNKS + c) * BEAM_STAT;
+    const int w0 = n0 >> 5, nw = n1 > n0 ? ((n1 - 1) >> 5) - w0 + 1 : 0;
+    for (int w = tid; w < nw; w += TS_T) s_sup[w] = a.suppress[w0 + w];
+    __syncthreads();
+    const float* lg = a.logits + (size_t)b * a.ldl;
+    const int last = a.row[4 * b + 0], pen = a.row[4 * b + 1], has_ts = a.row[4 * b + 2], seek_delta = a.row[4 * b + 3];
+    const bool last_ts = step > 0 && last >= beg;
+    const bool pen_ts = step < 2 || pen >= beg;
+    const MaskRule mr(P, step, eot, beg, a.blank, last_ts, pen_ts, has_ts, seek_delta);
+    float lv[TS_J];
+#pragma unroll
+    for (int j = 0; j < TS_J; ++j) lv[j] = lg[min(n0 + tid + j * TS_T, V - 1)];
+    uint32_t keep = 0, tsk = 0;
+#pragma unroll
+    for (int j = 0; j < TS_J; ++j) {
+        const int n = n0 + tid + j * TS_T;
+        const int nc = min(n, V - 1);
+        const bool sup = (s_sup[(nc >> 5) - w0] >> (nc & 31)) & 1u;
+        const bool k_ = (n < n1) & !(sup | mr.masked_rules(nc));
+        keep |= (uint32_t)k_ << j;
+        tsk |= (uint32_t)(k_ & (n >= beg)) << j;
+    }
+    const MaxI none{-INFINITY, 0x7fffffff};
+    MaxI mt = none, ms = none;
+#pragma unroll
+    for (int j = 0; j < TS_J; ++j) {
+        const int n = n0 + tid + j * TS_T;
+        const MaxI x = ((keep >> j) & 1) ? MaxI{lv[j], n} : none;
+        const bool t = n < beg;
+        mt = max_merge(mt, t ? x : none);
+        ms = max_merge(ms, t ? none : x);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mt = max_merge(mt, MaxI{__shfl_xor(mt.v, o, 64), __shfl_xor(mt.i, o, 64)});
+        ms = max_merge(ms, MaxI{__shfl_xor(ms.v, o, 64), __shfl_xor(ms.i, o, 64)});
+    }
+    if (lane == 0) { s_m[0][wv] = mt; s_m[1][wv] = ms; }
+    __syncthreads();
+    mt = s_m[0][0];
+    ms = s_m[1][0];
+    for (int w = 1; w < TS_T / 64; ++w) { mt = max_merge(mt, s_m[0][w]); ms = max_merge(ms, s_m[1][w]); }
+    const float M = fmaxf(mt.v, ms.v);
+    float sa = 0.0f, st = 0.0f;
+#pragma unroll
+    for (int j = 0; j < TS_J; ++j) {
+        const float ea = expf(lv[j] - M), et = expf(lv[j] - ms.v);
+        sa += ((keep >> j) & 1) ? ea : 0.0f;
+        st += ((tsk >> j) & 1) ? et : 0.0f;
+    }
+    sa = wave_sum(sa);
+    st = wave_sum(st);
+    if (lane == 0) { s_s[0][wv] = sa; s_s[1][wv] = st; }
+    __syncthreads();
+    if (tid == 0) {
+        float za = 0.0f, zt = 0.0f;
+        for (int w = 0; w < TS_T / 64; ++w) { za += s_s[0][w]; zt += s_s[1][w]; }
+        out[0] = mt.v; out[1] = __int_as_float(mt.i);
+        out[2] = ms.v; out[3] = __int_as_float(ms.i);
+        out[4] = M > -INFINITY ? za : 0.0f;
+        out[5] = ms.v > -INFINITY ? zt : 0.0f;
+    }
+    // the chunk's k best, over everything (list 0) and over the timestamps (list 1)
+    const int k = a.k;
+    for (int list = 0; list < 2; ++list) {
+        uint32_t kk = list ? tsk : keep;
+        for (int r = 0; r < 8; ++r) {
+            MaxI x = none;
+            if (r < k) {
+#pragma unroll
+                for (int j = 0; j < TS_J; ++j) x = max_merge(x, ((kk >> j) & 1) ? MaxI{lv[j], n0 + tid + j * TS_T} : none);
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) x = max_merge(x, MaxI{__shfl_xor(x.v, o, 64), __shfl_xor(x.i, o, 64)});
+                if (lane == 0) s_k[wv] = x;
+                __syncthreads();
+                if (tid == 0) {
+                    MaxI m = s_k[0];
+                    for (int w = 1; w < TS_T / 64; ++w) m = max_merge(m, s_k[w]);
+                    s_win = m;
+                }
+                __syncthreads();
+                x = s_win;
+                const int jj = (x.i - n0 - tid) / TS_T;  // the owner drops its winner
+                if (x.v > -INFINITY && x.i >= n0 && (x.i - n0) % TS_T == tid) kk &= ~(1u << jj);
+            }
+            if (tid == 0) {
+                out[6 + list * 16 + 2 * r] = x.v;
+                out[6 + list * 16 + 2 * r + 1] = __int_as_float(x.i);
+            }
+        }
+    }
+}
+
+// One wavefront per row: the chunks' maxima and sums merged in chunk order (the log-softmax
+// denominator and the timestamp rule), then the row's k best from the chunks' lists of the set the
+// rule allows, by (logit desc, id asc), with their log-probabilities.
+static __global__ __launch_bounds__(64) void beam_merge_kernel(BeamArgs a) {
+    const int b = blockIdx.x, lane = threadIdx.x;
+    const float* sp = a.stat + (size_t)b * TS_CHUNKS * BEAM_STAT;
+    const MaxI none{-INFINITY, 0x7fffffff};
+    MaxI mt = none, ms = none;
+    for (int c = 0; c < TS_CHUNKS; ++c) {
+        mt = max_merge(mt, MaxI{sp[c * BEAM_STAT + 0], __float_as_int(sp[c * BEAM_STAT + 1])});
+        ms = max_merge(ms, MaxI{sp[c * BEAM_STAT + 2], __float_as_int(sp[c * BEAM_STAT + 3])});
+    }
+    const float M = fmaxf(mt.v, ms.v);
+    float za = 0.0f, zt = 0.0f;  // every lane the same sums, in chunk order
+    for (int c = 0; c < TS_CHUNKS; ++c) {
+        const float* q = sp + c * BEAM_STAT;
+        const float mc = fmaxf(q[0], q[2]);
+        if (mc > -INFINITY) za += q[4] * expf(mc - M);
+        if (q[2] > -INFINITY) zt += q[5] * expf(q[2] - ms.v);
+    }
+    const float lse = logf(za) + M;
+    const float ts_lp = zt > 0.0f ? logf(zt) + ms.v - lse : -INFINITY;
+    const bool rule = ms.v > -INFINITY && ts_lp > mt.v - lse;
+    const int list = rule ? 1 : 0, k = a.k;
+    // candidates: chunk c's r-th entry at slot c * 8 + r; lane l holds slots l and l + 64
+    MaxI cand[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int slot = lane + 64 * h, c = slot >> 3, r = slot & 7;
+        const float* q = sp + c * BEAM_STAT + 6 + list * 16 + 2 * r;
+        cand[h] = (c < TS_CHUNKS && r < k) ? MaxI{q[0], __float_as_int(q[1])} : none;
+    }
+    for (int r = 0; r < k; ++r) {
+        MaxI x = max_merge(cand[0], cand[1]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) x = max_merge(x, MaxI{__shfl_xor(x.v, o, 64), __shfl_xor(x.i, o, 64)});
+        const bool ok = x.v > -INFINITY && x.i < a.n_vocab;
+        if (lane == 0) {
+            a.cand_id[b * 8 + r] = ok ? x.i : -1;
+            a.cand_lp[b * 8 + r] = ok ? x.v - lse : -INFINITY;
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            if (ok && cand[h].i == x.i) cand[h] = none;
+    }
+    if (lane == 0) a.tid[b] = ms.v > -INFINITY ? ms.i : 0;
+}
+
 void dec_beam_topk(const BeamArgs& a, int B, hipStream_t st) {
     if (a.k < 1 || a.k > 8) throw std::runtime_error("beam_topk: 1..8 candidates");
     if (a.n_vocab < 1 || a.n_vocab > VJ * TW) throw std::runtime_error("beam_topk: vocabulary above 53248 tokens");
-    hipLaunchKernelGGL(beam_topk_kernel, dim3(B), dim3(TW), 0, st, a);
+    if (a.stat) {
+        hipLaunchKernelGGL(beam_chunk_kernel, dim3(TS_CHUNKS, B), dim3(TS_T), 0, st, a);
+        SPT_LAUNCH_CHECK();
+        hipLaunchKernelGGL(beam_merge_kernel, dim3(B), dim3(64), 0, st, a);
+    } else {
+        hipLaunchKernelGGL(beam_topk_kernel, dim3(B), dim3(TW), 0, st, a);
+    }
     SPT_LAUNCH_CHECK();
 }
 
@@ -450,7 +672,15 @@ void dec_kv_gather(int dtype, const void* src, void* dst, const int* rows, int L
     SPT_LAUNCH_CHECK();
 }
 
+void dec_ts_stats(const TsArgs& a, int B, hipStream_t st) {
+    if (a.n_vocab < 1 || a.n_vocab > TS_CHUNKS * TS_T * TS_J) throw std::runtime_error("ts_stats: vocabulary above 53248 tokens");
+    if (!a.stat) throw std::runtime_error("ts_stats: no statistics buffer");
+    hipLaunchKernelGGL(ts_stats_kernel, dim3(TS_CHUNKS, B), dim3(TS_T), 0, st, a);
+    SPT_LAUNCH_CHECK();
+}
+
 void dec_finalize_ts(int dtype, const TsArgs& a, int B, hipStream_t st) {
+    if (!a.stat) throw std::runtime_error("finalize_ts: no chunk statistics (dec_ts_stats)");
     if (a.n_vocab < 1 || a.n_vocab > VJ * TW) throw std::runtime_error("finalize_ts: vocabulary above 53248 tokens");
     if (dtype == DT_BF16) hipLaunchKernelGGL(finalize_ts_kernel<bf16>, dim3(B), dim3(TW), 0, st, a);
     else hipLaunchKernelGGL(finalize_ts_kernel<float>, dim3(B), dim3(TW), 0, st, a);

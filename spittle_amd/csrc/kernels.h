@@ -223,8 +223,13 @@ struct TsArgs {
     const void* emb; const float* pos; int d, ctx, Tq;
     float* x;
     DecState* ds; unsigned* arrive;
+    float* stat;                         // [B][TS_CHUNKS][6] per-chunk maxima and sums (dec_ts_stats)
 };
-// whisper_process_logits + whisper_sample_token + per-decoder bookkeeping (k_sample.hip)
+constexpr int TS_CHUNKS = 16;  // vocabulary chunks per row in dec_ts_stats
+// whisper_process_logits' maxima and exp sums of each row, over TS_CHUNKS workgroups per row
+// (a.stat), then whisper_process_logits + whisper_sample_token + per-decoder bookkeeping, one
+// workgroup per row (k_sample.hip)
+void dec_ts_stats(const TsArgs& a, int B, hipStream_t st);
 void dec_finalize_ts(int dtype, const TsArgs& a, int B, hipStream_t st);
 // beam search: the k best processed candidates of each decoder row (k_sample.hip)
 struct BeamArgs {
@@ -237,7 +242,10 @@ struct BeamArgs {
     int k;             // 1..8
     int* cand_id; float* cand_lp;  // [B][8]
     int* tid;          // [B] most probable timestamp (0: none)
+    float* stat;       // [B][TS_CHUNKS][BEAM_STAT] per-chunk statistics and candidates (nullptr: one
+                       // workgroup per row sweeps the row itself, the r4 first kernel)
 };
+constexpr int BEAM_STAT = 6 + 4 * 8;  // maxima + sums, then 8 (v, id) over everything and 8 over timestamps
 void dec_beam_topk(const BeamArgs& a, int B, hipStream_t st);
 // self-K/V cache rows for the next beam step: dst row b <- src row rows[b], positions < pos0
 void dec_kv_gather(int dtype, const void* src, void* dst, const int* rows, int L, int B, int H, int ctx,
