@@ -613,14 +613,14 @@ struct AttnWave {
     float m[NQ], l[NQ], o[NQ][8];
     const T *Kb, *Vb;
     int n_keys, slot;
-    int64_t bstride = 2048;  // 32-key blocks this far apart (2048: key rows contiguous, [T][64])
+    int bstride = 2048;  // 32-key blocks this far apart (2048: key rows contiguous, [T][64])
 
     __device__ __forceinline__ void init(const T* K, const T* V, int nk, int lane, int64_t blk_stride = 0) {
         slot = lane >> 3;
         Kb = K;
         Vb = V;
         n_keys = nk;
-        bstride = blk_stride ? blk_stride : 32 * 64;  // one branch-free offset formula for both layouts
+        bstride = blk_stride ? (int)blk_stride : 32 * 64;  // one branch-free offset formula for both layouts
 #pragma unroll
         for (int t = 0; t < NQ; ++t) {
             m[t] = -INFINITY;
@@ -633,7 +633,9 @@ struct AttnWave {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             const int key = min(blk * KB + 8 * i + slot, n_keys - 1);
-            const size_t off = (size_t)(key >> 5) * bstride + (size_t)(key & 31) * 64;
+            // 32-bit element offsets (the launchers check that a layer's K/V spans < 2^31 elements):
+            // the 64-bit multiply per key was a third of the loop's address VALU (r4)
+            const uint32_t off = (uint32_t)((key >> 5) * bstride + (key & 31) * 64);  // zero-extends for free
             kc[i].load(Kb + off);
             vc[i].load(Vb + off);
         }
@@ -1096,6 +1098,8 @@ void dec_cross_attn(int dtype, const void* q, const void* kv, int B, int B_layou
     if (splits < 1 || splits > 4 || (splits > 1 && !part)) throw std::runtime_error("dec_cross_attn: 1..4 key chunks");
     if (share < 1 || share > 8 || B % share) throw std::runtime_error("dec_cross_attn: rows per window 1..8, dividing B");
     if (share > 1 && !kvrow) throw std::runtime_error("dec_cross_attn: shared windows need the window map");
+    if ((int64_t)cdiv(T_enc, 32) * B_layout * H * 4096 >= (int64_t)INT32_MAX)
+        throw std::runtime_error("dec_cross_attn: a layer's cross K/V exceeds 2^31 elements");
     const int nq = share * Tq;
     // queries per workgroup: 1 or 4 as without a window map; a decode step of several rows per
     // window takes 5 (bf16: beam 5 / best_of 5 in one workgroup; 8 would spill) or 4 (f32) of
@@ -1131,6 +1135,8 @@ void dec_cross_attn_vw(int dtype, const void* q, const void* kv, int B, int B_la
     if (Tq < 1 || Tq > 4) throw std::runtime_error("dec_cross_attn_vw: 1..4 queries per sequence");
     if (share < 1 || share > 8 || B % share) throw std::runtime_error("dec_cross_attn_vw: rows per window 1..8, dividing B");
     if (share > 1 && !kvrow) throw std::runtime_error("dec_cross_attn_vw: shared windows need the window map");
+    if ((int64_t)cdiv(T_enc, 32) * B_layout * H * 4096 >= (int64_t)INT32_MAX)
+        throw std::runtime_error("dec_cross_attn_vw: a layer's cross K/V exceeds 2^31 elements");
     if (!part) throw std::runtime_error("dec_cross_attn_vw: needs the partials buffer");
     const int nq = share * Tq;
     // the same query chunks and keys per lane as dec_cross_attn (bitwise the same partials); per_query
