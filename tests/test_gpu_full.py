@@ -110,6 +110,24 @@ def test_too_short_and_empty(tiny):
         assert r.text == "" and r.segments == [] and r.n_windows == 0
 
 
+@pytest.mark.parametrize("n", [16159, 16160, 16320, 480000, 480001, 496000])
+def test_window_boundary_lengths(tiny, n):
+    """Input lengths at the seek loop's edges (oracle/whisper_full.py:281-287): the one-second
+    threshold (16160 samples decode nothing, 16320 one window), exactly 30 s, 30 s + 1 sample,
+    and 31 s, whose second window starts within 5 s of the end (prompt_past cleared) -- the same
+    window count and tokens as the oracle (full.cpp's seek loop)."""
+    e, om = tiny
+    x = np.concatenate([O.synth_audio(95), O.synth_audio(96)])[:n]
+    p = W.Params(max_tokens=16)
+    r = e.transcribe_samples(x, _params(max_new_tokens=16))
+    wins, segs, toks, _ = W.transcribe(om, x, p)
+    if not wins:
+        assert r.n_windows == 0 and r.text == "" and r.segments == []
+        return
+    if _compare(r, wins, segs, toks):
+        assert r.n_windows == len(wins)
+
+
 def test_temperature_fallback(tiny):
     """logprob_thold above any average log-probability forces every fallback: 0, 0.2, ..., 1.0
     (5 fallbacks), best_of = 5 sampled decoders per window at temperature > 0; the same seed
