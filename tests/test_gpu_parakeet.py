@@ -115,6 +115,23 @@ def test_end_to_end_f32_matches_oracle(small32, ms):
     assert len(r.segments) == len(t)  # token granularity
 
 
+@pytest.mark.parametrize("n", [400, 1600, 160 * 63, 160 * 64, 160 * 64 + 1, 160 * 65, 160 * 127 + 159])
+def test_end_to_end_ragged_lengths(small32, n):
+    """Lengths at the mel hop and the 8x subsampling edges (63 / 64 / 65 mel frames -> 8 / 8 / 9
+    encoder frames, and clips of 1-2 encoder frames): encoder frame count, tokens and frames as
+    the oracle's, up to its first decision closer than 2e-3 (f32 bar)."""
+    e, om = small32
+    pcm = synth_audio(40, n)
+    r = e.transcribe_samples(pcm, _tok_params())
+    enc = om.encode(P.mel(pcm))
+    t, f, t1, _ = om.decode(enc)
+    i, gap = P.first_disagreement(list(r.tokens), list(r.frames), list(t), list(f), om.decode_gaps(enc)[4])
+    assert gap == float("inf") or gap < 2e-3, (i, gap)
+    assert e.debug_encode(P.mel(pcm)).shape == enc.shape
+    if gap == float("inf"):
+        assert np.abs(r.top1 - t1).max() < 1e-3
+
+
 def test_batch_matches_single(small32):
     e, _ = small32
     pcms = [synth_audio(10 + i, n) for i, n in enumerate([16000 * 3, 7777, 16000 + 160 * 5])]
