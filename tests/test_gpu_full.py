@@ -177,6 +177,19 @@ def test_beam_search(tiny, beam, seconds, seed):
     assert g.n_windows >= 1 and r.n_windows >= 1
 
 
+def test_beam_search_multi_window(tiny):
+    """beam_size 4 over 45 s: the winning decoder's tokens set each window's seek and the next
+    window's prompt, as in the oracle's seek loop."""
+    e, om = tiny
+    x = np.concatenate([O.synth_audio(92), O.synth_audio(93)[:240000]])
+    r = e.transcribe_samples(x, _params(beam_size=4, max_new_tokens=16))
+    wins, segs, toks, _ = W.transcribe(om, x, W.Params(max_tokens=16, beam_size=4))
+    assert len(wins) >= 2
+    if _compare(r, wins, segs, toks):
+        assert r.n_windows == len(wins)
+    assert r.n_windows >= 2
+
+
 def test_beam_needs_rows():
     from spittle_amd import TranscriptionError, WhisperEngine, WhisperModelParams
     e = WhisperEngine(WhisperModelParams(dtype="f32", max_batch=2, seed=SEED))
