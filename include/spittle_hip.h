@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SPT_ABI_VERSION 11
+#define SPT_ABI_VERSION 12
 
 typedef enum {
     SPT_OK = 0,
@@ -184,7 +184,12 @@ spt_status spt_get_timings(const spt_ctx* ctx, spt_timings* t);
  * ABI 11: whisper_full computes the log-mel of each whole utterance once (whisper_pcm_to_mel: its
  * own reflective head, the utterance's global max - 8 clamp) and encodes each 30 s window at
  * `seek` once (whisper_encode_internal), shared by every temperature fallback and by the
- * utterance's beam / best_of decoders: encoder_windows counts those encoder runs. */
+ * utterance's beam / best_of decoders: encoder_windows counts those encoder runs.
+ * ABI 12: one-token decoder passes of up to 8 rows run every decoder layer as ONE persistent
+ * launch (bitwise the per-stage launch chain); pd_passes counts them.  It needs every CU: when
+ * another context's or process's kernels hold some, the pass gives up and the call is re-run on
+ * the launch chain (pd_fallbacks; the result is the same).  SPT_PERSISTENT=0 in the environment
+ * (read when a context is created) keeps the launch chain. */
 typedef struct {
     int32_t engine_calls;     /* decoder runs (a prompt pass + its steps; ABI <= 10: each with its own
                                  mel + encoder + cross K/V) */
@@ -195,6 +200,8 @@ typedef struct {
     double device_ms;         /* device time of those runs and steps (HIP events) */
     double encoder_ms;
     double decode_ms;         /* decoder passes incl. prompt prefill and sampling */
+    int32_t pd_passes;        /* ABI 12: decoder passes that ran as one persistent launch */
+    int32_t pd_fallbacks;     /* ABI 12: calls / beam steps re-run on the launch chain */
 } spt_call_stats;
 
 spt_status spt_get_call_stats(const spt_ctx* ctx, spt_call_stats* s);

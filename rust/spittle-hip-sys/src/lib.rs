@@ -1,4 +1,4 @@
-//! Raw bindings to `include/spittle_hip.h` (ABI 11), the C boundary of the MI355X-native Whisper
+//! Raw bindings to `include/spittle_hip.h` (ABI 12), the C boundary of the MI355X-native Whisper
 //! and Parakeet-V3 backend.  One item per declaration of the header, same names, same layouts (x86-64 SysV; the
 //! layouts are checked field by field against gcc by tests/test_capi.py).  Safe wrappers live in
 //! the `spittle-hip` crate.
@@ -6,7 +6,7 @@
 
 use std::os::raw::{c_char, c_int, c_void};
 
-pub const SPT_ABI_VERSION: c_int = 11;
+pub const SPT_ABI_VERSION: c_int = 12;
 pub const SPT_PK_STAGE_COUNT: c_int = 9;
 
 pub type spt_status = c_int;
@@ -117,6 +117,10 @@ pub struct spt_call_stats {
     pub device_ms: f64,
     pub encoder_ms: f64,
     pub decode_ms: f64,
+    /// ABI 12: decoder passes run as one persistent launch
+    pub pd_passes: i32,
+    /// ABI 12: calls / beam steps re-run on the launch chain after the persistent pass gave up
+    pub pd_fallbacks: i32,
 }
 
 #[repr(C)]

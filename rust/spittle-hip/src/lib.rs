@@ -1,5 +1,5 @@
 //! `HipWhisperEngine` and `HipParakeetEngine`: the `transcribe_rs::TranscriptionEngine` surfaces
-//! Spittle binds to, backed by the MI355X-native library (`libspittle_hip.so`, C ABI 10), plus `HipFrameResampler` and
+//! Spittle binds to, backed by the MI355X-native library (`libspittle_hip.so`, C ABI 12), plus `HipFrameResampler` and
 //! `HipSmoothedVad` (the capture-side resampler and voice-activity gate).
 //!
 //! What it replaces in the app (/root/reference/src-tauri/src/managers/transcription.rs):

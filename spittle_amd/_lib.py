@@ -92,7 +92,8 @@ class Timings(C.Structure):
 
 class CallStats(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("engine_calls", "decoder_passes", "beam_steps", "encoder_windows")] + \
-               [(n, C.c_double) for n in ("device_ms", "encoder_ms", "decode_ms")]
+               [(n, C.c_double) for n in ("device_ms", "encoder_ms", "decode_ms")] + \
+               [(n, C.c_int32) for n in ("pd_passes", "pd_fallbacks")]
 
 
 class PkModelParams(C.Structure):

@@ -3,10 +3,11 @@
 // Mirrors transcribe-rs' WhisperEngine surface as Spittle uses it
 // (/root/reference/src-tauri/src/managers/transcription.rs: new + load_model 261-276,
 // transcribe_samples 494-503, unload_model 175-208): status codes + message,
-// borrowed input PCM, library-owned results.  On the fast path an utterance longer than
-// 30 s is decoded as 30 s windows of its whole log-mel (frames 3000 k ..), independent
-// batch items whose text is concatenated (whisper.cpp's seek loop also conditions each
-// window on the previous text: a documented difference).
+// borrowed input PCM, library-owned results.  The fast path (no timestamps, greedy, no
+// fallback) decodes one-window utterances; longer or sub-second ones take whisper_full's
+// seek loop at the same parameters (spt_transcribe_batch).  Only the benchmark / test hooks
+// (SPT_IGNORE_EOT, forced tokens) cut an utterance into fixed 30 s windows of its whole
+// log-mel (frames 3000 k ..), independent batch items whose text is concatenated.
 #include <hip/hip_runtime.h>
 #include <string.h>
 
@@ -282,17 +283,20 @@ spt_status run_windows(spt_ctx* c, std::vector<Window>& win, const float* const*
     // per call from offset 0); later windows reuse it
     std::vector<int> utt_lang(n_utt, (!autolang && rq.prompt.size() >= 3) ? rq.prompt[1] : -1);
     const int cap = e.max_batch();
+    std::vector<int> loaded;  // the utterances whose PCM and whole log-mel are resident
     for (size_t g0 = 0; g0 < win.size(); g0 += cap) {
         const int B = (int)std::min<size_t>(cap, win.size() - g0);
-        // the utterances of this batch of windows, each log-mel computed whole (an utterance whose
-        // windows span two batches is loaded by both: the same bytes, the same mel)
+        // the utterances of this batch of windows, each log-mel computed whole.  An utterance whose
+        // windows span several batches stays loaded while the batches hold only it (one long
+        // recording: loaded once, not once per batch of windows -- ADVICE r4)
         std::vector<const float*> up;
-        std::vector<int> un, wu(B), ws(B);
+        std::vector<int> un, uid, wu(B), ws(B);
         for (int b = 0; b < B; ++b) {
             const int u = win[g0 + b].utt;
             if (b == 0 || win[g0 + b - 1].utt != u) {
                 up.push_back(pcm[u]);
                 un.push_back((int)n_samples[u]);
+                uid.push_back(u);
             }
             wu[b] = (int)up.size() - 1;
             ws[b] = win[g0 + b].seek;
@@ -309,7 +313,10 @@ spt_status run_windows(spt_ctx* c, std::vector<Window>& win, const float* const*
         }
         std::vector<int> otok((size_t)B * rq.n_steps), lang(B, -1);
         std::vector<float> o1((size_t)B * rq.n_steps), o2((size_t)B * rq.n_steps);
-        e.load_utterances(up.data(), un.data(), (int)up.size());
+        if (uid != loaded) {
+            e.load_utterances(up.data(), un.data(), (int)up.size());
+            loaded = uid;
+        }
         e.encode_windows(wu.data(), ws.data(), B);
         e.decode(B, rq, otok.data(), o1.data(), o2.data(), lang.data());
         for (int b = 0; b < B; ++b) {
@@ -341,7 +348,7 @@ spt_status run_windows(spt_ctx* c, std::vector<Window>& win, const float* const*
 
 extern "C" {
 
-const char* spt_version(void) { return "spittle_amd 0.11.0 (gfx950, ABI 11)"; }
+const char* spt_version(void) { return "spittle_amd 0.12.0 (gfx950, ABI 12)"; }
 
 const char* spt_language_code(int32_t lang_id) { return spt::lang_code(lang_id); }
 
@@ -470,13 +477,23 @@ spt_status spt_transcribe_batch(spt_ctx* ctx, const float* const* pcm, const siz
             return fail(ctx, classify(e), e.what());
         }
     }
+    // The fast path decodes one window at seek 0, which is exactly whisper_full's result for an input
+    // of one window that passes its one-second check.  Other inputs take whisper_full's seek loop
+    // (full.cpp, at these same parameters: no timestamps, greedy, no fallback), so they follow its
+    // window rules: nothing under the one-second threshold (n_len_org < 100 frames), a window only
+    // while seek + 100 < seek_end (480 001 samples decode one window, not two), and each later window
+    // conditioned on the earlier windows' tokens (prompt_past).  The benchmark / test hooks
+    // (SPT_IGNORE_EOT, forced tokens) have no whisper_full meaning and keep fixed 30 s windows.
+    const bool hooks = (params->flags & SPT_IGNORE_EOT) || (params->forced_tokens && params->n_forced > 0);
     std::vector<Window> win;
-    std::vector<size_t> empty;
+    std::vector<size_t> empty, seek_loop;
     for (size_t u = 0; u < batch; ++u) {
         out[u] = nullptr;
         if (n_samples[u] == 0) { empty.push_back(u); continue; }  // "" without an engine call
         if (!pcm[u]) return fail(ctx, SPT_ERR_INVALID_ARG, "null pcm");
         if (n_samples[u] > (size_t)INT32_MAX / 2) return fail(ctx, SPT_ERR_INVALID_ARG, "utterance too long");
+        const int n_len = 1 + ((int)n_samples[u] - 200) / 160;  // log_mel_spectrogram's n_len_org
+        if (!hooks && (n_len < 100 || n_samples[u] > (size_t)kWindow)) { seek_loop.push_back(u); continue; }
         for (size_t o = 0; o < n_samples[u]; o += kWindow) win.push_back(Window{(int)u, (int)(o / 160)});
     }
     try {
@@ -487,6 +504,18 @@ spt_status spt_transcribe_batch(spt_ctx* ctx, const float* const* pcm, const siz
             s = run_windows(ctx, win, pcm, n_samples, batch, params, tmp.data());
             if (s != SPT_OK) return s;
             for (size_t u = 0; u < batch; ++u) out[u] = tmp[u];
+        }
+        if (!seek_loop.empty()) {
+            std::vector<const float*> sp;
+            std::vector<size_t> sn;
+            for (size_t u : seek_loop) { sp.push_back(pcm[u]); sn.push_back(n_samples[u]); }
+            std::vector<spt_result*> tmp(seek_loop.size(), nullptr);
+            s = run_full(ctx, sp.data(), sn.data(), sp.size(), params, tmp.data());
+            if (s != SPT_OK) {
+                for (size_t u = 0; u < batch; ++u) { spt_result_free(out[u]); out[u] = nullptr; }
+                return s;
+            }
+            for (size_t i = 0; i < seek_loop.size(); ++i) out[seek_loop[i]] = tmp[i];
         }
         for (size_t u : empty) {
             if (out[u]) spt_result_free(out[u]);
@@ -603,6 +632,7 @@ spt_status spt_get_call_stats(const spt_ctx* ctx, spt_call_stats* s) {
     s->engine_calls = c.engine_calls; s->decoder_passes = c.decoder_passes; s->beam_steps = c.beam_steps;
     s->encoder_windows = c.encoder_windows;
     s->device_ms = c.device_ms; s->encoder_ms = c.encoder_ms; s->decode_ms = c.decode_ms;
+    s->pd_passes = c.pd_passes; s->pd_fallbacks = c.pd_fallbacks;
     return SPT_OK;
 }
 

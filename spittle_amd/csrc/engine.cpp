@@ -98,6 +98,8 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     if ((3 * cp_ * esz_) % 128) cp_ = ((dm_.n_mels + 127) / 128) * 128;
     if (const char* g = getenv("SPT_DECODE_GROUPS")) n_groups_ = std::max(1, std::min(4, atoi(g)));
     if (const char* v = getenv("SPT_XATTN_SPLIT")) xsplit_ = std::max(1, std::min(4, atoi(v)));
+    if (const char* v = getenv("SPT_PERSISTENT")) pd_env_ = atoi(v) != 0;
+    pd_able_ = pdec_unsupported(dt_, dm_.d, dm_.n_head, 1, dm_.n_text_ctx, dm_.n_audio_ctx).empty();
     // cross-attention key split: fixed per engine (never per batch).  The fc2 K split (2; r1
     // exp14 measured 2 slightly faster per layer than 4: the next QKV LayerNorm prologue sums
     // fewer slabs) is fixed per engine too; the pending-slab count a LayerNorm prologue sums is
@@ -117,7 +119,18 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     try {
         gemv_prepare(dt_);
         gemm_prepare();  // > 64 KiB LDS attributes on this device, before any capture
+        if (pd_able_) pdec_prepare();
         alloc_weights();
+        if (pd_able_) {  // the persistent pass reads each layer's weight pointers from device memory
+            std::vector<PdLayer> t(dm_.n_dec);
+            for (int l = 0; l < dm_.n_dec; ++l) {
+                const DecL& e = dec_[l];
+                t[l] = PdLayer{e.ln1_w, e.ln1_b, e.qkv_w, e.qkv_b, e.so_w, e.so_b, e.ln2_w, e.ln2_b, e.cq_w, e.cq_b,
+                               e.co_w, e.co_b, e.ln3_w, e.ln3_b, e.fc1_w, e.fc1_b, e.fc2_w, e.fc2_b};
+            }
+            HIP_CHECK(hipMalloc(&pd_layers_, t.size() * sizeof(PdLayer)));
+            HIP_CHECK(hipMemcpy(pd_layers_, t.data(), t.size() * sizeof(PdLayer), hipMemcpyHostToDevice));
+        }
         if (external_weights) {
             // filled later by import_weights; clear it so a premature use reads zeros, not garbage
             HIP_CHECK(hipMemsetAsync(warena_, 0, wbytes_, st_));
@@ -152,6 +165,8 @@ void Engine::release() {
     if (warena_) (void)hipFree(warena_);
     if (aarena_) (void)hipFree(aarena_);
     if (kvtmp_) (void)hipFree(kvtmp_);
+    if (pd_layers_) (void)hipFree(pd_layers_);
+    pd_layers_ = nullptr;
     for (void* p : {(void*)upcm_, (void*)umel_, (void*)uinfo_})
         if (p) (void)hipFree(p);
     upcm_ = umel_ = nullptr;
@@ -593,6 +608,11 @@ void Engine::alloc_workspace() {
             g.cand_lp = (float*)c.take(B * 8 * 4);
             g.beam_tid = (int*)c.take(B * 4);
             g.kvrow = (int*)c.take(B * 4);
+            if (pd_able_) {
+                g.pctl = (unsigned*)c.take(64);
+                g.gran_bytes = pdec_granules((int)std::min<int64_t>(8, B), (int)d, dm_.n_head) * 8;
+                g.gran = (unsigned long long*)c.take(g.gran_bytes);
+            }
         }
         zero_ = (float*)c.take(R * d * 4);  // never written: the "no pending slab" operand
         if (!pass) {
@@ -863,6 +883,23 @@ float* Engine::enqueue_layers(DecGroup& g, int E, int Tq) {
     const int xs = vw ? (vw_merge ? 1 : 8) : mapped ? 1 : xsplit_;
     const int ks = dt_ == DT_BF16 ? 128 : 64;
     hipStream_t st = g.st;
+    if (Tq == 1 && pd_active_ && R <= 8) {
+        // every layer in one persistent launch (k_pdec.hip), bitwise this chain's result; it leaves
+        // the head's operands where the chain does: x (here dx2) + fc2's two pending slabs
+        PdArgs p{};
+        p.layers = pd_layers_; p.L = dm_.n_dec;
+        p.d = d; p.H = H; p.R = R; p.ctx = ctx; p.T_enc = T; p.B_layout = E;
+        p.ckv = (const char*)ckv_ + (mapped ? 0 : (int64_t)g.b0 * H * 4096) * esz_;
+        p.cross_layer = cross_layer;
+        p.kvrow = mapped ? g.kvrow : nullptr;
+        p.skv = g.skv; p.self_layer = self_layer;
+        p.x = g.dx; p.xo = g.dx2; p.pend = g.pend; p.ds = g.ds; p.gran = g.gran; p.ctl = g.pctl;
+        pdec_launch(p, st);
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        HIP_CHECK(hipStreamIsCapturing(st, &cap));
+        if (cap == hipStreamCaptureStatusNone) cs_.pd_passes++;  // replays of a captured pass count where launched
+        return g.dx2;
+    }
     float* xc = g.dx;   // current residual rows (dec_embed / dec_finalize wrote this pass's input here)
     float* xo = g.dx2;  // the other buffer
     int np = 0;         // pending slabs in g.pend
@@ -1026,11 +1063,27 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
     // groups (in whole windows of S rows), and a group whose prompt rows exceed it prefills the
     // prompt a chunk of tokens at a time (the same rows, positions and keys) and runs the logits
     // pass on the last prompt token alone
+    auto group_split = [&](int unit_rows, int* G_out) {  // -> the largest group's rows
+        const int nU = B / unit_rows;
+        *G_out = std::min((int)groups_.size(),
+                          std::max(std::min(n_groups_, nU), cdiv(nU, std::max(1, max_rows_ / unit_rows))));
+        return cdiv(nU, *G_out) * unit_rows;
+    };
+    int G = 0;
+    int Bg = group_split(std::max(1, S), &G);
+    // whole windows of S rows do not always fit the groups (groups_ is sized for rows split at any
+    // point: e.g. f32 medium, 23 rows per pass, 3 groups at max_batch 64: best_of 6 over 10 windows
+    // puts 4 windows = 24 rows in the largest group); the window
+    // map then runs with one row per run (share 1), which every strategy computes bitwise the same
+    if (S > 1 && Bg > max_rows_) {
+        S = 1;
+        Bg = group_split(1, &G);
+    }
     const int unit = std::max(1, S), nU = B / unit;
-    const int G = std::min((int)groups_.size(),
-                           std::max(std::min(n_groups_, nU), cdiv(nU, std::max(1, max_rows_ / unit))));
-    const int Bg = cdiv(nU, G) * unit;  // the largest group
     if (Bg > max_rows_) throw std::runtime_error("batch exceeds the decoder's rows per pass");
+    // one-token passes of up to 8 rows in one group run the persistent pass (it needs every CU: two
+    // groups' passes on two streams would each hold part of the chip)
+    pd_active_ = pd_able_ && pd_env_ && !pd_fallback_ && G == 1 && Bg <= 8;
     const int cmax = std::max(1, std::min(4, max_rows_ / Bg));
     const int Tq_head = Bg * Tq > max_rows_ ? 1 : Tq;
     if (P > ctx / 2 + 1) throw std::runtime_error("prompt prefix longer than n_text_ctx / 2 + 1");
@@ -1111,6 +1164,10 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         fill_f32(g.out_t1, (int64_t)g.B * out_cap, -INFINITY, g.st);
         fill_f32(g.out_t2, (int64_t)g.B * out_cap, -INFINITY, g.st);
         dec_reset(g.ds, g.arrive, g.st);
+        if (pd_active_) {  // the persistent pass's control words and granules start each call at zero
+            HIP_CHECK(hipMemsetAsync(g.pctl, 0, 16, g.st));
+            HIP_CHECK(hipMemsetAsync(g.gran, 0, (size_t)pdec_granules(g.B, dm_.d, dm_.n_head) * 8, g.st));
+        }
         if (rq.full)  // WHISPER_DECODER_INIT: seek_delta starts at a whole window (3000 frames)
             HIP_CHECK(hipMemcpyAsync(g.ts_state, ts_init_.data() + (size_t)g.b0 * 4, g.B * 16, hipMemcpyHostToDevice,
                                      g.st));
@@ -1142,8 +1199,10 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         for (DecGroup* g : act) {
             HIP_CHECK(hipMemcpyAsync(first.data() + (size_t)g->b0 * out_cap, g->out_tok, (size_t)g->B * out_cap * 4,
                                      hipMemcpyDeviceToHost, g->st));
+            if (pd_active_) HIP_CHECK(hipMemcpyAsync(&pd_err_host_, g->pctl + 2, 4, hipMemcpyDeviceToHost, g->st));
             HIP_CHECK(hipStreamSynchronize(g->st));
         }
+        if (pd_active_ && pd_err_host_) throw PdGaveUp();  // decode() re-runs the call on the chain
         for (int b = 0; b < B; ++b) {
             const int v = rq.lang_tok[b];
             lang[b] = v >= 0 ? v : first[(size_t)(-v - 1) * out_cap];
@@ -1189,6 +1248,7 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
     if (rq.beam_k > 0) {  // beam search continues step by step from the host (beam_next)
         tm_.n_decode_passes = 1;
         for (DecGroup* g : act) {
+            if (pd_active_) HIP_CHECK(hipMemcpyAsync(&pd_err_host_, g->pctl + 2, 4, hipMemcpyDeviceToHost, g->st));
             HIP_CHECK(hipEventRecord(g->ev, g->st));
             HIP_CHECK(hipStreamWaitEvent(st_, g->ev, 0));
         }
@@ -1216,6 +1276,7 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
             // into the cross-attention grid (the map itself is read from g->kvrow)
             GraphKey key{g->B, E, g->b0, out_cap, rq.n_forced, rq.flags, rq.full};
             key.share = S;
+            key.pd = pd_active_;
             auto it = g->graphs.find(key);
             if (it == g->graphs.end()) {
                 hipGraph_t graph;
@@ -1234,6 +1295,7 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         for (int s = 1; s < rq.n_steps; ++s) {
             for (size_t i = 0; i < act.size(); ++i) HIP_CHECK(hipGraphLaunch(ex[i], act[i]->st));
             ++passes;
+            if (pd_active_) cs_.pd_passes += (int)act.size();
             if (early_exit && (s % 16) == 0) {
                 bool all = true;
                 for (DecGroup* g : act) {
@@ -1254,6 +1316,7 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         if (ts_state_out && rq.full)
             HIP_CHECK(hipMemcpyAsync(ts_state_out + (size_t)g->b0 * 4, g->ts_state, (size_t)g->B * 16,
                                      hipMemcpyDeviceToHost, g->st));
+        if (pd_active_) HIP_CHECK(hipMemcpyAsync(&pd_err_host_, g->pctl + 2, 4, hipMemcpyDeviceToHost, g->st));
         HIP_CHECK(hipEventRecord(g->ev, g->st));
         HIP_CHECK(hipStreamWaitEvent(st_, g->ev, 0));
     }
@@ -1264,10 +1327,37 @@ void Engine::decode(int B, const DecodeRequest& rq, int* tokens, float* top1, fl
     select();
     require_weights();
     HIP_CHECK(hipEventRecord(ev_[6], st_));  // the decode groups wait for the encoded windows here
-    run_decode(B, rq, tokens, top1, top2, lang_out, ts_state_out);
+    pd_err_host_ = 0;
+    bool gave_up = false;
+    try {
+        run_decode(B, rq, tokens, top1, top2, lang_out, ts_state_out);
+    } catch (const PdGaveUp&) {
+        gave_up = true;
+    }
     HIP_CHECK(hipEventRecord(ev_[7], st_));
     HIP_CHECK(hipStreamSynchronize(st_));
     HIP_CHECK(hipGetLastError());
+    if (gave_up || (pd_active_ && pd_err_host_ != 0)) {
+        // the persistent pass could not hold every CU (another context's or process's kernels ran
+        // beside it) and gave up: the whole call again on the launch chain (re-runs are idempotent:
+        // outputs, state and caches are reset or rewritten)
+        fprintf(stderr, "[spt] persistent decoder pass gave up (code %u); re-running the call on the launch chain\n",
+                pd_err_host_);
+        for (DecGroup& g : groups_) HIP_CHECK(hipStreamSynchronize(g.st));
+        pd_fallback_ = true;
+        cs_.pd_fallbacks++;
+        try {
+            HIP_CHECK(hipEventRecord(ev_[6], st_));
+            run_decode(B, rq, tokens, top1, top2, lang_out, ts_state_out);
+            HIP_CHECK(hipEventRecord(ev_[7], st_));
+            HIP_CHECK(hipStreamSynchronize(st_));
+        } catch (...) {
+            pd_fallback_ = false;
+            throw;
+        }
+        pd_fallback_ = false;
+        pd_active_ = false;
+    }
     tm_.batch = B;
     cs_.engine_calls++;
     cs_.decoder_passes += tm_.n_decode_passes;
@@ -1420,29 +1510,42 @@ void Engine::beam_next(const int* src, const int* tokens, const int* rowstate, i
         enqueue_head(g, 1, beam_rq_, beam_rq_.n_steps, x, suppress_, (beam_rq_.flags & 1u) != 0);
     };
     static const bool no_graph = getenv("SPT_NO_GRAPH") != nullptr;
-    HIP_CHECK(hipEventRecord(ev_[8], g.st));
-    if (no_graph) {
-        beam_pass();
-    } else {
-        // n_forced = -beam_k marks a beam-step graph (a real n_forced is >= 0)
-        GraphKey key{B, enc_E_, side, beam_rq_.n_steps, -beam_rq_.beam_k, beam_rq_.flags, beam_rq_.full};  // b0: cache side
-        key.share = g.share;
-        auto it = g.graphs.find(key);
-        if (it == g.graphs.end()) {
-            hipGraph_t graph;
-            HIP_CHECK(hipStreamBeginCapture(g.st, hipStreamCaptureModeThreadLocal));
+    for (;;) {
+        HIP_CHECK(hipEventRecord(ev_[8], g.st));
+        if (no_graph) {
             beam_pass();
-            HIP_CHECK(hipStreamEndCapture(g.st, &graph));
-            hipGraphExec_t exec;
-            HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
-            HIP_CHECK(hipGraphDestroy(graph));
-            it = g.graphs.emplace(key, exec).first;
+        } else {
+            // n_forced = -beam_k marks a beam-step graph (a real n_forced is >= 0)
+            GraphKey key{B, enc_E_, side, beam_rq_.n_steps, -beam_rq_.beam_k, beam_rq_.flags, beam_rq_.full};  // b0: cache side
+            key.share = g.share;
+            key.pd = pd_active_;
+            auto it = g.graphs.find(key);
+            if (it == g.graphs.end()) {
+                hipGraph_t graph;
+                HIP_CHECK(hipStreamBeginCapture(g.st, hipStreamCaptureModeThreadLocal));
+                beam_pass();
+                HIP_CHECK(hipStreamEndCapture(g.st, &graph));
+                hipGraphExec_t exec;
+                HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+                HIP_CHECK(hipGraphDestroy(graph));
+                it = g.graphs.emplace(key, exec).first;
+            }
+            HIP_CHECK(hipGraphLaunch(it->second, g.st));
+            if (pd_active_) cs_.pd_passes++;
         }
-        HIP_CHECK(hipGraphLaunch(it->second, g.st));
+        HIP_CHECK(hipEventRecord(ev_[9], g.st));
+        pd_err_host_ = 0;
+        if (pd_active_) HIP_CHECK(hipMemcpyAsync(&pd_err_host_, g.pctl + 2, 4, hipMemcpyDeviceToHost, g.st));
+        read_cands(B, out);  // synchronises g.st
+        if (!pd_active_ || pd_err_host_ == 0) break;
+        // the persistent pass gave up (decode()): this step again, and the rest of the search, on
+        // the launch chain (the step is idempotent: the gather, the appends and the candidates are
+        // rewritten from the same inputs)
+        fprintf(stderr, "[spt] persistent decoder pass gave up in a beam step (code %u); launch chain\n", pd_err_host_);
+        pd_active_ = false;
+        cs_.pd_fallbacks++;
     }
-    HIP_CHECK(hipEventRecord(ev_[9], g.st));
     beam_side_ ^= 1;
-    read_cands(B, out);  // synchronises g.st
     float ms = 0.0f;
     HIP_CHECK(hipEventElapsedTime(&ms, ev_[8], ev_[9]));
     cs_.beam_steps++;

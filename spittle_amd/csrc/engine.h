@@ -65,8 +65,12 @@ struct Timings {
 // and beam step), summed; reset by the C ABI at the start of each spt_transcribe* call
 struct CallStats {
     int engine_calls = 0, decoder_passes = 0, beam_steps = 0, encoder_windows = 0;
+    int pd_passes = 0;     // decoder passes run as the persistent launch
+    int pd_fallbacks = 0;  // calls re-run on the launch chain after the persistent pass gave up
     double device_ms = 0, encoder_ms = 0, decode_ms = 0;
 };
+
+struct PdGaveUp {};  // the persistent decoder pass gave up inside run_decode (decode() re-runs the call)
 
 class Engine {
 public:
@@ -149,7 +153,9 @@ private:
         uint32_t flags;
         bool full;
         int share = 0;  // rows per window (0: identity rows, no window map)
+        bool pd = false;  // the layers run as the persistent pass (k_pdec.hip)
         bool operator<(const GraphKey& o) const {
+            if (pd != o.pd) return pd < o.pd;
             if (full != o.full) return full < o.full;
             if (B != o.B) return B < o.B;
             if (share != o.share) return share < o.share;
@@ -186,6 +192,9 @@ private:
         int *cand_id = nullptr, *beam_tid = nullptr;
         float* cand_lp = nullptr;
         int* kvrow = nullptr;         // [B] encoded window of each row (window map)
+        unsigned* pctl = nullptr;     // persistent pass: [kPdCtlWords] census / exits / error / launch
+        unsigned long long* gran = nullptr;  // persistent pass: granule arena (pdec_granules words)
+        int64_t gran_bytes = 0;
         int share = 0;                // rows per window of this call (0: identity, no map)
         std::map<GraphKey, hipGraphExec_t> graphs;
         std::vector<int> host_tok;    // host sources of the call's token uploads
@@ -212,6 +221,15 @@ private:
     float* enqueue_layers(DecGroup& g, int E, int Tq);
     void enqueue_head(DecGroup& g, int Tq, const DecodeRequest& rq, int out_cap, float* xc, const uint32_t* sup,
                       bool blank);
+
+    // the persistent decoder pass (k_pdec.hip): one launch for every layer of a one-token pass of at
+    // most 8 rows in one decode group.  SPT_PERSISTENT=0 keeps the launch chain (A/B measurements).
+    bool pd_able_ = false;       // this model / dtype / batch geometry can run it
+    bool pd_env_ = false;        // SPT_PERSISTENT=1 (default off until validated on the GPU)
+    bool pd_active_ = false;     // this call's one-token passes run it (set per run_decode)
+    bool pd_fallback_ = false;   // re-running a call whose persistent pass gave up (the chain instead)
+    PdLayer* pd_layers_ = nullptr;  // device copy of the decoder layers' pointers
+    unsigned pd_err_host_ = 0;      // the last call's error word (read back with the tokens)
 
     ModelDims dm_;
     int dt_, dev_, max_batch_;

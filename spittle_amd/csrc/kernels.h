@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 namespace spt {
 
 enum { DT_F32 = 0, DT_BF16 = 1, DT_F16 = 2 };  // DT_F16: the Parakeet encoder only
@@ -198,6 +200,49 @@ struct FinalizeArgs {
 // argmax reduce + record + next-token embed + step advance (replaces embed/argmax/advance)
 void dec_finalize(int dtype, const FinalizeArgs& a, int B, hipStream_t st);
 void dec_reset(DecState* ds, unsigned* arrive, hipStream_t st);
+
+// ------------------------------------------------------------------ persistent decoder pass (k_pdec.hip)
+// Every decoder layer of a one-token pass (Tq = 1, bf16) in ONE launch of one 512-thread workgroup
+// per CU: the eight per-layer stages of enqueue_layers (LN1+QKV, self-attention, self-out, LN2 +
+// cross-Q, cross-attention in 8 key chunks, their merge, cross-out, LN3+fc1, fc2) run as units
+// spread over the workgroups, each handing its output to the next stage as data-tagged 8-byte
+// granules.  Every unit repeats the per-stage kernels' arithmetic operation for operation (the
+// same K chains of each GEMV and their summation order, AttnWave's online softmax, attn_merge):
+// the pass is bitwise the launch chain's.
+struct PdLayer {
+    const float *ln1_w, *ln1_b; const void* qkv_w; const float* qkv_b;
+    const void* so_w; const float* so_b;
+    const float *ln2_w, *ln2_b; const void* cq_w; const float* cq_b;
+    const void* co_w; const float* co_b;
+    const float *ln3_w, *ln3_b; const void* fc1_w; const float* fc1_b;
+    const void* fc2_w; const float* fc2_b;
+};
+constexpr int kPdStages = 9;   // A B C D E E2 F G H
+struct PdArgs {
+    const PdLayer* layers; int L;            // device array [L]
+    int d, H, R, ctx, T_enc, B_layout;
+    const void* ckv; int64_t cross_layer;     // cross K/V (kv_offset layout, B_layout windows); at the
+                                              // group's first window when kvrow is null
+    const int* kvrow;                         // [R] window of each row, or null (row b -> window b)
+    void* skv; int64_t self_layer;            // self K/V, per layer [2][R][H][ctx][64]
+    const float* x;                           // [R][d] layer-0 input rows (kept: a failed pass re-runs)
+    float* xo;                                // [R][d] on return the last layer's cross-out residual
+    float* pend;                              // [2][R][d]: on return the last fc2's two K-split partials
+    const DecState* ds;
+    unsigned long long* gran;                 // granule arena: pdec_granules() words, zeroed per call
+    unsigned* ctl;                            // [4] census, exits, error, launch index (zeroed per call)
+    // geometry (pdec_launch fills it)
+    int nwg, e_vw, nss, U;
+    int n[kPdStages], pre[kPdStages], ks[kPdStages];
+    int64_t go[12];                           // granule buffer offsets
+};
+int64_t pdec_granules(int R, int d, int H);
+constexpr int kPdCtlWords = 4;
+// empty string if the persistent pass can run this geometry, else why not
+std::string pdec_unsupported(int dtype, int d, int H, int R, int ctx, int T_enc);
+void pdec_launch(PdArgs a, hipStream_t st);
+void pdec_prepare();  // kernel attributes (outside stream capture)
+
 
 // whisper_full decoding parameters of one call (device memory: read by graph-captured launches)
 struct TsParams {

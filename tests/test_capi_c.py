@@ -36,7 +36,7 @@ def test_c_program_compiles_and_links(tmp_path):
     r = subprocess.run([exe, "synthetic:tiny", "--link-only", _model_dir(tmp_path)], capture_output=True, text=True,
                        timeout=60)
     assert r.returncode == 0, r.stderr
-    assert "ABI 11" in r.stdout
+    assert "ABI 12" in r.stdout
     assert "parakeet dir: d 256, layers 2, heads 4, vocab 1024" in r.stdout
 
 

@@ -128,6 +128,106 @@ def test_window_boundary_lengths(tiny, n):
         assert r.n_windows == len(wins)
 
 
+def _long_audio(n, seed):
+    return np.concatenate([O.synth_audio(seed + k) for k in range((n + 479999) // 480000)])[:n]
+
+
+@pytest.mark.parametrize("n,seed", [(15000, 130), (480001, 131), (45 * 16000, 133), (75 * 16000, 136)])
+def test_fast_path_follows_seek_loop(tiny, n, seed):
+    """The fast path's protocol (no timestamps, greedy, temperature_inc 0: capi.cpp full_mode() is
+    false) on inputs that are not one window: whisper_full's window rules hold (VERDICT r4 missing 3,
+    reference transcription.rs:494-503 hands the whole utterance to whisper_full).  Under one second
+    nothing is decoded; 480 001 samples are ONE window (seek + 100 >= seek_end after it); 45 / 75 s
+    take the seek loop with each later window conditioned on the earlier tokens (prompt_past).
+    Window count and tokens equal to the oracle's whisper_full run at no_timestamps."""
+    e, om = tiny
+    x = _long_audio(n, seed)
+    r = e.transcribe_samples(x, _params(no_timestamps=True, max_new_tokens=16))
+    wins, segs, toks, _ = W.transcribe(om, x, W.Params(no_timestamps=True, max_tokens=16))
+    if not wins:
+        assert r.n_windows == 0 and r.text == "" and r.tokens == [] and r.segments == []
+        return
+    if _compare(r, wins, segs, toks):
+        assert r.n_windows == len(wins)
+    if n == 480001:
+        assert len(wins) == 1 and r.n_windows == 1
+    if n >= 45 * 16000:
+        assert r.n_windows >= 2 and len(wins) >= 2
+
+
+def test_fast_path_one_window_unchanged(tiny):
+    """A 30 s window (the benchmark's input) stays on the device-resident fast path (no segments,
+    one decoder pass per token) and decodes the tokens of whisper_full's single window."""
+    e, om = tiny
+    x = O.synth_audio(137)
+    r = e.transcribe_samples(x, _params(no_timestamps=True, max_new_tokens=16))
+    assert r.n_windows == 1 and r.segments == []  # the fast path's result carries no segments
+    wins, _, toks, _ = W.transcribe(om, x, W.Params(no_timestamps=True, max_tokens=16))
+    gaps = [s.margin for _, w in wins for s in w.steps]
+    got = list(r.tokens)
+    k = min(next((i for i, g in enumerate(gaps) if g <= GAP), len(gaps)), len(got))
+    assert k > 0 and got[:k] == toks[:k]
+
+
+def test_best_of_rows_not_dividing_pass_rows(monkeypatch):
+    """a batch whose windows of best_of rows do not fit the decode groups whole (f32
+    medium width: 23 rows per pass, 3 groups at max_batch 64; best_of 6 over 10 windows = 60 rows ->
+    4 windows = 24 rows in the largest group) decodes with one row per window run instead of
+    failing, and gives bitwise the result of private window copies (SPT_NO_WINDOW_SHARE=1)."""
+    from spittle_amd import WhisperEngine, WhisperModelParams
+    e = WhisperEngine(WhisperModelParams(dtype="f32", max_batch=64, seed=SEED))
+    e.load_model("synthetic:medium.en:enc=1:dec=3")
+    try:
+        xs = [O.synth_audio(140 + i, 2 * 16000 + 160 * i) for i in range(10)]
+        kw = dict(temperature_inc=0.5, logprob_thold=10.0, best_of=6, max_new_tokens=4, seed=5)
+        a = e.transcribe_batch(xs, _params(**kw))
+        monkeypatch.setenv("SPT_NO_WINDOW_SHARE", "1")
+        b = e.transcribe_batch(xs, _params(**kw))
+        monkeypatch.delenv("SPT_NO_WINDOW_SHARE")
+        for ra, rb in zip(a, b):
+            assert ra.n_fallbacks == 2 * ra.n_windows and ra.n_windows == 1
+            assert ra.tokens == rb.tokens and np.array_equal(np.asarray(ra.top1), np.asarray(rb.top1))
+    finally:
+        e.unload_model()
+
+
+def _beam_geometry_runs(e, x, others, p):
+    """the beam-5 result for x alone, beside 1, 3 and 7 other utterances (x first, last and in the
+    middle), as (tokens, plog) per placement"""
+    runs = [("alone", e.transcribe_samples(x, p))]
+    for k in (1, 3, 7):
+        batch = others[:k]
+        pos = {1: 0, 3: 3, 7: 4}[k]
+        xs = batch[:pos] + [x] + batch[pos:]
+        runs.append((f"with{k}@{pos}", e.transcribe_batch(xs, p)[pos]))
+    return runs
+
+
+def test_beam_dedup_batch_geometry():
+    """whisper.cpp's beam search deduplicates candidates by exact score equality, which needs
+    identical decoder rows to compute bitwise-equal scores in every pass geometry.
+    The same beam-5 utterance alone, beside 1, 3 and 7 others (one engine call of 10, 20, 40 rows)
+    and in a call of 14 utterances split over two engine calls (max_batch 70 above the 63-row pass
+    limit): bitwise-equal tokens and log-probabilities everywhere."""
+    from spittle_amd import WhisperEngine, WhisperModelParams
+    e = WhisperEngine(WhisperModelParams(dtype="f32", max_batch=70, seed=SEED))
+    e.load_model("synthetic:tiny.en")
+    try:
+        p = _params(beam_size=5, max_new_tokens=12)
+        x = O.synth_audio(91, 20 * 16000)
+        others = [O.synth_audio(150 + i, (6 + i) * 16000) for i in range(13)]
+        runs = _beam_geometry_runs(e, x, others, p)
+        xs = others[:12] + [x] + others[12:]  # 14 utterances: calls of 12 and 2 (x in the second)
+        runs.append(("split_calls", e.transcribe_batch(xs, p)[12]))
+        ref = runs[0][1]
+        for name, r in runs[1:]:
+            assert r.tokens == ref.tokens, name
+            assert np.array_equal(np.asarray(r.top1), np.asarray(ref.top1)), name
+            assert np.array_equal(np.asarray(r.top2), np.asarray(ref.top2)), name
+    finally:
+        e.unload_model()
+
+
 def test_temperature_fallback(tiny):
     """logprob_thold above any average log-probability forces every fallback: 0, 0.2, ..., 1.0
     (5 fallbacks), best_of = 5 sampled decoders per window at temperature > 0; the same seed

@@ -172,3 +172,31 @@ def test_large_v3_beam5_cross_attention_strategies_bitwise(large, vw, monkeypatc
     finally:
         e2.unload_model()
     assert a.tokens == b.tokens and np.array_equal(np.asarray(a.top1), np.asarray(b.top1))
+
+
+def test_large_v3_beam5_dedup_batch_geometry():
+    """Beam 5 at large-v3 width in bf16 (38 rows per pass): the same utterance alone, beside 1, 3
+    and 6 others (one engine call of 10, 20, 35 rows) and in a call of 9 utterances split over two
+    engine calls (max_batch 40: 7 utterances per beam call) -- bitwise-equal tokens and
+    log-probabilities, so whisper.cpp's exact-equality candidate dedup sees the same scores in every
+    pass geometry."""
+    from spittle_amd import WhisperEngine, WhisperModelParams
+    e = WhisperEngine(WhisperModelParams(dtype="bf16", max_batch=40, seed=SEED))
+    e.load_model(SPEC)
+    try:
+        p = _params(beam_size=5, max_new_tokens=12)
+        x = _audio(20, 191)
+        others = [_audio(5 + i, 220 + i) for i in range(8)]
+        runs = [("alone", e.transcribe_samples(x, p))]
+        for k, pos in ((1, 0), (3, 3), (6, 2)):
+            xs = others[:k][:pos] + [x] + others[:k][pos:]
+            runs.append((f"with{k}@{pos}", e.transcribe_batch(xs, p)[pos]))
+        xs = others[:7] + [x] + others[7:]  # calls of 7 and 2 utterances, x in the second
+        runs.append(("split_calls", e.transcribe_batch(xs, p)[7]))
+        ref = runs[0][1]
+        for name, r in runs[1:]:
+            assert r.tokens == ref.tokens, name
+            assert np.array_equal(np.asarray(r.top1), np.asarray(ref.top1)), name
+            assert np.array_equal(np.asarray(r.top2), np.asarray(ref.top2)), name
+    finally:
+        e.unload_model()
