@@ -271,8 +271,7 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
             for (int i = 0; i < 6; ++i) {
                 const int k = lane * 4 + 256 * i;
                 if (k < K) {
-                    const float p = v[i].x - mean, q = v[i].y - mean, u = v[i].z - mean, ww = v[i].w - mean;
-                    s2 += (p * p + q * q) + (u * u + ww * ww);
+                    s2 += ln_sq4(v[i], mean);
                 }
             }
             const float rstd = 1.0f / sqrtf(wave_sum(s2) / (float)K + 1e-5f);
@@ -283,10 +282,10 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
                     const float4 g = lnw_pre[i];
                     const float4 b = lnb_pre[i];
                     T* o = img + (size_t)r * lds_ld + k;
-                    o[0] = from_f<T>((v[i].x - mean) * rstd * g.x + b.x);
-                    o[1] = from_f<T>((v[i].y - mean) * rstd * g.y + b.y);
-                    o[2] = from_f<T>((v[i].z - mean) * rstd * g.z + b.z);
-                    o[3] = from_f<T>((v[i].w - mean) * rstd * g.w + b.w);
+                    o[0] = from_f<T>(ln_out(v[i].x, mean, rstd, g.x, b.x));
+                    o[1] = from_f<T>(ln_out(v[i].y, mean, rstd, g.y, b.y));
+                    o[2] = from_f<T>(ln_out(v[i].z, mean, rstd, g.z, b.z));
+                    o[3] = from_f<T>(ln_out(v[i].w, mean, rstd, g.w, b.w));
                 }
             }
         }

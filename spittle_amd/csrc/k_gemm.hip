@@ -30,6 +30,7 @@
 #include <set>
 #include <tuple>
 #include <type_traits>
+#include <vector>
 
 namespace spt {
 
@@ -275,7 +276,13 @@ constexpr int G2_LDS_ALL = 8 * 128 * (128 + 16) > G2_LDS ? 8 * 128 * (128 + 16) 
 // wave must have waited for a half-tile by the end of the phase two before its read, so the
 // waits become vmcnt(8) at the ends of P1 / P3 / P4 (4 half-tiles in flight; see the schedule
 // below).  The MFMA order per accumulator is unchanged: results are bitwise those of STG = false.
-template <int EPI, bool F16, bool STG = false>
+// RM: C rows per tile, 256 or 240.  M = 12000 (eight 30 s windows) is 50 tiles of 240 rows against
+// 46.9 of 256: the four encoder GEMMs then fill their last round of 256 CUs almost whole (qkv 750
+// tiles = 2.93 rounds, fc1 1000 = 3.91, out / fc2 250 = 0.98), and a 240-row tile does 15/16 of the
+// 256-row tile's work -- its last 16-row fragment row (waves 4-7, rows 240..255) is neither read
+// from LDS nor multiplied, and each SIMD runs one wave of each half, so the MFMA pipe time drops
+// with it.  Every C element is the same MFMA chain in either tile: results are bitwise equal.
+template <int EPI, bool F16, bool STG = false, int RM = 256>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -286,8 +293,10 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     const int tm = wg / nnt, tn = wg - tm * nnt;
-    const int m0 = tm * G2_BM, n0 = tn * G2_BN;
+    const int m0 = tm * RM, n0 = tn * G2_BN;
     const int bz = blockIdx.z;
+    // RM = 240: waves 4-7 skip their last fragment row (tile rows 240..255 belong to the next tile)
+    const bool skip7 = RM == 240 && wr == 1;
     const int Kc = g.K / g.ksplit;
     const bf16* A = (const bf16*)g.A + (size_t)bz * g.sA + (size_t)blockIdx.y * Kc;
     const bf16* W = (const bf16*)g.W + (size_t)blockIdx.y * Kc;
@@ -331,6 +340,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
         const SPT_LDS char* la = (const SPT_LDS char*)smem + buf * G2_BUF;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
+            if (rh == 1 && i == 3 && skip7) continue;
             const int r = wr * 128 + rh * 64 + 16 * i + fr;
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
@@ -364,7 +374,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
-                    if constexpr (F16)
+                    if (rh == 1 && i == 3 && skip7) continue;
+                    else if constexpr (F16)
                         acc[rh * 4 + i][ch * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
                             __builtin_bit_cast(f16x8, af[i][s]), __builtin_bit_cast(f16x8, bw[ch][j][s]),
                             acc[rh * 4 + i][ch * 2 + j], 0, 0, 0);
@@ -504,7 +515,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
             const int rl = it * RPI + rsub;
             const int row = m0 + wr * 128 + pass * PR + rl;
             const uint4 v = *(const uint4*)(wreg + rl * RS + ch * 16);
-            if (row >= g.M) continue;
+            if (row >= g.M || (RM < 256 && wr * 128 + pass * PR + rl >= RM)) continue;
             const int col = n0 + wc * 64 + ch * (16 / ESZ);
             if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_SWISH || EPI == EPI_BIAS_RELU) {
                 *(uint4*)((bf16*)g.C + (size_t)bz * g.sC + (size_t)row * g.ldc + col) = v;
@@ -603,6 +614,30 @@ void launch_skinny(const GemmArgs& g, hipStream_t st) {
     SPT_LAUNCH_CHECK();
 }
 
+int device_cus() {
+    static std::mutex m;
+    static std::vector<int> cache;
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(m);
+    if ((int)cache.size() <= dev) cache.resize(dev + 1, 0);
+    if (!cache[dev]) HIP_CHECK(hipDeviceGetAttribute(&cache[dev], hipDeviceAttributeMultiprocessorCount, dev));
+    return cache[dev];
+}
+
+// rows per tile: 240 where its rounds of one tile per CU times 15/16 of a tile's work beat 256's
+// (SPT_G2_ROWS = 256 / 240 forces one)
+int g2_rows(const GemmArgs& g, int batch) {
+    static const int force = getenv("SPT_G2_ROWS") ? atoi(getenv("SPT_G2_ROWS")) : 0;
+    if (force == 256 || force == 240) return force;
+    const int64_t cus = device_cus();
+    auto cost = [&](int rm) {
+        const int64_t tiles = (int64_t)cdiv(g.M, rm) * (g.N / G2_BN) * g.ksplit * batch;
+        return ((tiles + cus - 1) / cus) * rm;
+    };
+    return cost(240) < cost(256) ? 240 : 256;
+}
+
 template <int EPI, bool F16>
 void launch_256(const GemmArgs& g, int batch, hipStream_t st) {
     // staggered wave groups: bitwise-identical results, encoder 21.54 -> 21.28 ms (r2, two A/B pairs);
@@ -611,9 +646,17 @@ void launch_256(const GemmArgs& g, int batch, hipStream_t st) {
     // > 64 KiB dynamic LDS: per kernel and device (gemm_prepare sets them before any capture)
     ensure_lds_attr((const void*)gemm256_kernel<EPI, F16, false>, G2_LDS_ALL);
     ensure_lds_attr((const void*)gemm256_kernel<EPI, F16, true>, G2_LDS_ALL);
-    dim3 grid(cdiv(g.M, G2_BM) * (g.N / G2_BN), g.ksplit, batch);
-    if (stg) hipLaunchKernelGGL((gemm256_kernel<EPI, F16, true>), grid, dim3(512), G2_LDS_ALL, st, g);
-    else hipLaunchKernelGGL((gemm256_kernel<EPI, F16, false>), grid, dim3(512), G2_LDS_ALL, st, g);
+    ensure_lds_attr((const void*)gemm256_kernel<EPI, F16, false, 240>, G2_LDS_ALL);
+    ensure_lds_attr((const void*)gemm256_kernel<EPI, F16, true, 240>, G2_LDS_ALL);
+    const int rm = g2_rows(g, batch);
+    dim3 grid(cdiv(g.M, rm) * (g.N / G2_BN), g.ksplit, batch);
+    if (rm == 240) {
+        if (stg) hipLaunchKernelGGL((gemm256_kernel<EPI, F16, true, 240>), grid, dim3(512), G2_LDS_ALL, st, g);
+        else hipLaunchKernelGGL((gemm256_kernel<EPI, F16, false, 240>), grid, dim3(512), G2_LDS_ALL, st, g);
+    } else {
+        if (stg) hipLaunchKernelGGL((gemm256_kernel<EPI, F16, true>), grid, dim3(512), G2_LDS_ALL, st, g);
+        else hipLaunchKernelGGL((gemm256_kernel<EPI, F16, false>), grid, dim3(512), G2_LDS_ALL, st, g);
+    }
     SPT_LAUNCH_CHECK();
 }
 
@@ -662,6 +705,10 @@ void prepare_epi() {
     ensure_lds_attr((const void*)gemm256_kernel<EPI, false, true>, G2_LDS_ALL);
     ensure_lds_attr((const void*)gemm256_kernel<EPI, true, false>, G2_LDS_ALL);
     ensure_lds_attr((const void*)gemm256_kernel<EPI, true, true>, G2_LDS_ALL);
+    ensure_lds_attr((const void*)gemm256_kernel<EPI, false, false, 240>, G2_LDS_ALL);
+    ensure_lds_attr((const void*)gemm256_kernel<EPI, false, true, 240>, G2_LDS_ALL);
+    ensure_lds_attr((const void*)gemm256_kernel<EPI, true, false, 240>, G2_LDS_ALL);
+    ensure_lds_attr((const void*)gemm256_kernel<EPI, true, true, 240>, G2_LDS_ALL);
     ensure_lds_attr((const void*)gemm_nt_kernel<bf16, EPI, 3>, 3 * 2 * BM * SLAB);
     ensure_lds_attr((const void*)gemm_nt_kernel<f16, EPI, 3>, 3 * 2 * BM * SLAB);
     ensure_lds_attr((const void*)gemm_nt_kernel<float, EPI, 3>, 3 * 2 * BM * SLAB);

@@ -345,8 +345,7 @@ __device__ __forceinline__ bool gather_ln(const PdArgs& a, __amdgpu_buffer_rsrc_
         for (int i = 0; i < NC; ++i) {
             const int k = lane * 4 + 256 * i;
             if (k < K) {
-                const float p = v[i].x - mean, q = v[i].y - mean, u = v[i].z - mean, ww = v[i].w - mean;
-                s2 += (p * p + q * q) + (u * u + ww * ww);
+                s2 += ln_sq4(v[i], mean);
             }
         }
         const float rstd = 1.0f / sqrtf(wave_sum(s2) / (float)K + 1e-5f);
@@ -357,10 +356,10 @@ __device__ __forceinline__ bool gather_ln(const PdArgs& a, __amdgpu_buffer_rsrc_
                 const float4 g = lnw_pre[i];
                 const float4 b = lnb_pre[i];
                 bf16* o = img + (size_t)r * ld + k;
-                o[0] = from_f<bf16>((v[i].x - mean) * rstd * g.x + b.x);
-                o[1] = from_f<bf16>((v[i].y - mean) * rstd * g.y + b.y);
-                o[2] = from_f<bf16>((v[i].z - mean) * rstd * g.z + b.z);
-                o[3] = from_f<bf16>((v[i].w - mean) * rstd * g.w + b.w);
+                o[0] = from_f<bf16>(ln_out(v[i].x, mean, rstd, g.x, b.x));
+                o[1] = from_f<bf16>(ln_out(v[i].y, mean, rstd, g.y, b.y));
+                o[2] = from_f<bf16>(ln_out(v[i].z, mean, rstd, g.z, b.z));
+                o[3] = from_f<bf16>(ln_out(v[i].w, mean, rstd, g.w, b.w));
             }
         }
     }
@@ -469,7 +468,7 @@ struct Smem {
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t gran_rsrc(const PdArgs& a) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)a.gran, (short)0, (int)(a.R * (8 * a.d + 528 * a.H) * 8), 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)a.gran, (short)0, (int)(a.R * (9 * a.d + 528 * a.H) * 8), 0x00020000);
 }
 
 // waves 0-3: per unit, its inputs into LDS; the barriers of compute_loop (A, [E: mid], B); then
@@ -902,7 +901,7 @@ int cu_count(int dev) {
 
 }  // namespace
 
-int64_t pdec_granules(int R, int d, int H) { return (int64_t)R * (8 * (int64_t)d + 528 * (int64_t)H); }
+int64_t pdec_granules(int R, int d, int H) { return (int64_t)R * (9 * (int64_t)d + 528 * (int64_t)H); }
 
 std::string pdec_unsupported(int dtype, int d, int H, int R, int ctx, int T_enc) {
     if (dtype != DT_BF16) return "bf16 models only";

@@ -207,10 +207,10 @@ def test_beam_dedup_batch_geometry():
     """whisper.cpp's beam search deduplicates candidates by exact score equality, which needs
     identical decoder rows to compute bitwise-equal scores in every pass geometry.
     The same beam-5 utterance alone, beside 1, 3 and 7 others (one engine call of 10, 20, 40 rows)
-    and in a call of 14 utterances split over two engine calls (max_batch 70 above the 63-row pass
-    limit): bitwise-equal tokens and log-probabilities everywhere."""
+    and in a call of 14 utterances split over two engine calls (max_batch 64: 12 beam-5 utterances
+    per call): bitwise-equal tokens and log-probabilities everywhere."""
     from spittle_amd import WhisperEngine, WhisperModelParams
-    e = WhisperEngine(WhisperModelParams(dtype="f32", max_batch=70, seed=SEED))
+    e = WhisperEngine(WhisperModelParams(dtype="f32", max_batch=64, seed=SEED))
     e.load_model("synthetic:tiny.en")
     try:
         p = _params(beam_size=5, max_new_tokens=12)
