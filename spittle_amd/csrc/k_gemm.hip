@@ -63,11 +63,28 @@ __device__ __forceinline__ EpiCol epi_col(const GemmArgs& g, int col) {
     }
     return e;
 }
+// the residual / positional operand of one output element (the f32 epilogues that read one)
+template <int EPI>
+constexpr bool epi_reads_y() { return EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU_POS; }
+template <int EPI>
+__device__ __forceinline__ float epi_y(const GemmArgs& g, int bz, int row, const EpiCol& e) {
+    if constexpr (EPI == EPI_BIAS_RESID) return ((const float*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col];
+    else if constexpr (EPI == EPI_BIAS_GELU_POS) return g.pos[(size_t)row * g.N + e.col];
+    else return 0.0f;
+}
+// Every epilogue load (bias columns, residual / positional operands) is issued before the first
+// store and waited for here, once.  Left to the compiler, each row-guarded store waited with
+// vmcnt(0) -- for its bias value along the paths that skipped the earlier guarded blocks, and so
+// for every earlier store too (vmcnt counts stores in order): the stores of a tile went one
+// round trip at a time.
+__device__ __forceinline__ void epi_loads_landed() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
+
 // No contraction here: the residual / positional add is a separate rounding after the scaled
 // (or GELU'd) product, as in the 256 x 256 tile's LDS-staged epilogue, so every tile writes the same
-// bits (a fused alpha * v + C differed in the last bit: r3, single-window Whisper encoder)
+// bits (a fused alpha * v + C differed in the last bit: r3, single-window Whisper encoder).
+// y: epi_y of the element (loaded before any store)
 template <typename T, int EPI>
-__device__ __forceinline__ void epi_store(const GemmArgs& g, int bz, int row, const EpiCol& e, float acc) {
+__device__ __forceinline__ void epi_store(const GemmArgs& g, int bz, int row, const EpiCol& e, float acc, float y = 0.0f) {
 #pragma clang fp contract(off)
     const float v = acc + e.bv;
     if constexpr (EPI == EPI_BIAS) {
@@ -83,9 +100,9 @@ __device__ __forceinline__ void epi_store(const GemmArgs& g, int bz, int row, co
     } else if constexpr (EPI == EPI_BIAS_GELU) {
         ((T*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col] = from_f<T>(gelu_tanh(v));
     } else if constexpr (EPI == EPI_BIAS_GELU_POS) {
-        ((float*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col] = gelu_tanh(v) + g.pos[(size_t)row * g.N + e.col];
+        ((float*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col] = gelu_tanh(v) + y;
     } else if constexpr (EPI == EPI_BIAS_RESID) {
-        ((float*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col] += g.alpha * v;
+        ((float*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + e.col] = y + g.alpha * v;
     } else if constexpr (EPI == EPI_KVSPLIT) {
         const int bb = row / g.kv_T, t = row - bb * g.kv_T;
         ((T*)g.C)[kv_offset(e.l, e.kvi, bb, e.h, t, e.el, g.kv_B, g.kv_H, g.kv_T)] = from_f<T>(v);
@@ -230,17 +247,29 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256,
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing repeat slabs land before exit
 
     // ---------------------------------------------------------------- epilogue
+    EpiCol ec[NJ];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-        const EpiCol ec = epi_col<EPI>(g, n0 + wn * (BNT / 2) + 16 * j + fr);
+    for (int j = 0; j < NJ; ++j) ec[j] = epi_col<EPI>(g, n0 + wn * (BNT / 2) + 16 * j + fr);
+    float y[epi_reads_y<EPI>() ? MI : 1][NJ][4];
+    if constexpr (epi_reads_y<EPI>()) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    y[i][j][r] = epi_y<EPI>(g, bz, min(m0 + wm * (BMT / 2) + 16 * i + 4 * fq + r, g.M - 1), ec[j]);
+    }
+    epi_loads_landed();
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = m0 + wm * (BMT / 2) + 16 * i + 4 * fq + r;
-                if (row < g.M) epi_store<T, EPI>(g, bz, row, ec, acc[i][j][r]);
+                if (row < g.M) epi_store<T, EPI>(g, bz, row, ec[j], acc[i][j][r], y[epi_reads_y<EPI>() ? i : 0][j][r]);
             }
-    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -542,6 +571,168 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Ring GEMM for a few hundred rows (Parakeet's streaming pass: 64 one-second windows, M = 832).
+// There every tile shape is one round of workgroups with 16 K-steps, and the 64 x 64 tile's cost
+// is what each CU takes in: 3.25 workgroups x (64 + 64) rows x K x 2 B = 852 KB per CU at K = 1024,
+// ~56 GB/s.  Here one workgroup per CU owns a 208-row x 64-column tile (557 KB at K = 1024) and
+// splits its waves by role (MI355X_MICROARCH.md, ring-gemm):
+//   waves 4-7 (loaders): LDS-DMA the tile's 272 slab rows (208 A + 64 W, 128 B = one 64-deep K-step
+//     each) into a 4-slot ring, two K-steps in flight, and publish a slot with a FULL word once
+//     their own DMA into it has landed (counted vmcnt);
+//   waves 0-3 (consumers, one per SIMD): all 13 row fragments x one 16-column fragment each; read a
+//     slot's fragments as two 32-deep halves, the next half's reads in flight under the current
+//     half's 13 MFMAs, and hand the slot back with a FREE word once both halves are in registers.
+// No barrier inside the K loop: a loader waits only for the four FREE words of the slot it refills,
+// a consumer only for the four FULL words of the slot it reads.  Every C element is the same
+// v_mfma_f32_16x16x32 chain over K as in the other tiles (k-step order, lane group fq = k chunk),
+// so the results are bitwise those of the 64 x 64 tile at the same split.
+constexpr int RG_RF = 13, RG_RT = 16 * RG_RF, RG_CT = 64;  // tile: 208 rows x 64 columns
+constexpr int RG_NS = 4, RG_D = 2;                          // ring slots, K-steps in flight per loader
+constexpr int RG_ROWS = RG_RT + RG_CT;                      // 272 slab rows per slot
+constexpr int RG_SLOT = RG_ROWS * SLAB;                     // 34,816 B
+constexpr int RG_NI = (RG_ROWS / 8 + 3) / 4;                // 9 DMA instructions per loader wave per slot
+constexpr int RG_LDS = RG_NS * RG_SLOT + 2 * RG_NS * 4 * 4; // + FULL [slot][loader], FREE [slot][consumer]
+static_assert(RG_NI == 9, "the loader's counted waits below assume 9 instructions per slot");
+
+__device__ __forceinline__ void rg_wait(const SPT_LDS int* w, int target) {
+    while (true) {
+        const int a = *(volatile const SPT_LDS int*)(w + 0), b = *(volatile const SPT_LDS int*)(w + 1);
+        const int c = *(volatile const SPT_LDS int*)(w + 2), d = *(volatile const SPT_LDS int*)(w + 3);
+        if (min(min(a, b), min(c, d)) >= target) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    asm volatile("" ::: "memory");  // no slot read moves above the wait
+}
+__device__ __forceinline__ void rg_post(SPT_LDS int* w, int v) {
+    asm volatile("" ::: "memory");
+    *(volatile SPT_LDS int*)w = v;
+}
+
+template <typename T, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    SPT_LDS char* lds = (SPT_LDS char*)smem;
+    SPT_LDS int* full = (SPT_LDS int*)(lds + RG_NS * RG_SLOT);  // [slot][loader wave]
+    SPT_LDS int* freew = full + RG_NS * 4;                       // [slot][consumer wave]
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // bijective XCD-aware remap; row blocks fastest, so the workgroups streaming the same W
+    // columns are neighbours in one XCD's run (share its L2)
+    const int nrb = cdiv(g.M, RG_RT);
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const int tn = wg / nrb, tm = wg - tn * nrb;
+    const int m0 = tm * RG_RT, n0 = tn * RG_CT;
+    const int bz = blockIdx.z;
+    const int Kc = g.K / g.ksplit;
+    const T* A = (const T*)g.A + (size_t)bz * g.sA + (size_t)blockIdx.y * Kc;
+    const T* W = (const T*)g.W + (size_t)blockIdx.y * Kc;
+    const int nkt = Kc * (int)sizeof(T) / SLAB;
+    if (tid < 2 * RG_NS * 4) full[tid] = 0;  // FULL and FREE words are contiguous
+    __syncthreads();
+
+    if (wid >= 4) {
+        // ------------------------------------------------------------ loaders
+        const int lw = wid - 4, prow = lane >> 3, pch = lane & 7;
+        const char* src[RG_NI];
+        int dst[RG_NI];
+#pragma unroll
+        for (int i = 0; i < RG_NI; ++i) {
+            // 34 instructions of 8 rows per slot over 4 waves; the two spare issues repeat the last
+            // group (same bytes to the same LDS, landed before their wave's FULL word like the rest)
+            const int j = min(lw + 4 * i, RG_ROWS / 8 - 1);
+            const int r = 8 * j + prow;
+            const int c = (pch ^ swz(r)) << 4;
+            src[i] = r < RG_RT ? (const char*)(A + (size_t)min(m0 + r, g.M - 1) * g.lda) + c
+                               : (const char*)(W + (size_t)(n0 + r - RG_RT) * g.ldw) + c;
+            dst[i] = 8 * j * SLAB;
+        }
+        for (int k = 0; k < nkt; ++k) {
+            const int s = k % RG_NS;
+            if (k >= RG_NS) rg_wait(freew + 4 * s, k - RG_NS + 1);  // the slot's last occupant is in registers
+            const size_t ko = (size_t)k * SLAB;
+#pragma unroll
+            for (int i = 0; i < RG_NI; ++i)
+                __builtin_amdgcn_global_load_lds((const void*)(src[i] + ko), (SPT_LDS void*)(lds + s * RG_SLOT + dst[i]), 16, 0, 0);
+            if (k >= RG_D) {
+                asm volatile("s_waitcnt vmcnt(18)" ::: "memory");  // K-step k - 2 landed (RG_NI * RG_D younger)
+                rg_post(full + 4 * ((k - RG_D) % RG_NS) + lw, k - RG_D + 1);
+            }
+        }
+        if (nkt >= 2) {
+            asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+            rg_post(full + 4 * ((nkt - 2) % RG_NS) + lw, nkt - 1);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        rg_post(full + 4 * ((nkt - 1) % RG_NS) + lw, nkt);
+        return;
+    }
+
+    // ---------------------------------------------------------------- consumers
+    const int cw = wid, fr = lane & 15, fq = lane >> 4;
+    f32x4 acc[RG_RF];
+#pragma unroll
+    for (int i = 0; i < RG_RF; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 fa0[RG_RF], fa1[RG_RF], fw0, fw1;
+    auto rd = [&](int s, int half, bf16x8 (&a)[RG_RF], bf16x8& w) {
+        const SPT_LDS char* sl = lds + s * RG_SLOT;
+        const int c = 4 * half + fq;
+#pragma unroll
+        for (int i = 0; i < RG_RF; ++i) {
+            const int r = 16 * i + fr;
+            a[i] = *(const SPT_LDS bf16x8*)(sl + r * SLAB + ((c ^ swz(r)) << 4));
+        }
+        const int r = RG_RT + 16 * cw + fr;
+        w = *(const SPT_LDS bf16x8*)(sl + r * SLAB + ((c ^ swz(r)) << 4));
+    };
+    auto mm = [&](const bf16x8 (&a)[RG_RF], const bf16x8& w) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < RG_RF; ++i) {
+            if constexpr (TypeTag<T>::id == 2)
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a[i]), __builtin_bit_cast(f16x8, w),
+                                                                acc[i], 0, 0, 0);
+            else
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], w, acc[i], 0, 0, 0);
+        }
+        __builtin_amdgcn_s_setprio(0);
+    };
+    // Straight-line LDS traffic in the loop (the FREE word written by every lane, the next slot's
+    // first half read even after the last K-step: unused) so the compiler's lgkmcnt waits before
+    // the MFMAs stay counted instead of draining to 0 at a merge
+    rg_wait(full, 1);
+    rd(0, 0, fa0, fw0);
+    for (int k = 0; k < nkt; ++k) {
+        const int s = k % RG_NS;
+        rd(s, 1, fa1, fw1);
+        mm(fa0, fw0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // both halves of slot s are in registers
+        rg_post(freew + 4 * s + cw, k + 1);
+        if (k + 1 < nkt) rg_wait(full + 4 * ((k + 1) % RG_NS), k + 2);
+        rd((k + 1) % RG_NS, 0, fa0, fw0);
+        mm(fa1, fw1);
+    }
+
+    // ---------------------------------------------------------------- epilogue
+    const EpiCol ec = epi_col<EPI>(g, n0 + 16 * cw + fr);
+    float y[epi_reads_y<EPI>() ? RG_RF : 1][4];
+    if constexpr (epi_reads_y<EPI>()) {
+#pragma unroll
+        for (int i = 0; i < RG_RF; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) y[i][r] = epi_y<EPI>(g, bz, min(m0 + 16 * i + 4 * fq + r, g.M - 1), ec);
+    }
+    epi_loads_landed();
+#pragma unroll
+    for (int i = 0; i < RG_RF; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = m0 + 16 * i + 4 * fq + r;
+            if (row < g.M) epi_store<T, EPI>(g, bz, row, ec, acc[i][r], y[epi_reads_y<EPI>() ? i : 0][r]);
+        }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Skinny GEMM (M <= 64 rows: a short streaming window, one utterance): the weight stream is the
 // whole cost, so the grid spreads W over >= 256 workgroups -- a workgroup owns 16 columns and a
 // K range (split-K over grid.y for the EPI_PARTIAL residual products), its 4 waves split that
@@ -593,11 +784,20 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs g) {
         for (int r = 0; r < 4; ++r) red[wid][mt * 16 + 4 * fq + r][fr] = acc[mt][r];
     __syncthreads();
     typedef typename std::conditional<F16, f16, bf16>::type T;
-    for (int e = threadIdx.x; e < MT * 16 * 16; e += 256) {
-        const int row = e >> 4, c = e & 15;
+    // element e = threadIdx.x + 256 u: row (threadIdx.x >> 4) + 16 u, column threadIdx.x & 15
+    const int c = threadIdx.x & 15;
+    const EpiCol ec = epi_col<EPI>(g, n0 + c);
+    float y[MT];
+#pragma unroll
+    for (int u = 0; u < MT; ++u)
+        y[u] = epi_reads_y<EPI>() ? epi_y<EPI>(g, 0, min((int)(threadIdx.x >> 4) + 16 * u, g.M - 1), ec) : 0.0f;
+    epi_loads_landed();
+#pragma unroll
+    for (int u = 0; u < MT; ++u) {
+        const int row = (threadIdx.x >> 4) + 16 * u;
         if (row >= g.M) continue;
         const float v = red[0][row][c] + red[1][row][c] + red[2][row][c] + red[3][row][c];
-        epi_store<T, EPI>(g, 0, row, epi_col<EPI>(g, n0 + c), v);
+        epi_store<T, EPI>(g, 0, row, ec, v, y[u]);
     }
 }
 
@@ -689,7 +889,19 @@ void launch_small(const GemmArgs& g0, int batch, hipStream_t st) {  // 64 x 128 
 }
 
 template <typename T, int EPI>
+void launch_ring(const GemmArgs& g, int batch, hipStream_t st) {
+    if constexpr (sizeof(T) == 2) {
+        ensure_lds_attr((const void*)gemm_ring_kernel<T, EPI>, RG_LDS);
+        dim3 grid(cdiv(g.M, RG_RT) * (g.N / RG_CT), g.ksplit, batch);
+        hipLaunchKernelGGL((gemm_ring_kernel<T, EPI>), grid, dim3(512), RG_LDS, st, g);
+    } else {
+        throw std::runtime_error("gemm_nt: the ring variant needs a 16-bit dtype");
+    }
+}
+
+template <typename T, int EPI>
 void launch_t(const GemmArgs& g, int batch, int variant, hipStream_t st) {
+    if (variant == 6) return launch_ring<T, EPI>(g, batch, st);
     if (variant == 4) return launch_small<T, EPI, 64, 128>(g, batch, st);
     if (variant == 5) return launch_small<T, EPI, 64, 64>(g, batch, st);
     switch (nt_stages()) {
@@ -709,6 +921,8 @@ void prepare_epi() {
     ensure_lds_attr((const void*)gemm256_kernel<EPI, false, true, 240>, G2_LDS_ALL);
     ensure_lds_attr((const void*)gemm256_kernel<EPI, true, false, 240>, G2_LDS_ALL);
     ensure_lds_attr((const void*)gemm256_kernel<EPI, true, true, 240>, G2_LDS_ALL);
+    ensure_lds_attr((const void*)gemm_ring_kernel<bf16, EPI>, RG_LDS);
+    ensure_lds_attr((const void*)gemm_ring_kernel<f16, EPI>, RG_LDS);
     ensure_lds_attr((const void*)gemm_nt_kernel<bf16, EPI, 3>, 3 * 2 * BM * SLAB);
     ensure_lds_attr((const void*)gemm_nt_kernel<f16, EPI, 3>, 3 * 2 * BM * SLAB);
     ensure_lds_attr((const void*)gemm_nt_kernel<float, EPI, 3>, 3 * 2 * BM * SLAB);
@@ -748,7 +962,9 @@ void gemm_nt_variant(int dtype, int epi, const GemmArgs& g, int batch, int varia
     const int esz = dtype == DT_F32 ? 4 : 2;
     if (g.ksplit < 1 || g.K % g.ksplit || (g.ksplit > 1 && epi != EPI_PARTIAL))
         throw std::runtime_error("gemm_nt: split-K needs EPI_PARTIAL and K % ksplit == 0");
-    if (variant != 3 && (g.N % (variant == 5 ? 64 : BN) != 0 || (g.K / g.ksplit * esz) % SLAB != 0 || g.M <= 0))
+    if (variant == 6 && (dtype == DT_F32 || g.N % RG_CT != 0 || (g.K / g.ksplit) % 64 != 0 || g.M <= 0))
+        throw std::runtime_error("gemm_nt: the ring variant needs a 16-bit dtype, N % 64, (K / ksplit) % 64");
+    if (variant != 3 && variant != 6 && (g.N % (variant == 5 ? 64 : BN) != 0 || (g.K / g.ksplit * esz) % SLAB != 0 || g.M <= 0))
         throw std::runtime_error("gemm_nt: unsupported shape M=" + std::to_string(g.M) + " N=" +
                                  std::to_string(g.N) + " K=" + std::to_string(g.K));
 #define SPT_GEMM_CASES(T)                                                          \

@@ -43,6 +43,7 @@ void gemm_nt(int dtype, int epi, const GemmArgs& g, int batch, hipStream_t st);
 // 3: skinny (M <= 64, 16-bit dtypes: 16 columns per workgroup, the weight stream spread over the grid)
 // 4: 64 x 128 tile (16-bit or f32; small M: two workgroups per CU where the 128-row tile gives one)
 // 5: 64 x 64 tile (N % 64; up to four workgroups per CU)
+// 6: ring (16-bit, N % 64: 208 x 64 tile, one workgroup per CU, loader / consumer waves; M of a few hundred)
 // sets the > 64 KiB dynamic-LDS attribute of every GEMM kernel on the current device (engine
 // constructors call it before any stream capture; launches check it too)
 void gemm_prepare();
