@@ -175,9 +175,11 @@ KERNEL_NAMES = {
 
 
 def roofline(eng, iters: int = 50):
-    """Dominant-kernel roofline from HIP events on the engine stream (spt_probe_kernel: the
-    kernel re-launched on the buffers of the last timed call; decoder kernels one launch at a
-    time behind a 512 MB cache-evicting read, as in the decode loop).
+    """Dominant-kernel roofline from HIP events on the engine's streams (spt_probe_kernel, on the
+    buffers of the last timed call, in situ: decoder kernels inside eager one-token passes over
+    all layers with an event pair around the probed kernel of each layer, or around the logits
+    launch after them; encoder kernels right behind their producer from the encoder sequence --
+    LayerNorm 2 before fc1, the q/k/v GEMM before the attention).
     achieved = algorithmic bytes (or flops) per launch / average launch duration.
     traffic = PMC-measured HBM bytes per launch of the same kernel, from the committed
     rocprofv3 --pmc summary (profiles/pmc_<kernel>.json), when present."""

@@ -131,7 +131,8 @@ typedef struct {
     int64_t workspace_bytes;
 } spt_model_info;
 
-/* per-phase device time of the last call, from HIP events on the engine stream */
+/* per-phase device time of the last call, from HIP events on the engine stream; total_ms = the
+ * sum of the phases */
 typedef struct {
     double mel_ms, encoder_ms, cross_kv_ms, decode_ms, total_ms, h2d_ms;
     int32_t n_decode_passes;
@@ -185,11 +186,14 @@ spt_status spt_get_timings(const spt_ctx* ctx, spt_timings* t);
  * own reflective head, the utterance's global max - 8 clamp) and encodes each 30 s window at
  * `seek` once (whisper_encode_internal), shared by every temperature fallback and by the
  * utterance's beam / best_of decoders: encoder_windows counts those encoder runs.
- * ABI 12: one-token decoder passes of up to 8 rows run every decoder layer as ONE persistent
- * launch (bitwise the per-stage launch chain); pd_passes counts them.  It needs every CU: when
- * another context's or process's kernels hold some, the pass gives up and the call is re-run on
- * the launch chain (pd_fallbacks; the result is the same).  SPT_PERSISTENT=0 in the environment
- * (read when a context is created) keeps the launch chain. */
+ * ABI 12: opt-in (SPT_PERSISTENT=1 in the environment, read when a context is created): one-token
+ * decoder passes of up to 8 rows run every decoder layer as ONE persistent launch (bitwise the
+ * per-stage launch chain, measured slower: DESIGN.md 4.1f); pd_passes counts them.  It needs every
+ * CU: when another context's or process's kernels hold some, the pass gives up and the call is
+ * re-run on the launch chain (pd_fallbacks; the result is the same).  Default: the launch chain,
+ * both counters 0.
+ * device_ms (and spt_timings.total_ms) sum the stage intervals (mel, window norm, encoder, cross
+ * K/V, decode); host time between the stages is not in them. */
 typedef struct {
     int32_t engine_calls;     /* decoder runs (a prompt pass + its steps; ABI <= 10: each with its own
                                  mel + encoder + cross K/V) */

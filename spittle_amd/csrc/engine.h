@@ -223,9 +223,10 @@ private:
                       bool blank);
 
     // the persistent decoder pass (k_pdec.hip): one launch for every layer of a one-token pass of at
-    // most 8 rows in one decode group.  SPT_PERSISTENT=0 keeps the launch chain (A/B measurements).
+    // most 8 rows in one decode group, bitwise the launch chain but measured 1.35-1.82x slower
+    // (DESIGN.md 4.1f): opt-in, SPT_PERSISTENT=1.
     bool pd_able_ = false;       // this model / dtype / batch geometry can run it
-    bool pd_env_ = false;        // SPT_PERSISTENT=1 (default off until validated on the GPU)
+    bool pd_env_ = false;        // SPT_PERSISTENT=1
     bool pd_active_ = false;     // this call's one-token passes run it (set per run_decode)
     bool pd_fallback_ = false;   // re-running a call whose persistent pass gave up (the chain instead)
     PdLayer* pd_layers_ = nullptr;  // device copy of the decoder layers' pointers
@@ -242,6 +243,10 @@ private:
     int max_rows_ = 64;  // decoder rows per pass (gemv_max_image_rows); larger batches use more groups  // SPT_DECODE_GROUPS=2 splits the batch over two streams
     hipStream_t st_ = nullptr;
     std::vector<hipEvent_t> ev_;
+    // probe(): the decoder kernel kind timed in situ by an eager enqueue_layers (-1: none), and
+    // its event pair per layer
+    int probe_kind_ = -1;
+    std::vector<hipEvent_t> probe_ev_;
 
     // ---- weights (one arena)
     char* warena_ = nullptr;

@@ -203,10 +203,15 @@ __device__ __forceinline__ int kswz(int r) { return (SW & 1) ? ((r >> 1) & 7) : 
 template <int SW>
 __device__ __forceinline__ int vswz(int r) { return (SW & 2) ? ((r & 2) << 1) : 0; }
 
-template <int SUM, int SW = 1>  // row sums: 0 packed f32 VALU, 1 scalar f32 VALU, 2 an MFMA with a ones operand
+// QL: the wave's Q fragments (2 query blocks x 4 k-steps, 32 VGPRs) live in LDS ([8][64 lanes] x 16 B
+// per wave, lane-linear: conflict-free ds_read_b128) and are re-read at the start of every tile.
+// Held in registers for the whole kernel they pushed it past 256 VGPRs at two waves per SIMD: 16
+// spilled, and the loop reloaded K/V stage addresses and Q pieces from scratch on every tile (r5).
+template <int SUM, int SW = 1, bool QL = false>  // row sums: 0 packed f32 VALU, 1 scalar f32 VALU, 2 an MFMA with a ones operand
 __global__ __launch_bounds__(256, 2) void attn_bf16_q64_kernel(const bf16* __restrict__ qkv, int T, int H,
                                                                bf16* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128];  // [buf][K|V][64 keys][128 B]
+    // [buf][K|V][64 keys][128 B] (+ QL: [wave][qb * 4 + s][lane] x 16 B)
+    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128 + (QL ? 4 * 8 * 64 * 16 : 0)];
     const int d = H * 64, ld = 3 * d;
     const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -226,6 +231,13 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_q64_kernel(const bf16* __res
 #pragma unroll
                 for (int e = 0; e < 8; ++e) qf[qb][s][e] = (short)f2bf(bf2f((bf16)qf[qb][s][e]) * kScaleLog2);
         }
+    }
+    SPT_LDS bf16x8* qlds = (SPT_LDS bf16x8*)(smem + 2 * 2 * 64 * 128) + wid * 8 * 64;
+    if constexpr (QL) {  // this wave's own region: its later reads follow these writes in LDS order
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) qlds[(qb * 4 + s) * 64 + lane] = qf[qb][s];
     }
 
     auto lds_k = [&](int buf) -> SPT_LDS char* { return (SPT_LDS char*)smem + (buf * 2 + 0) * 8192; };
@@ -271,6 +283,17 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_q64_kernel(const bf16* __res
         const SPT_LDS char* lk = lds_k(cur);
         const SPT_LDS char* lv = lds_v(cur);
         f32x16 s[2][2];
+        bf16x8 qt[QL ? 2 : 1][4];
+        if constexpr (QL) {
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+                for (int st = 0; st < 4; ++st) qt[qb][st] = qlds[(qb * 4 + st) * 64 + lane];
+        }
+        auto qfrag = [&](int qb, int st) -> const bf16x8& {
+            if constexpr (QL) return qt[qb][st];
+            else return qf[qb][st];
+        };
 #pragma unroll
         for (int kt2 = 0; kt2 < 2; ++kt2) {
             // SUM == 4: the accumulator starts at -m (the query's running maximum, log2 units, a
@@ -282,8 +305,8 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_q64_kernel(const bf16* __res
             for (int st = 0; st < 4; ++st) {
                 const int c = 2 * st + hf;
                 const bf16x8 a = *(const SPT_LDS bf16x8*)(lk + row * 128 + ((c ^ kswz<SW>(row)) << 4));
-                s[0][kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[0][st], st == 0 ? cinit[0] : s[0][kt2], 0, 0, 0);
-                s[1][kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[1][st], st == 0 ? cinit[1] : s[1][kt2], 0, 0, 0);
+                s[0][kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qfrag(0, st), st == 0 ? cinit[0] : s[0][kt2], 0, 0, 0);
+                s[1][kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qfrag(1, st), st == 0 ? cinit[1] : s[1][kt2], 0, 0, 0);
             }
         }
         if (kt * 64 + 64 > T) {
@@ -635,13 +658,19 @@ __global__ __launch_bounds__(256, 1) void attn_f32_kernel(const float* __restric
 
 void enc_attention(int dtype, const void* qkv, int B, int T, int H, void* out, hipStream_t st) {
     static const bool q32 = getenv("SPT_ATTN_Q32") != nullptr;  // A/B switch: 32 queries per wave
-    static const int sum = getenv("SPT_ATTN_SUM") ? atoi(getenv("SPT_ATTN_SUM")) : 4;  // 4: scores relative to the running max (r4: 133 -> 127 us); 3: r2-r3 optimistic softmax
+    // 4: scores relative to the running max (r4: 133 -> 127 us); 3: r2-r3 optimistic softmax.  Read per
+    // launch (eager runs: debug_encode; a captured encoder keeps its variant) so a test can compare them
+    const char* sum_env = getenv("SPT_ATTN_SUM");
+    const int sum = sum_env ? atoi(sum_env) : 4;
+    const char* ql_env = getenv("SPT_ATTN_QL");  // Q fragments in LDS (default; 0: in registers, r4)
+    const bool ql = !(ql_env && atoi(ql_env) == 0);
     static const int swz = getenv("SPT_ATTN_SWZ") ? atoi(getenv("SPT_ATTN_SWZ")) : 1;
     if (dtype == DT_BF16 && !q32) {
         dim3 g(cdiv(T, 256), H, B);
         if (sum == 1) hipLaunchKernelGGL(attn_bf16_q64_kernel<1>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
         else if (sum == 2) hipLaunchKernelGGL(attn_bf16_q64_kernel<2>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
         else if (sum == 3 && swz == 3) hipLaunchKernelGGL((attn_bf16_q64_kernel<3, 3>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
+        else if (sum == 4 && ql) hipLaunchKernelGGL((attn_bf16_q64_kernel<4, 1, true>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
         else if (sum == 4) hipLaunchKernelGGL(attn_bf16_q64_kernel<4>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
         else if (sum == 3) hipLaunchKernelGGL(attn_bf16_q64_kernel<3>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
         else if (swz == 0) hipLaunchKernelGGL((attn_bf16_q64_kernel<0, 0>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);

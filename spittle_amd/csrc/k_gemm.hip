@@ -814,28 +814,16 @@ void launch_skinny(const GemmArgs& g, hipStream_t st) {
     SPT_LAUNCH_CHECK();
 }
 
-int device_cus() {
-    static std::mutex m;
-    static std::vector<int> cache;
-    int dev = 0;
-    HIP_CHECK(hipGetDevice(&dev));
-    std::lock_guard<std::mutex> lk(m);
-    if ((int)cache.size() <= dev) cache.resize(dev + 1, 0);
-    if (!cache[dev]) HIP_CHECK(hipDeviceGetAttribute(&cache[dev], hipDeviceAttributeMultiprocessorCount, dev));
-    return cache[dev];
-}
-
-// rows per tile: 240 where its rounds of one tile per CU times 15/16 of a tile's work beat 256's
-// (SPT_G2_ROWS = 256 / 240 forces one)
+// rows per tile: 256; SPT_G2_ROWS=240 selects the 240-row tile.  Priced as rounds of one tile per
+// CU times 15/16 of a tile's work it looked 4-6 % cheaper at M = 12000, but it measured slower in
+// every encoder GEMM (r5, profiles/r5/exp_gemm240.txt: qkv 127.4 -> 134.7 us, fc1 194.8 -> 197.4,
+// fc2 147.8 -> 154.7, out 51.5 -> 53.6 standalone; in situ fc1 166.8 -> 181.2): a 240-row tile still
+// stages 256 A rows and writes its epilogue at the 256-row tile's cost, so it is not 15/16 of one
 int g2_rows(const GemmArgs& g, int batch) {
+    (void)g;
+    (void)batch;
     static const int force = getenv("SPT_G2_ROWS") ? atoi(getenv("SPT_G2_ROWS")) : 0;
-    if (force == 256 || force == 240) return force;
-    const int64_t cus = device_cus();
-    auto cost = [&](int rm) {
-        const int64_t tiles = (int64_t)cdiv(g.M, rm) * (g.N / G2_BN) * g.ksplit * batch;
-        return ((tiles + cus - 1) / cus) * rm;
-    };
-    return cost(240) < cost(256) ? 240 : 256;
+    return force == 240 ? 240 : 256;
 }
 
 template <int EPI, bool F16>
