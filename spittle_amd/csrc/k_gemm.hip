@@ -365,30 +365,30 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     };
     // fragment reads: A rows of quadrant half rh, W rows (C columns) of half ch, k-steps 0/1
     bf16x8 af[4][2], bw[2][2][2];
+    // k-step-major read order (s = 0 pieces first): the quadrant's first 8 MFMAs (k-step 0) can
+    // start once half of a phase's reads have landed (a counted lgkmcnt instead of 0)
     auto readA = [&](int buf, int rh) {
         const SPT_LDS char* la = (const SPT_LDS char*)smem + buf * G2_BUF;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (rh == 1 && i == 3 && skip7) continue;
-            const int r = wr * 128 + rh * 64 + 16 * i + fr;
+        for (int s = 0; s < 2; ++s)
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
+            for (int i = 0; i < 4; ++i) {
+                if (rh == 1 && i == 3 && skip7) continue;
+                const int r = wr * 128 + rh * 64 + 16 * i + fr;
                 const int c = 4 * s + fq;
                 af[i][s] = *(const SPT_LDS bf16x8*)(la + r * G2_ROW + ((c ^ swz(r)) << 4));
             }
-        }
     };
     auto readW = [&](int buf, int ch) {
         const SPT_LDS char* lw = (const SPT_LDS char*)smem + buf * G2_BUF + 256 * G2_ROW;
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int r = wc * 64 + ch * 32 + 16 * j + fr;
+        for (int s = 0; s < 2; ++s)
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
+            for (int j = 0; j < 2; ++j) {
+                const int r = wc * 64 + ch * 32 + 16 * j + fr;
                 const int c = 4 * s + fq;
                 bw[ch][j][s] = *(const SPT_LDS bf16x8*)(lw + r * G2_ROW + ((c ^ swz(r)) << 4));
             }
-        }
     };
     f32x4 acc[8][4];
 #pragma unroll
@@ -425,10 +425,12 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
         if (wr == 1) G2_BARRIER();  // group 1 starts one phase behind
         for (int kt = 0; kt < nkt; ++kt) {
             const int c = kt & 1;
-            // P1: A0 W0 -> (0,0); stage A1 of kt+1.  Wait: A1(kt) (read in P3)
+            // P1: A0 W0 -> (0,0); stage A1 of kt+1.  Wait: A1(kt) (read in P3).  Each phase issues
+            // its DMA before its fragment reads, so the reads are the youngest LDS-counter ops and
+            // the MFMAs wait for them with counted lgkmcnt, not 0
+            stageA(c ^ 1, kt + 1, 1);
             readA(c, 0);
             readW(c, 0);
-            stageA(c ^ 1, kt + 1, 1);
             quad(0, 0);
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
             G2_BARRIER();
@@ -437,9 +439,9 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
             quad(0, 1);
             G2_BARRIER();
             // P3: A1 -> (1,1); stage A0, W0 of kt+2.  Wait: A0(kt+1), W0(kt+1) (read in P1')
-            readA(c, 1);
             stageA(c, kt + 2, 0);
             stageW(c, kt + 2, 0);
+            readA(c, 1);
             quad(1, 1);
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
             G2_BARRIER();
@@ -454,21 +456,21 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     for (int kt = 0; kt < nkt; ++kt) {
         const int c = kt & 1;
         // P1
+        stageA(c ^ 1, kt + 1, 1);
         readA(c, 0);
         readW(c, 0);
-        stageA(c ^ 1, kt + 1, 1);
         quad(0, 0);
         G2_VMWAIT();
         G2_BARRIER();
         // P2
-        readW(c, 1);
         stageA(c, kt + 2, 0);
+        readW(c, 1);
         quad(0, 1);
         G2_VMWAIT();
         G2_BARRIER();
         // P3
-        readA(c, 1);
         stageW(c, kt + 2, 0);
+        readA(c, 1);
         quad(1, 1);
         G2_BARRIER();
         // P4
@@ -587,7 +589,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
 // v_mfma_f32_16x16x32 chain over K as in the other tiles (k-step order, lane group fq = k chunk),
 // so the results are bitwise those of the 64 x 64 tile at the same split.
 constexpr int RG_RF = 13, RG_RT = 16 * RG_RF, RG_CT = 64;  // tile: 208 rows x 64 columns
-constexpr int RG_NS = 4, RG_D = 2;                          // ring slots, K-steps in flight per loader
+constexpr int RG_NS = 4;                                    // ring slots (K-steps in flight per loader: template D, 2 or 3)
 constexpr int RG_ROWS = RG_RT + RG_CT;                      // 272 slab rows per slot
 constexpr int RG_SLOT = RG_ROWS * SLAB;                     // 34,816 B
 constexpr int RG_NI = (RG_ROWS / 8 + 3) / 4;                // 9 DMA instructions per loader wave per slot
@@ -608,8 +610,9 @@ __device__ __forceinline__ void rg_post(SPT_LDS int* w, int v) {
     *(volatile SPT_LDS int*)w = v;
 }
 
-template <typename T, int EPI>
+template <typename T, int EPI, int RG_D = 2>
 __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
+    static_assert(RG_D == 2 || RG_D == 3, "K-steps in flight");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     SPT_LDS char* lds = (SPT_LDS char*)smem;
     SPT_LDS int* full = (SPT_LDS int*)(lds + RG_NS * RG_SLOT);  // [slot][loader wave]
@@ -655,8 +658,16 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
             for (int i = 0; i < RG_NI; ++i)
                 __builtin_amdgcn_global_load_lds((const void*)(src[i] + ko), (SPT_LDS void*)(lds + s * RG_SLOT + dst[i]), 16, 0, 0);
             if (k >= RG_D) {
-                asm volatile("s_waitcnt vmcnt(18)" ::: "memory");  // K-step k - 2 landed (RG_NI * RG_D younger)
+                // K-step k - D landed (RG_NI * RG_D younger instructions)
+                if constexpr (RG_D == 2) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(27)" ::: "memory");
                 rg_post(full + 4 * ((k - RG_D) % RG_NS) + lw, k - RG_D + 1);
+            }
+        }
+        if constexpr (RG_D == 3) {
+            if (nkt >= 3) {
+                asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+                rg_post(full + 4 * ((nkt - 3) % RG_NS) + lw, nkt - 2);
             }
         }
         if (nkt >= 2) {
@@ -879,9 +890,13 @@ void launch_small(const GemmArgs& g0, int batch, hipStream_t st) {  // 64 x 128 
 template <typename T, int EPI>
 void launch_ring(const GemmArgs& g, int batch, hipStream_t st) {
     if constexpr (sizeof(T) == 2) {
-        ensure_lds_attr((const void*)gemm_ring_kernel<T, EPI>, RG_LDS);
+        // SPT_RING_D = 3: three K-steps in flight per loader (default 2)
+        static const int d3 = getenv("SPT_RING_D") && atoi(getenv("SPT_RING_D")) == 3;
+        ensure_lds_attr((const void*)gemm_ring_kernel<T, EPI, 2>, RG_LDS);
+        ensure_lds_attr((const void*)gemm_ring_kernel<T, EPI, 3>, RG_LDS);
         dim3 grid(cdiv(g.M, RG_RT) * (g.N / RG_CT), g.ksplit, batch);
-        hipLaunchKernelGGL((gemm_ring_kernel<T, EPI>), grid, dim3(512), RG_LDS, st, g);
+        if (d3) hipLaunchKernelGGL((gemm_ring_kernel<T, EPI, 3>), grid, dim3(512), RG_LDS, st, g);
+        else hipLaunchKernelGGL((gemm_ring_kernel<T, EPI, 2>), grid, dim3(512), RG_LDS, st, g);
     } else {
         throw std::runtime_error("gemm_nt: the ring variant needs a 16-bit dtype");
     }
@@ -909,8 +924,10 @@ void prepare_epi() {
     ensure_lds_attr((const void*)gemm256_kernel<EPI, false, true, 240>, G2_LDS_ALL);
     ensure_lds_attr((const void*)gemm256_kernel<EPI, true, false, 240>, G2_LDS_ALL);
     ensure_lds_attr((const void*)gemm256_kernel<EPI, true, true, 240>, G2_LDS_ALL);
-    ensure_lds_attr((const void*)gemm_ring_kernel<bf16, EPI>, RG_LDS);
-    ensure_lds_attr((const void*)gemm_ring_kernel<f16, EPI>, RG_LDS);
+    ensure_lds_attr((const void*)gemm_ring_kernel<bf16, EPI, 2>, RG_LDS);
+    ensure_lds_attr((const void*)gemm_ring_kernel<f16, EPI, 2>, RG_LDS);
+    ensure_lds_attr((const void*)gemm_ring_kernel<bf16, EPI, 3>, RG_LDS);
+    ensure_lds_attr((const void*)gemm_ring_kernel<f16, EPI, 3>, RG_LDS);
     ensure_lds_attr((const void*)gemm_nt_kernel<bf16, EPI, 3>, 3 * 2 * BM * SLAB);
     ensure_lds_attr((const void*)gemm_nt_kernel<f16, EPI, 3>, 3 * 2 * BM * SLAB);
     ensure_lds_attr((const void*)gemm_nt_kernel<float, EPI, 3>, 3 * 2 * BM * SLAB);
