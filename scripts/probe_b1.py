@@ -1,0 +1,25 @@
+"""GPU box, profiling: the app's B = 1 call shape on large-v3 bf16 (one 30 s window, greedy fast
+path, 128 tokens), three timed calls after a capture call.  Run under rocprofv3 --kernel-trace
+--stats once with SPT_PERSISTENT=0 (the launch chain) and once with 1 (the persistent pass)."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from spittle_amd import WhisperEngine, WhisperInferenceParams, WhisperModelParams  # noqa: E402
+from spittle_amd.synth import synth_audio  # noqa: E402
+
+e = WhisperEngine(WhisperModelParams(dtype="bf16", max_batch=int(os.environ.get("B1_MAX_BATCH", "8"))))
+e.load_model("synthetic:large-v3")
+p = WhisperInferenceParams(language="en", no_timestamps=True, temperature_inc=0.0, ignore_eot=True, max_new_tokens=128)
+x = synth_audio(1000)
+e.transcribe_samples(x, p)
+for _ in range(3):
+    e.transcribe_samples(x, p)
+t = e.timings()
+cs = e.call_stats()
+print(json.dumps({"persistent": os.environ.get("SPT_PERSISTENT", "0"), "decode_ms": t["decode_ms"],
+                  "passes": t["n_decode_passes"], "pass_ms": t["decode_ms"] / t["n_decode_passes"],
+                  "pd_passes": cs["pd_passes"], "pd_fallbacks": cs["pd_fallbacks"]}))
+e.unload_model()
