@@ -311,7 +311,12 @@ constexpr int G2_LDS_ALL = 8 * 128 * (128 + 16) > G2_LDS ? 8 * 128 * (128 + 16) 
 // 256-row tile's work -- its last 16-row fragment row (waves 4-7, rows 240..255) is neither read
 // from LDS nor multiplied, and each SIMD runs one wave of each half, so the MFMA pipe time drops
 // with it.  Every C element is the same MFMA chain in either tile: results are bitwise equal.
-template <int EPI, bool F16, bool STG = false, int RM = 256>
+// PP (with STG): every phase gets a second barrier between its fragment reads / DMA issue and its
+// MFMAs, so the two groups' half-phase lag alternates them: on each SIMD one wave reads while the
+// other multiplies.  The restaging and wait rules above hold unchanged (a read completes before its
+// phase's MFMAs; a half-tile is restaged >= 2 phases after its last read and read >= 2 phases after
+// every wave's wait for it), and the MFMA order per accumulator is the same: bitwise equal results.
+template <int EPI, bool F16, bool STG = false, int RM = 256, bool PP = false>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -431,22 +436,26 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
             stageA(c ^ 1, kt + 1, 1);
             readA(c, 0);
             readW(c, 0);
+            if constexpr (PP) G2_BARRIER();
             quad(0, 0);
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
             G2_BARRIER();
             // P2: W1 -> (0,1)
             readW(c, 1);
+            if constexpr (PP) G2_BARRIER();
             quad(0, 1);
             G2_BARRIER();
             // P3: A1 -> (1,1); stage A0, W0 of kt+2.  Wait: A0(kt+1), W0(kt+1) (read in P1')
             stageA(c, kt + 2, 0);
             stageW(c, kt + 2, 0);
             readA(c, 1);
+            if constexpr (PP) G2_BARRIER();
             quad(1, 1);
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
             G2_BARRIER();
             // P4: (1,0) from registers; stage W1 of kt+2.  Wait: W1(kt+1) (read in P2')
             stageW(c, kt + 2, 1);
+            if constexpr (PP) G2_BARRIER();
             quad(1, 0);
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
             G2_BARRIER();
@@ -847,13 +856,18 @@ void launch_256(const GemmArgs& g, int batch, hipStream_t st) {
     ensure_lds_attr((const void*)gemm256_kernel<EPI, F16, true>, G2_LDS_ALL);
     ensure_lds_attr((const void*)gemm256_kernel<EPI, F16, false, 240>, G2_LDS_ALL);
     ensure_lds_attr((const void*)gemm256_kernel<EPI, F16, true, 240>, G2_LDS_ALL);
+    ensure_lds_attr((const void*)gemm256_kernel<EPI, F16, true, 256, true>, G2_LDS_ALL);
+    // ping-pong phases (a barrier between each phase's reads and its MFMAs; r5: q/k/v 125.4 -> 119.4 us,
+    // 4096^3 1182 -> 1246 TF/s standalone, encoder 20.4 -> 20.2 ms, bitwise equal); SPT_G2_PP=0: off
+    static const bool pp = !getenv("SPT_G2_PP") || atoi(getenv("SPT_G2_PP")) != 0;
     const int rm = g2_rows(g, batch);
     dim3 grid(cdiv(g.M, rm) * (g.N / G2_BN), g.ksplit, batch);
     if (rm == 240) {
         if (stg) hipLaunchKernelGGL((gemm256_kernel<EPI, F16, true, 240>), grid, dim3(512), G2_LDS_ALL, st, g);
         else hipLaunchKernelGGL((gemm256_kernel<EPI, F16, false, 240>), grid, dim3(512), G2_LDS_ALL, st, g);
     } else {
-        if (stg) hipLaunchKernelGGL((gemm256_kernel<EPI, F16, true>), grid, dim3(512), G2_LDS_ALL, st, g);
+        if (stg && pp) hipLaunchKernelGGL((gemm256_kernel<EPI, F16, true, 256, true>), grid, dim3(512), G2_LDS_ALL, st, g);
+        else if (stg) hipLaunchKernelGGL((gemm256_kernel<EPI, F16, true>), grid, dim3(512), G2_LDS_ALL, st, g);
         else hipLaunchKernelGGL((gemm256_kernel<EPI, F16, false>), grid, dim3(512), G2_LDS_ALL, st, g);
     }
     SPT_LAUNCH_CHECK();
@@ -924,6 +938,8 @@ void prepare_epi() {
     ensure_lds_attr((const void*)gemm256_kernel<EPI, false, true, 240>, G2_LDS_ALL);
     ensure_lds_attr((const void*)gemm256_kernel<EPI, true, false, 240>, G2_LDS_ALL);
     ensure_lds_attr((const void*)gemm256_kernel<EPI, true, true, 240>, G2_LDS_ALL);
+    ensure_lds_attr((const void*)gemm256_kernel<EPI, false, true, 256, true>, G2_LDS_ALL);
+    ensure_lds_attr((const void*)gemm256_kernel<EPI, true, true, 256, true>, G2_LDS_ALL);
     ensure_lds_attr((const void*)gemm_ring_kernel<bf16, EPI, 2>, RG_LDS);
     ensure_lds_attr((const void*)gemm_ring_kernel<f16, EPI, 2>, RG_LDS);
     ensure_lds_attr((const void*)gemm_ring_kernel<bf16, EPI, 3>, RG_LDS);
