@@ -7,13 +7,20 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+import torch  # noqa: E402  (HIP initialised by the runtime the profiler expects, as bench.py does)
+
+torch.cuda.init()
+
 from spittle_amd import WhisperEngine, WhisperInferenceParams, WhisperModelParams  # noqa: E402
 from spittle_amd.synth import synth_audio  # noqa: E402
 
 e = WhisperEngine(WhisperModelParams(dtype="bf16", max_batch=int(os.environ.get("B1_MAX_BATCH", "8"))))
 e.load_model("synthetic:large-v3")
-p = WhisperInferenceParams(language="en", no_timestamps=True, temperature_inc=0.0, ignore_eot=True, max_new_tokens=128)
-x = synth_audio(1000)
+if os.environ.get("B1_FULL"):  # the app's own call: whisper_full defaults (timestamps, fallback, best_of 5)
+    p = WhisperInferenceParams(language="en")
+else:
+    p = WhisperInferenceParams(language="en", no_timestamps=True, temperature_inc=0.0, ignore_eot=True, max_new_tokens=128)
+x = synth_audio(1000)[: int(os.environ.get("B1_SAMPLES", "480000"))]
 e.transcribe_samples(x, p)
 for _ in range(3):
     e.transcribe_samples(x, p)
