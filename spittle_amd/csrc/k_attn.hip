@@ -664,12 +664,15 @@ void enc_attention(int dtype, const void* qkv, int B, int T, int H, void* out, h
     const int sum = sum_env ? atoi(sum_env) : 4;
     const char* ql_env = getenv("SPT_ATTN_QL");  // Q fragments in LDS (default; 0: in registers, r4)
     const bool ql = !(ql_env && atoi(ql_env) == 0);
-    static const int swz = getenv("SPT_ATTN_SWZ") ? atoi(getenv("SPT_ATTN_SWZ")) : 1;
+    const char* swz_env = getenv("SPT_ATTN_SWZ");  // read per launch, as sum
+    const int swz = swz_env ? atoi(swz_env) : 1;
     if (dtype == DT_BF16 && !q32) {
         dim3 g(cdiv(T, 256), H, B);
         if (sum == 1) hipLaunchKernelGGL(attn_bf16_q64_kernel<1>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
         else if (sum == 2) hipLaunchKernelGGL(attn_bf16_q64_kernel<2>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
         else if (sum == 3 && swz == 3) hipLaunchKernelGGL((attn_bf16_q64_kernel<3, 3>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
+        else if (sum == 4 && ql && swz == 3)
+            hipLaunchKernelGGL((attn_bf16_q64_kernel<4, 3, true>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
         else if (sum == 4 && ql) hipLaunchKernelGGL((attn_bf16_q64_kernel<4, 1, true>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
         else if (sum == 4) hipLaunchKernelGGL(attn_bf16_q64_kernel<4>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
         else if (sum == 3) hipLaunchKernelGGL(attn_bf16_q64_kernel<3>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
