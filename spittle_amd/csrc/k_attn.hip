@@ -664,8 +664,10 @@ void enc_attention(int dtype, const void* qkv, int B, int T, int H, void* out, h
     const int sum = sum_env ? atoi(sum_env) : 4;
     const char* ql_env = getenv("SPT_ATTN_QL");  // Q fragments in LDS (default; 0: in registers, r4)
     const bool ql = !(ql_env && atoi(ql_env) == 0);
-    const char* swz_env = getenv("SPT_ATTN_SWZ");  // read per launch, as sum
-    const int swz = swz_env ? atoi(swz_env) : 1;
+    // read per launch, as sum.  3 (K and V tiles swizzled): r5, 129.3 -> 128.5 us in two A/B pairs,
+    // bitwise equal (scripts/enc_swz_bitwise.py)
+    const char* swz_env = getenv("SPT_ATTN_SWZ");
+    const int swz = swz_env ? atoi(swz_env) : 3;
     if (dtype == DT_BF16 && !q32) {
         dim3 g(cdiv(T, 256), H, B);
         if (sum == 1) hipLaunchKernelGGL(attn_bf16_q64_kernel<1>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);

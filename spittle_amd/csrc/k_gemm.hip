@@ -850,7 +850,10 @@ template <int EPI, bool F16>
 void launch_256(const GemmArgs& g, int batch, hipStream_t st) {
     // staggered wave groups: bitwise-identical results, encoder 21.54 -> 21.28 ms (r2, two A/B pairs);
     // SPT_G2_STAGGER=0 restores the lock-step schedule
-    static const bool stg = !getenv("SPT_G2_STAGGER") || atoi(getenv("SPT_G2_STAGGER")) != 0;
+    // (both switches read per launch: eager runs such as debug_encode pick them up; a captured encoder
+    // keeps what it was captured with)
+    const char* stg_env = getenv("SPT_G2_STAGGER");
+    const bool stg = !stg_env || atoi(stg_env) != 0;
     // > 64 KiB dynamic LDS: per kernel and device (gemm_prepare sets them before any capture)
     ensure_lds_attr((const void*)gemm256_kernel<EPI, F16, false>, G2_LDS_ALL);
     ensure_lds_attr((const void*)gemm256_kernel<EPI, F16, true>, G2_LDS_ALL);
@@ -859,7 +862,8 @@ void launch_256(const GemmArgs& g, int batch, hipStream_t st) {
     ensure_lds_attr((const void*)gemm256_kernel<EPI, F16, true, 256, true>, G2_LDS_ALL);
     // ping-pong phases (a barrier between each phase's reads and its MFMAs; r5: q/k/v 125.4 -> 119.4 us,
     // 4096^3 1182 -> 1246 TF/s standalone, encoder 20.4 -> 20.2 ms, bitwise equal); SPT_G2_PP=0: off
-    static const bool pp = !getenv("SPT_G2_PP") || atoi(getenv("SPT_G2_PP")) != 0;
+    const char* pp_env = getenv("SPT_G2_PP");
+    const bool pp = !pp_env || atoi(pp_env) != 0;
     const int rm = g2_rows(g, batch);
     dim3 grid(cdiv(g.M, rm) * (g.N / G2_BN), g.ksplit, batch);
     if (rm == 240) {
