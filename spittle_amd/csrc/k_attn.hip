@@ -37,6 +37,14 @@ __device__ __forceinline__ float max3f(float a, float b, float c) {
     return r;
 }
 
+// ds_read_b64_tr_b16 as inline asm at base + OFF: the caller waits lgkmcnt itself before using it
+template <int OFF>
+__device__ __forceinline__ bf16x4v ds_tr16_asm(const SPT_LDS char* base) {
+    bf16x4v v;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(base), "i"(OFF) : "memory");
+    return v;
+}
+
 __device__ __forceinline__ int key_of(int kt2, int r, int hf) { return 32 * kt2 + (r & 3) + 8 * (r >> 2) + 4 * hf; }
 
 // -------------------------------------------------------------------- bf16
@@ -486,6 +494,41 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_q64_kernel(const bf16* __res
         }
         // O^T += V^T . P^T for both query blocks from one V^T fragment
         const int g = lane >> 4, i16 = lane & 15;
+        if constexpr (QL) {
+            // the V^T reads as inline asm: issued through the builtin, each made the compiler wait
+            // vmcnt(0) first -- for the NEXT tile's K/V DMA, issued at this tile's start into the
+            // other buffer (it cannot tell the two LDS regions apart), so no tile's DMA overlapped
+            // its own PV phase.  One lgkmcnt(0) per 8 reads instead (sched_barrier: the MFMAs stay
+            // behind it); the data is the previous tile's DMA, retired by its end-of-tile wait.
+            // the non-QL loop's addresses, split into a lane base per dt and constant offsets: key0 =
+            // 32 kt2 + 16 sp + kl (+ 8 for hi), whose swizzle bit (bit 1) is kl's; chunk 4 dt + cl
+            const int kl = 4 * hf + (i16 >> 2);
+            const int sb = (SW & 2) ? ((kl >> 1) & 1) : 0;  // vswz = 4: chunk ^ 4 flips dt's bit
+            const int cl = 2 * (g & 1) + ((i16 & 3) >> 1), c8 = 8 * (i16 & 1);
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt) {
+                const SPT_LDS char* vb = lv + kl * 128 + ((4 * (dt ^ sb) + cl) << 4) + c8;
+                bf16x4v lo[2][2], hi[2][2];
+                lo[0][0] = ds_tr16_asm<0>(vb);
+                hi[0][0] = ds_tr16_asm<1024>(vb);
+                lo[0][1] = ds_tr16_asm<2048>(vb);
+                hi[0][1] = ds_tr16_asm<3072>(vb);
+                lo[1][0] = ds_tr16_asm<4096>(vb);
+                hi[1][0] = ds_tr16_asm<5120>(vb);
+                lo[1][1] = ds_tr16_asm<6144>(vb);
+                hi[1][1] = ds_tr16_asm<7168>(vb);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+                    for (int sp = 0; sp < 2; ++sp) {
+                        const bf16x8 va = __builtin_shufflevector(lo[kt2][sp], hi[kt2][sp], 0, 1, 2, 3, 4, 5, 6, 7);
+                        o[0][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pf[0][kt2][sp], o[0][dt], 0, 0, 0);
+                        o[1][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pf[1][kt2][sp], o[1][dt], 0, 0, 0);
+                    }
+            }
+        } else
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) {
             const int col = 32 * dt + 16 * (g & 1) + 4 * (i16 & 3);
