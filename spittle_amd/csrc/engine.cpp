@@ -108,6 +108,10 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     HIP_CHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     ev_.resize(12);  // 0-1 mel, 2-5 window / encoder / cross K/V, 6-7 decode, 8-9 a beam step, 10-11 H2D
     for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
+    enc_st_.assign(kEncGroupsMax - 1, nullptr);
+    for (auto& s : enc_st_) HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    enc_ev_.assign(kEncGroupsMax, nullptr);
+    for (auto& e : enc_ev_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     // a decoder pass stages at most max_rows_ rows in its LayerNorm GEMVs' LDS images; a batch
     // above that is decoded as several groups (each sized for the whole batch, re-sliced per call)
     max_rows_ = gemv_max_image_rows(dt_, dm_.d);
@@ -162,6 +166,15 @@ void Engine::release() {
     }
     for (auto& kv : enc_graphs_) (void)hipGraphExecDestroy(kv.second);
     enc_graphs_.clear();
+    for (auto& s : enc_st_)
+        if (s) {
+            (void)hipStreamSynchronize(s);
+            (void)hipStreamDestroy(s);
+        }
+    enc_st_.clear();
+    for (auto& e : enc_ev_)
+        if (e) (void)hipEventDestroy(e);
+    enc_ev_.clear();
     if (warena_) (void)hipFree(warena_);
     if (aarena_) (void)hipFree(aarena_);
     if (kvtmp_) (void)hipFree(kvtmp_);
@@ -764,7 +777,7 @@ void Engine::encode_windows(const int* utt, const int* seek, int E) {
 }
 
 void Engine::run_encoder(int B) {
-    const int d = dm_.d, T = dm_.n_audio_ctx, H = dm_.n_head, M = B * T;
+    const int d = dm_.d, T = dm_.n_audio_ctx, H = dm_.n_head;
     GemmArgs g{};
     // conv1 (k3, s1, p1) + GELU -> y1p rows 1..3000
     g.A = mel_in_; g.lda = cp_; g.sA = (int64_t)MEL_ROWS * cp_;
@@ -782,29 +795,72 @@ void Engine::run_encoder(int B) {
     g.C = x_; g.ldc = d; g.sC = (int64_t)T * d;
     g.pos = enc_pos_;
     gemm_nt(dt_, EPI_BIAS_GELU_POS, g, B, st_);
+    // The layers run per window group, each group's rows (whole windows: every kernel below is
+    // row-local or per window) on its own stream, so one group's kernels fill the CUs the other's
+    // leave idle: a 256 x 256-tile GEMM's last partial round, the attention's tail, the
+    // memory-bound LayerNorms beside MFMA-bound GEMMs.  Every output row is computed by the same
+    // operations in the same order whatever the grouping (the GEMM tile variants are bitwise
+    // equal), so the grouping never changes a bit (test_encoder_groups_bitwise).
+    const int G = enc_groups(B);
+    int b0[kEncGroupsMax + 1];
+    for (int i = 0; i <= G; ++i) b0[i] = (int)((int64_t)B * i / G);
+    auto stream_of = [&](int i) { return i == 0 ? st_ : enc_st_[i - 1]; };
+    if (G > 1) {
+        HIP_CHECK(hipEventRecord(enc_ev_[0], st_));
+        for (int i = 1; i < G; ++i) HIP_CHECK(hipStreamWaitEvent(stream_of(i), enc_ev_[0], 0));
+    }
+    auto rows = [&](void* base, int64_t row, int64_t ld, int es) { return (char*)base + row * ld * es; };
     for (int l = 0; l < dm_.n_enc; ++l) {
         const EncL& e = enc_[l];
-        layernorm(dt_, x_, M, d, e.ln1_w, e.ln1_b, xn_, st_);
-        g = GemmArgs{};
-        g.A = xn_; g.lda = d; g.W = e.qkv_w; g.ldw = d; g.M = M; g.N = 3 * d; g.K = d; g.bias = e.qkv_b;
-        g.C = qkv_; g.ldc = 3 * d;
-        gemm_nt(dt_, EPI_BIAS, g, 1, st_);
-        enc_attention(dt_, qkv_, B, T, H, ao_, st_);
-        g = GemmArgs{};
-        g.A = ao_; g.lda = d; g.W = e.o_w; g.ldw = d; g.M = M; g.N = d; g.K = d; g.bias = e.o_b;
-        g.C = x_; g.ldc = d;
-        gemm_nt(dt_, EPI_BIAS_RESID, g, 1, st_);
-        layernorm(dt_, x_, M, d, e.ln2_w, e.ln2_b, xn_, st_);
-        g = GemmArgs{};
-        g.A = xn_; g.lda = d; g.W = e.fc1_w; g.ldw = d; g.M = M; g.N = 4 * d; g.K = d; g.bias = e.fc1_b;
-        g.C = ff_; g.ldc = 4 * d;
-        gemm_nt(dt_, EPI_BIAS_GELU, g, 1, st_);
-        g = GemmArgs{};
-        g.A = ff_; g.lda = 4 * d; g.W = e.fc2_w; g.ldw = 4 * d; g.M = M; g.N = d; g.K = 4 * d; g.bias = e.fc2_b;
-        g.C = x_; g.ldc = d;
-        gemm_nt(dt_, EPI_BIAS_RESID, g, 1, st_);
+        for (int i = 0; i < G; ++i) {  // layer l of every group before layer l + 1 of any
+            hipStream_t s = stream_of(i);
+            const int Bg = b0[i + 1] - b0[i], M = Bg * T;
+            const int64_t r0 = (int64_t)b0[i] * T;
+            float* x = (float*)rows(x_, r0, d, 4);
+            void* xn = rows(xn_, r0, d, esz_);
+            void* qkv = rows(qkv_, r0, 3 * d, esz_);
+            void* ao = rows(ao_, r0, d, esz_);
+            void* ff = rows(ff_, r0, 4 * d, esz_);
+            layernorm(dt_, x, M, d, e.ln1_w, e.ln1_b, xn, s);
+            g = GemmArgs{};
+            g.A = xn; g.lda = d; g.W = e.qkv_w; g.ldw = d; g.M = M; g.N = 3 * d; g.K = d; g.bias = e.qkv_b;
+            g.C = qkv; g.ldc = 3 * d;
+            gemm_nt(dt_, EPI_BIAS, g, 1, s);
+            enc_attention(dt_, qkv, Bg, T, H, ao, s);
+            g = GemmArgs{};
+            g.A = ao; g.lda = d; g.W = e.o_w; g.ldw = d; g.M = M; g.N = d; g.K = d; g.bias = e.o_b;
+            g.C = x; g.ldc = d;
+            gemm_nt(dt_, EPI_BIAS_RESID, g, 1, s);
+            layernorm(dt_, x, M, d, e.ln2_w, e.ln2_b, xn, s);
+            g = GemmArgs{};
+            g.A = xn; g.lda = d; g.W = e.fc1_w; g.ldw = d; g.M = M; g.N = 4 * d; g.K = d; g.bias = e.fc1_b;
+            g.C = ff; g.ldc = 4 * d;
+            gemm_nt(dt_, EPI_BIAS_GELU, g, 1, s);
+            g = GemmArgs{};
+            g.A = ff; g.lda = 4 * d; g.W = e.fc2_w; g.ldw = 4 * d; g.M = M; g.N = d; g.K = 4 * d; g.bias = e.fc2_b;
+            g.C = x; g.ldc = d;
+            gemm_nt(dt_, EPI_BIAS_RESID, g, 1, s);
+        }
     }
-    layernorm(dt_, x_, M, d, lnp_w_, lnp_b_, enc_out_, st_);
+    for (int i = 0; i < G; ++i) {
+        const int64_t r0 = (int64_t)b0[i] * T;
+        layernorm(dt_, (float*)rows(x_, r0, d, 4), (b0[i + 1] - b0[i]) * T, d, lnp_w_, lnp_b_,
+                  rows(enc_out_, r0, d, esz_), stream_of(i));
+    }
+    for (int i = 1; i < G; ++i) {
+        HIP_CHECK(hipEventRecord(enc_ev_[i], stream_of(i)));
+        HIP_CHECK(hipStreamWaitEvent(st_, enc_ev_[i], 0));
+    }
+}
+
+// Window groups of an encoder call: SPT_ENC_GROUPS (1..4, read per call; at most one group per
+// window); default two groups from eight windows up (C3: groups of 6000 rows keep the 256 x 256
+// tiles; r5 A/B, profiles/r5/exp_enc_groups.txt: encoder 20.15 -> 20.04 ms), else one.  Three or
+// four groups at B = 8 drop the N = 1280 GEMMs to 128-row tiles and were 15-35 % slower.
+int Engine::enc_groups(int B) const {
+    int G = B >= 8 ? 2 : 1;
+    if (const char* v = getenv("SPT_ENC_GROUPS")) G = atoi(v);
+    return std::max(1, std::min({G, kEncGroupsMax, B}));
 }
 
 // The encoder is one fixed chain of launches per batch size (about 7 per layer, 230 for
@@ -813,12 +869,13 @@ void Engine::run_encoder(int B) {
 // kernels' one-time attributes outside any capture.  SPT_NO_GRAPH / SPT_ENC_GRAPH=0: eager.
 void Engine::enqueue_encoder(int B) {
     static const bool eager = getenv("SPT_NO_GRAPH") || (getenv("SPT_ENC_GRAPH") && atoi(getenv("SPT_ENC_GRAPH")) == 0);
-    if (eager || !enc_seen_.count(B)) {
-        enc_seen_.insert(B);
+    const std::pair<int, int> key{B, enc_groups(B)};
+    if (eager || !enc_seen_.count(key)) {
+        enc_seen_.insert(key);
         run_encoder(B);
         return;
     }
-    auto it = enc_graphs_.find(B);
+    auto it = enc_graphs_.find(key);
     if (it == enc_graphs_.end()) {
         hipGraph_t graph;
         HIP_CHECK(hipStreamBeginCapture(st_, hipStreamCaptureModeThreadLocal));
@@ -832,7 +889,7 @@ void Engine::enqueue_encoder(int B) {
         hipGraphExec_t exec;
         HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
         HIP_CHECK(hipGraphDestroy(graph));
-        it = enc_graphs_.emplace(B, exec).first;
+        it = enc_graphs_.emplace(key, exec).first;
     }
     HIP_CHECK(hipGraphLaunch(it->second, st_));
 }

@@ -243,6 +243,12 @@ private:
     int max_rows_ = 64;  // decoder rows per pass (gemv_max_image_rows); larger batches use more groups  // SPT_DECODE_GROUPS=2 splits the batch over two streams
     hipStream_t st_ = nullptr;
     std::vector<hipEvent_t> ev_;
+    // the encoder's window groups (run_encoder): groups 1.. run on these streams beside group 0 on
+    // st_; enc_ev_[0] forks them off st_, enc_ev_[i] joins group i back
+    static constexpr int kEncGroupsMax = 4;
+    std::vector<hipStream_t> enc_st_;
+    std::vector<hipEvent_t> enc_ev_;
+    int enc_groups(int B) const;
     // probe(): the decoder kernel kind timed in situ by an eager enqueue_layers (-1: none), and
     // its event pair per layer
     int probe_kind_ = -1;
@@ -264,8 +270,10 @@ private:
     std::vector<DecL> dec_;
     struct TRef { void* p; int64_t n; int dt; };
     std::map<int, TRef> tref_;
-    std::map<int, hipGraphExec_t> enc_graphs_;  // batch size -> captured encoder (enqueue_encoder)
-    std::set<int> enc_seen_;                     // batch sizes whose first, eager encoder call ran  // tensor id -> device location (for checksums)
+    // (batch size, window groups) -> captured encoder (enqueue_encoder), and the keys whose first,
+    // eager encoder call ran
+    std::map<std::pair<int, int>, hipGraphExec_t> enc_graphs_;
+    std::set<std::pair<int, int>> enc_seen_;
 
     // ---- tables
     float *hann_ = nullptr, *sinv_ = nullptr, *cosv_ = nullptr, *filt_ = nullptr;
