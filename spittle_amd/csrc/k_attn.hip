@@ -217,7 +217,7 @@ __device__ __forceinline__ int vswz(int r) { return (SW & 2) ? ((r & 2) << 1) : 
 // spilled, and the loop reloaded K/V stage addresses and Q pieces from scratch on every tile (r5).
 template <int SUM, int SW = 1, bool QL = false>  // row sums: 0 packed f32 VALU, 1 scalar f32 VALU, 2 an MFMA with a ones operand
 __global__ __launch_bounds__(256, 2) void attn_bf16_q64_kernel(const bf16* __restrict__ qkv, int T, int H,
-                                                               bf16* __restrict__ out) {
+                                                               bf16* __restrict__ out, int fulldma) {
     // [buf][K|V][64 keys][128 B] (+ QL: [wave][qb * 4 + s][lane] x 16 B)
     __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128 + (QL ? 4 * 8 * 64 * 16 : 0)];
     const int d = H * 64, ld = 3 * d;
@@ -262,6 +262,21 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_q64_kernel(const bf16* __res
             glds16(kr + d + 8 * (pch ^ vswz<SW>(rt)), lds_v(buf) + p * 1024);
         }
     };
+    // SW == 3, a tile wholly inside T: a wave-uniform row address plus two per-lane byte offsets.
+    // Row 8p + prow's K swizzle (r >> 1) & 7 is (prow >> 1) ^ 4 (p & 1) and its V swizzle
+    // (r & 2) << 1 is prow's, and a row is a multiple of 128 B, so the offsets are fixed per lane:
+    // no per-tile clamp, multiply and 64-bit add per piece (r5)
+    const uint32_t lk0 = (uint32_t)(prow * ld * 2) + ((pch ^ (prow >> 1)) << 4);
+    const uint32_t lv0 = (uint32_t)(prow * ld * 2) + ((pch ^ ((prow & 2) << 1)) << 4);
+    auto stage_full = [&](int buf, int kt) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int p = wid * 2 + i;
+            const char* row = (const char*)(base + (size_t)(kt * 64 + 8 * p) * ld + d + h * 64);
+            glds16(row + (i ? (lk0 ^ 64u) : lk0), lds_k(buf) + p * 1024);
+            glds16(row + 2 * d + lv0, lds_v(buf) + p * 1024);
+        }
+    };
 
     float m_run[2] = {-INFINITY, -INFINITY}, lsum[2] = {0.f, 0.f};
     f32x16 o[2][2], lacc[2];
@@ -287,7 +302,10 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_q64_kernel(const bf16* __res
     // one K/V tile; called with a literal buffer index (the loop below is unrolled by two), so every
     // LDS address is a constant offset from one base: no per-tile address VALU beside the MFMAs (r4)
     auto tile = [&](const int kt, const int cur) __attribute__((always_inline)) {
-        if (kt + 1 < nkt) stage(cur ^ 1, kt + 1);
+        if (kt + 1 < nkt) {
+            if (SW == 3 && fulldma && (kt + 1) * 64 + 64 <= T) stage_full(cur ^ 1, kt + 1);
+            else stage(cur ^ 1, kt + 1);
+        }
         const SPT_LDS char* lk = lds_k(cur);
         const SPT_LDS char* lv = lds_v(cur);
         f32x16 s[2][2];
@@ -980,6 +998,10 @@ void enc_attention(int dtype, const void* qkv, int B, int T, int H, void* out, h
     const int swz = swz_env ? atoi(swz_env) : 3;
     // 1: the ping-pong wave groups (attn_bf16_pp_kernel, bitwise the SUM = 4 / SWZ = 3 / QL kernel's
     // output); read per launch, as sum
+    // DMA sources of whole tiles as a row address + fixed lane offsets (SW = 3; 0: the clamped
+    // per-tile address arithmetic of r4); read per launch, as sum
+    const char* fd_env = getenv("SPT_ATTN_FULLDMA");
+    const int fulldma = !(fd_env && atoi(fd_env) == 0);
     const char* pp_env = getenv("SPT_ATTN_PP");
     const bool pp = pp_env && atoi(pp_env) != 0;
     if (dtype == DT_BF16 && !q32 && pp && sum == 4 && ql && swz == 3 && (int64_t)T * 3 * H * 64 < (1ll << 31)) {
@@ -989,17 +1011,17 @@ void enc_attention(int dtype, const void* qkv, int B, int T, int H, void* out, h
     }
     if (dtype == DT_BF16 && !q32) {
         dim3 g(cdiv(T, 256), H, B);
-        if (sum == 1) hipLaunchKernelGGL(attn_bf16_q64_kernel<1>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
-        else if (sum == 2) hipLaunchKernelGGL(attn_bf16_q64_kernel<2>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
-        else if (sum == 3 && swz == 3) hipLaunchKernelGGL((attn_bf16_q64_kernel<3, 3>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
+        if (sum == 1) hipLaunchKernelGGL(attn_bf16_q64_kernel<1>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out, fulldma);
+        else if (sum == 2) hipLaunchKernelGGL(attn_bf16_q64_kernel<2>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out, fulldma);
+        else if (sum == 3 && swz == 3) hipLaunchKernelGGL((attn_bf16_q64_kernel<3, 3>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out, fulldma);
         else if (sum == 4 && ql && swz == 3)
-            hipLaunchKernelGGL((attn_bf16_q64_kernel<4, 3, true>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
-        else if (sum == 4 && ql) hipLaunchKernelGGL((attn_bf16_q64_kernel<4, 1, true>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
-        else if (sum == 4) hipLaunchKernelGGL(attn_bf16_q64_kernel<4>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
-        else if (sum == 3) hipLaunchKernelGGL(attn_bf16_q64_kernel<3>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
-        else if (swz == 0) hipLaunchKernelGGL((attn_bf16_q64_kernel<0, 0>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
-        else if (swz == 1) hipLaunchKernelGGL((attn_bf16_q64_kernel<0, 1>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
-        else hipLaunchKernelGGL((attn_bf16_q64_kernel<0, 3>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out);
+            hipLaunchKernelGGL((attn_bf16_q64_kernel<4, 3, true>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out, fulldma);
+        else if (sum == 4 && ql) hipLaunchKernelGGL((attn_bf16_q64_kernel<4, 1, true>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out, fulldma);
+        else if (sum == 4) hipLaunchKernelGGL(attn_bf16_q64_kernel<4>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out, fulldma);
+        else if (sum == 3) hipLaunchKernelGGL(attn_bf16_q64_kernel<3>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out, fulldma);
+        else if (swz == 0) hipLaunchKernelGGL((attn_bf16_q64_kernel<0, 0>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out, fulldma);
+        else if (swz == 1) hipLaunchKernelGGL((attn_bf16_q64_kernel<0, 1>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out, fulldma);
+        else hipLaunchKernelGGL((attn_bf16_q64_kernel<0, 3>), g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out, fulldma);
         return;
     }
     dim3 grid(cdiv(T, 128), H, B);
