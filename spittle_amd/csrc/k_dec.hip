@@ -553,8 +553,10 @@ void gemv_launch_rg(const GemvArgs& a, hipStream_t st) {
             // K = 10 super-steps (large-v3's d = 1280 in bf16): 10 waves, each an exact slice, so
             // the LayerNorm does not wait for the weight stream (GV_EXACT_LN=0 restores r1's shapes)
             static const bool exact_ln = !getenv("GV_EXACT_LN") || atoi(getenv("GV_EXACT_LN")) != 0;
+            // SPT_GV_CT2_MIN: the smallest N given two column tiles per workgroup (experiments)
+            static const int ct2_min = getenv("SPT_GV_CT2_MIN") ? atoi(getenv("SPT_GV_CT2_MIN")) : 4096;
             if (exact_ln && nss == 10) {
-                if (a.N >= 4096) gemv_launch_cfg<T, MODE, ASRC, RG, 10, 2, 2, true>(a, st);
+                if (a.N >= ct2_min) gemv_launch_cfg<T, MODE, ASRC, RG, 10, 2, 2, true>(a, st);
                 else gemv_launch_cfg<T, MODE, ASRC, RG, 10, 1, 1, true>(a, st);
                 return;
             }
