@@ -61,6 +61,7 @@ def parse():
     ap.add_argument("--no-app-latency", action="store_true", help="skip the B=1 whisper_full (app default) latency")
     ap.add_argument("--no-probe", action="store_true", help="skip the per-kernel HIP-event probes")
     ap.add_argument("--no-turbo", action="store_true", help="skip the Whisper Turbo (4 decoder layers) line")
+    ap.add_argument("--no-c2", action="store_true", help="skip the Whisper-small f32 B=1 line (BASELINE config 2)")
     ap.add_argument("--no-parakeet", action="store_true", help="skip the Parakeet-V3 (BASELINE config 5) lines")
     ap.add_argument("--parakeet-only", action="store_true", help="only the Parakeet-V3 lines (developer runs)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -505,6 +506,57 @@ def turbo_bench(device: int, pcm_list, steps: int, warmup: int, decode_steps: in
             "decode_ms_per_pass": round(t["decode_ms"] / max(1, t["n_decode_passes"]), 4)}
 
 
+C2_SPEC = "synthetic:small"
+C2_TRAFFIC_JSON = "profiles/r6/pmc_c2_small_f32.json"
+
+
+def small_f32_bench(device: int, steps: int, warmup: int, decode_steps: int, with_cpu: bool) -> dict:
+    """BASELINE.json configs[1] (C2): Whisper-small, fp32 end to end (exact-f32 MFMA), one 30 s
+    chunk per call (B = 1: the app's one-utterance call, transcription.rs:494-503), the benchmark
+    protocol (greedy en, no timestamps, 4-token prompt + decode_steps passes, EOT ignored), host PCM
+    in, text out.  RTFx of the median call; encoder fraction of the 157.3 TF f32 peak; decode-pass
+    HBM fraction (bytes one pass streams / mean pass time); `traffic`: PMC FETCH_SIZE of the C2
+    decode pass's kernels per pass from its own rocprofv3 run (scripts/c2_pmc.sh ->
+    profiles/r6/pmc_c2_small_f32.json), never the large-v3 figure; cpu_baseline: the oracle on
+    the same chunk, whole (mel + encoder + every decoder pass)."""
+    import numpy as np
+    from spittle_amd import WhisperEngine, WhisperInferenceParams, WhisperModelParams
+    from spittle_amd.synth import synth_audio
+    e = WhisperEngine(WhisperModelParams(dtype="f32", device=device, max_batch=1, seed=1234))
+    e.load_model(C2_SPEC)
+    info = e.info()
+    p = WhisperInferenceParams(language="en", no_timestamps=True, temperature_inc=0.0, ignore_eot=True,
+                               max_new_tokens=decode_steps)
+    x = synth_audio(0)
+    for _ in range(warmup):
+        e.transcribe_samples(x, p)
+    marks = [time.perf_counter()]
+    for _ in range(steps):
+        r = e.transcribe_samples(x, p)
+        marks.append(time.perf_counter())
+    assert len(r.tokens) == decode_steps
+    med = float(np.median(np.diff(marks)))
+    t = e.timings()
+    roofs = phase_rooflines(info, t, 1, decode_steps, "f32")
+    e.unload_model()
+    dp = roofs.get("decode_pass", {})
+    if dp:
+        dp["traffic"] = None
+        pmc = os.path.join(ROOT, C2_TRAFFIC_JSON)
+        if os.path.exists(pmc):
+            j = json.load(open(pmc))
+            dp["traffic"] = j.get("hbm_bytes_per_pass")
+            dp["traffic_ratio"] = round(j["hbm_bytes_per_pass"] / dp["bytes_per_pass"], 3)
+            dp["traffic_source"] = C2_TRAFFIC_JSON
+    out = {"model": C2_SPEC, "dtype": "f32", "batch": 1, "steps": steps, "rtfx": round(CHUNK_S / med, 2),
+           "ms_per_call_median": round(med * 1e3, 3),
+           "phases_ms": {k: round(v, 3) for k, v in t.items() if k.endswith("_ms")},
+           "rooflines": roofs}
+    if with_cpu:
+        out["cpu_baseline"] = cpu_baseline(C2_SPEC, decode_steps)
+    return out
+
+
 def main():
     args = parse()
     world_env = os.environ.get("WORLD_SIZE")
@@ -623,6 +675,9 @@ def main():
     tb = None
     if rank == 0 and world == 1 and not args.no_turbo and args.model == "synthetic:large-v3":
         tb = turbo_bench(local, pcm_list, min(args.steps, 5), 1, args.decode_steps)
+    c2 = None
+    if rank == 0 and world == 1 and not args.no_c2 and args.model == "synthetic:large-v3":
+        c2 = small_f32_bench(local, args.steps, args.warmup, args.decode_steps, not args.no_cpu_baseline)
     pk = None
     if rank == 0 and world == 1 and not args.no_parakeet:
         eng.unload_model()  # free the Whisper arenas first
@@ -654,6 +709,8 @@ def main():
             out["weight_load"] = wload
         if tb:
             out["whisper_turbo"] = tb
+        if c2:
+            out["whisper_small_f32_b1"] = c2
         if pk:
             out["parakeet_v3"] = pk
         if rs:

@@ -7,9 +7,16 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-import torch  # noqa: E402  (HIP initialised by the runtime the profiler expects, as bench.py does)
+if os.environ.get("B1_TORCH"):  # initialise HIP through torch first (its bundled runtime), as bench.py does
+    import torch  # noqa: E402
 
-torch.cuda.init()
+    torch.cuda.init()
+else:  # the Rust app's configuration: the library initialises HIP itself (the system runtime)
+    import ctypes  # noqa: E402
+
+    _st = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsegv_trace.so"))
+    os.makedirs("gpurun_out", exist_ok=True)
+    _st.segv_trace_install(os.environ.get("B1_SEGV_OUT", "gpurun_out/segv_b1.txt").encode())
 
 from spittle_amd import WhisperEngine, WhisperInferenceParams, WhisperModelParams  # noqa: E402
 from spittle_amd.synth import synth_audio  # noqa: E402
@@ -21,9 +28,12 @@ if os.environ.get("B1_FULL"):  # the app's own call: whisper_full defaults (time
 else:
     p = WhisperInferenceParams(language="en", no_timestamps=True, temperature_inc=0.0, ignore_eot=True, max_new_tokens=128)
 x = synth_audio(1000)[: int(os.environ.get("B1_SAMPLES", "480000"))]
-e.transcribe_samples(x, p)
+nb = int(os.environ.get("B1_BATCH", "1"))  # > 1: one batched call of that many chunks (C3 shape at 8)
+xs = [synth_audio(1000 + i)[: len(x)] for i in range(nb)]
+run = (lambda: e.transcribe_samples(x, p)) if nb == 1 else (lambda: e.transcribe_batch(xs, p))
+run()
 for _ in range(3):
-    e.transcribe_samples(x, p)
+    run()
 t = e.timings()
 cs = e.call_stats()
 print(json.dumps({"persistent": os.environ.get("SPT_PERSISTENT", "0"), "decode_ms": t["decode_ms"],

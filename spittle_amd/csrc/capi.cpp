@@ -524,6 +524,8 @@ spt_status spt_transcribe_batch(spt_ctx* ctx, const float* const* pcm, const siz
         }
         return SPT_OK;
     } catch (const std::exception& e) {
+        // run_full may throw after run_windows filled out[]: no partial results with a failure status
+        for (size_t u = 0; u < batch; ++u) { spt_result_free(out[u]); out[u] = nullptr; }
         return fail(ctx, classify(e), e.what());
     }
 }

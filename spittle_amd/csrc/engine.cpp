@@ -99,6 +99,7 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     if (const char* g = getenv("SPT_DECODE_GROUPS")) n_groups_ = std::max(1, std::min(4, atoi(g)));
     if (const char* v = getenv("SPT_XATTN_SPLIT")) xsplit_ = std::max(1, std::min(4, atoi(v)));
     if (const char* v = getenv("SPT_PERSISTENT")) pd_env_ = atoi(v) != 0;
+    if (const char* v = getenv("SPT_PD_STAMP")) pd_stamp_path_ = v;
     pd_able_ = pdec_unsupported(dt_, dm_.d, dm_.n_head, 1, dm_.n_text_ctx, dm_.n_audio_ctx).empty();
     // cross-attention key split: fixed per engine (never per batch).  The fc2 K split (2; r1
     // exp14 measured 2 slightly faster per layer than 4: the next QKV LayerNorm prologue sums
@@ -180,6 +181,8 @@ void Engine::release() {
     if (kvtmp_) (void)hipFree(kvtmp_);
     if (pd_layers_) (void)hipFree(pd_layers_);
     pd_layers_ = nullptr;
+    if (pd_stamps_) (void)hipFree(pd_stamps_);
+    pd_stamps_ = nullptr;
     for (void* p : {(void*)upcm_, (void*)umel_, (void*)uinfo_})
         if (p) (void)hipFree(p);
     upcm_ = umel_ = nullptr;
@@ -953,6 +956,16 @@ float* Engine::enqueue_layers(DecGroup& g, int E, int Tq) {
         p.kvrow = mapped ? g.kvrow : nullptr;
         p.skv = g.skv; p.self_layer = self_layer;
         p.x = g.dx; p.xo = g.dx2; p.pend = g.pend; p.ds = g.ds; p.gran = g.gran; p.ctl = g.pctl;
+        if (!pd_stamp_path_.empty()) {
+            int ncu = 0;
+            HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev_));
+            if (!pd_stamps_) {
+                const size_t n = (size_t)ncu * kPdStampMax * kPdStampRec * 8;
+                HIP_CHECK(hipMalloc(&pd_stamps_, n));
+                HIP_CHECK(hipMemset(pd_stamps_, 0, n));
+            }
+            p.stamps = pd_stamps_;
+        }
         pdec_launch(p, st);
         hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
         HIP_CHECK(hipStreamIsCapturing(st, &cap));
@@ -1391,6 +1404,17 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
     }
 }
 
+void Engine::dump_pd_stamps() {
+    int ncu = 0;
+    HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev_));
+    std::vector<unsigned long long> h((size_t)ncu * kPdStampMax * kPdStampRec);
+    HIP_CHECK(hipMemcpy(h.data(), pd_stamps_, h.size() * 8, hipMemcpyDeviceToHost));
+    if (FILE* f = fopen(pd_stamp_path_.c_str(), "wb")) {
+        fwrite(h.data(), 8, h.size(), f);
+        fclose(f);
+    }
+}
+
 void Engine::decode(int B, const DecodeRequest& rq, int* tokens, float* top1, float* top2, int* lang_out,
                     int* ts_state_out) {
     select();
@@ -1406,6 +1430,7 @@ void Engine::decode(int B, const DecodeRequest& rq, int* tokens, float* top1, fl
     HIP_CHECK(hipEventRecord(ev_[7], st_));
     HIP_CHECK(hipStreamSynchronize(st_));
     HIP_CHECK(hipGetLastError());
+    if (pd_stamps_ && pd_active_) dump_pd_stamps();
     if (gave_up || (pd_active_ && pd_err_host_ != 0)) {
         // the persistent pass could not hold every CU (another context's or process's kernels ran
         // beside it) and gave up: the whole call again on the launch chain (re-runs are idempotent:

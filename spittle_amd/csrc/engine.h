@@ -231,6 +231,11 @@ private:
     bool pd_fallback_ = false;   // re-running a call whose persistent pass gave up (the chain instead)
     PdLayer* pd_layers_ = nullptr;  // device copy of the decoder layers' pointers
     unsigned pd_err_host_ = 0;      // the last call's error word (read back with the tokens)
+    // SPT_PD_STAMP=<file>: per-unit stage stamps of every persistent pass (k_pdec.hip), the last
+    // pass of each decode call written to <file> (u64 [CUs][kPdStampMax][kPdStampRec])
+    unsigned long long* pd_stamps_ = nullptr;
+    std::string pd_stamp_path_;
+    void dump_pd_stamps();
 
     ModelDims dm_;
     int dt_, dev_, max_batch_;

@@ -125,6 +125,11 @@ __device__ __forceinline__ bool poll(const PdArgs& a, __amdgpu_buffer_rsrc_t rs,
     }
 }
 
+// diagnostics: field f of this workgroup's k-th unit record (lane 0 of the calling wave), SPT_PD_STAMP
+__device__ __forceinline__ void stamp(const PdArgs& a, int wg, int k, int f, u64 v, int lane) {
+    if (lane == 0 && k < kPdStampMax) a.stamps[((size_t)wg * kPdStampMax + k) * kPdStampRec + f] = v;
+}
+
 // ------------------------------------------------------------------ geometry helpers
 struct Cur { int l, s, u; };
 
@@ -481,9 +486,15 @@ __device__ __forceinline__ void gather_loop(const PdArgs& a, const Smem& sm, uns
     Cur c{0, 0, unit0(a, 0, 0, wg) - a.nwg};
     bool has = advance(a, wg, c);
     int img_key = -1;  // (layer, stage) of the A image in LDS
+    const bool stp = a.stamps != nullptr && wave == 0;
+    int nk = 0;  // units this workgroup has run (stamp record index)
     while (has) {
         const PdLayer& Lw = a.layers[c.l];
         const int key = (c.l << 4) | c.s;
+        if (stp) {
+            stamp(a, wg, nk, 0, (u64)c.l | ((u64)c.s << 8) | ((u64)c.u << 16), lane);
+            stamp(a, wg, nk, 1, wall_clock64(), lane);
+        }
         const bool need_img = img_key != key;
         bool ok = true;
         switch (c.s) {
@@ -530,6 +541,7 @@ __device__ __forceinline__ void gather_loop(const PdArgs& a, const Smem& sm, uns
                 break;
         }
         if (!ok) sm.misc[0] = 1u;
+        if (stp) stamp(a, wg, nk, 2, wall_clock64(), lane);
         // the epilogue's operands, fetched ahead (wave 0): the bias of this unit's columns
         float bv = 0.f;
         const unsigned ep = ep_of(launch, L, c.l, c.s);
@@ -572,6 +584,7 @@ __device__ __forceinline__ void gather_loop(const PdArgs& a, const Smem& sm, uns
         }
         if (c.s == S_E) __syncthreads();  // E mid: the first halves' softmax state in LDS
         __syncthreads();  // B: chain partials / attention partials in LDS
+        if (stp) stamp(a, wg, nk, 5, wall_clock64(), lane);
         // ---------------- epilogue + publish (gather wave 0)
         if (wave == 0) {
             float resv[4] = {0.f, 0.f, 0.f, 0.f};
@@ -687,6 +700,11 @@ __device__ __forceinline__ void gather_loop(const PdArgs& a, const Smem& sm, uns
                 if (!(lane & 1)) gran_put(a.gran, a.go[G_A] + (int64_t)b * (a.d / 2) + 32 * h + lane / 2, ep, mine | (nb << 16));
             }
         }
+        if (stp) {  // the publish has landed (diagnostic builds of a pass only: waits for the stores)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            stamp(a, wg, nk, 7, wall_clock64(), lane);
+        }
+        ++nk;
         has = advance(a, wg, c);
     }
 }
@@ -702,6 +720,8 @@ __device__ __forceinline__ void compute_loop(const PdArgs& a, const Smem& sm, un
     Cur c{0, 0, unit0(a, 0, 0, wg) - a.nwg};
     bool has = advance(a, wg, c);
     u32x4 pre[PNPRE];
+    const bool stp = a.stamps != nullptr && cw == 0;
+    int nk = 0;
     if (has) prefetch(a, c, cw, lane, pos0, pre);
     while (has) {
         const PdLayer& Lw = a.layers[c.l];
@@ -710,6 +730,11 @@ __device__ __forceinline__ void compute_loop(const PdArgs& a, const Smem& sm, un
         const bool nhas = advance(a, wg, nx);
         __syncthreads();  // A: inputs in LDS
         if (sm.misc[0]) break;
+        if (stp) {  // after barrier A, then once this unit's prefetched operands have landed
+            stamp(a, wg, nk, 3, wall_clock64(), lane);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            stamp(a, wg, nk, 4, wall_clock64(), lane);
+        }
         if (is_gemv(c.s)) {
             const Gv g = gv_of(a, Lw, c.s, c.u);
             const int ld = g.K + 8;
@@ -835,6 +860,8 @@ __device__ __forceinline__ void compute_loop(const PdArgs& a, const Smem& sm, un
                 }
             }
         }
+        if (stp) stamp(a, wg, nk, 6, wall_clock64(), lane);
+        ++nk;
         if (nhas) prefetch(a, nx, cw, lane, pos0, pre);
         __syncthreads();  // B: chain partials / attention partials in LDS; the image is free again
         c = nx;

@@ -232,6 +232,8 @@ struct PdArgs {
     const DecState* ds;
     unsigned long long* gran;                 // granule arena: pdec_granules() words, zeroed per call
     unsigned* ctl;                            // [4] census, exits, error, launch index (zeroed per call)
+    unsigned long long* stamps;               // diagnostics (SPT_PD_STAMP): per workgroup kPdStampMax
+                                              // records of kPdStampRec s_memrealtime words, or null
     // geometry (pdec_launch fills it)
     int nwg, e_vw, nss, U;
     int n[kPdStages], pre[kPdStages], ks[kPdStages];
@@ -239,6 +241,10 @@ struct PdArgs {
 };
 int64_t pdec_granules(int R, int d, int H);
 constexpr int kPdCtlWords = 4;
+// per-unit stage stamps (100 MHz s_memrealtime) of one pass, record = {meta = l | s << 8 | u << 16,
+// gather start, gather wave 0 inputs ready, compute after barrier A, compute weights landed, gather
+// after barrier B, compute done, publish landed}
+constexpr int kPdStampRec = 8, kPdStampMax = 512;
 // empty string if the persistent pass can run this geometry, else why not
 std::string pdec_unsupported(int dtype, int d, int H, int R, int ctx, int T_enc);
 void pdec_launch(PdArgs a, hipStream_t st);
