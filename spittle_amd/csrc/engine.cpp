@@ -100,6 +100,8 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     if (const char* v = getenv("SPT_XATTN_SPLIT")) xsplit_ = std::max(1, std::min(4, atoi(v)));
     if (const char* v = getenv("SPT_PERSISTENT")) pd_env_ = atoi(v) != 0;
     if (const char* v = getenv("SPT_PD_STAMP")) pd_stamp_path_ = v;
+    // the encoder's LayerNorm fold (SPT_LN_FOLD=0: separate LayerNorm launches)
+    lnf_on_ = dm_.n_enc > 0 && dm_.d % 64 == 0 && dm_.d <= 1280 && !(getenv("SPT_LN_FOLD") && atoi(getenv("SPT_LN_FOLD")) == 0);
     pd_able_ = pdec_unsupported(dt_, dm_.d, dm_.n_head, 1, dm_.n_text_ctx, dm_.n_audio_ctx).empty();
     // cross-attention key split: fixed per engine (never per batch).  The fc2 K split (2; r1
     // exp14 measured 2 slightly faster per layer than 4: the next QKV LayerNorm prologue sums
@@ -125,6 +127,13 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
         gemv_prepare(dt_);
         gemm_prepare();  // > 64 KiB LDS attributes on this device, before any capture
         if (pd_able_) pdec_prepare();
+        if (pd_able_ && !pd_stamp_path_.empty()) {
+            int ncu = 0;
+            HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev_));
+            const size_t n = (size_t)ncu * kPdStampMax * kPdStampRec * 8;
+            HIP_CHECK(hipMalloc(&pd_stamps_, n));
+            HIP_CHECK(hipMemset(pd_stamps_, 0, n));
+        }
         alloc_weights();
         if (pd_able_) {  // the persistent pass reads each layer's weight pointers from device memory
             std::vector<PdLayer> t(dm_.n_dec);
@@ -145,6 +154,8 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
             generate_weights();
         }
         weights_ready_ = !external_weights;
+        lnf_ready_ = false;
+        if (lnf_on_) HIP_CHECK(hipMalloc(&lnf_tab_, (size_t)dm_.n_enc * 14 * dm_.d * 4));
         upload_tables(src ? &src->mel_filters() : nullptr);
         alloc_workspace();
         HIP_CHECK(hipStreamSynchronize(st_));
@@ -183,6 +194,8 @@ void Engine::release() {
     pd_layers_ = nullptr;
     if (pd_stamps_) (void)hipFree(pd_stamps_);
     pd_stamps_ = nullptr;
+    if (lnf_tab_) (void)hipFree(lnf_tab_);
+    lnf_tab_ = nullptr;
     for (void* p : {(void*)upcm_, (void*)umel_, (void*)uinfo_})
         if (p) (void)hipFree(p);
     upcm_ = umel_ = nullptr;
@@ -229,12 +242,14 @@ void Engine::import_weights(const void* dev_src, int64_t bytes) {
     HIP_CHECK(hipMemcpyAsync(warena_, dev_src, (size_t)wbytes_, hipMemcpyDeviceToDevice, st_));
     HIP_CHECK(hipStreamSynchronize(st_));
     weights_ready_ = true;
+    lnf_ready_ = false;
 }
 
 void Engine::commit_weights() {
     select();
     HIP_CHECK(hipDeviceSynchronize());  // the writer may have used any stream of this device
     weights_ready_ = true;
+    lnf_ready_ = false;
 }
 
 void Engine::alloc_weights() {
@@ -590,6 +605,7 @@ void Engine::alloc_workspace() {
         ao_ = A(B * T * d);
         ff_ = A(B * T * 4 * d);
         enc_out_ = A(B * T * d);
+        lnf_part_ = (float2*)c.take(B * T * (d / kLnfGroup) * 8);
         ckv_ = A(L * kv_layer_elems((int)B, dm_.n_head, (int)T));
         suppress_ = (uint32_t*)c.take((V / 32 + 1) * 4);
         suppress_lang_ = (uint32_t*)c.take((V / 32 + 1) * 4);
@@ -766,6 +782,7 @@ void Engine::upload_windows(const int* utt, const int* seek, int E) {
 void Engine::encode_windows(const int* utt, const int* seek, int E) {
     select();
     require_weights();
+    ensure_lnf_tables();
     upload_windows(utt, seek, E);
     HIP_CHECK(hipEventRecord(ev_[2], st_));
     mel_norm(dt_, umel_, umax_, mu_, win_utt_, win_seek_, E, dm_.n_mels, cp_, mel_in_, nullptr, st_);
@@ -779,8 +796,71 @@ void Engine::encode_windows(const int* utt, const int* seek, int E) {
     cs_.encoder_windows += E;
 }
 
+// One encoder layer over the Bg windows starting at row r0 (whisper_build_graph_encoder's block:
+// LN1 -> q/k/v -> attention -> out-proj + residual -> LN2 -> fc1 + GELU -> fc2 + residual).  With the
+// LayerNorm fold (lnf_on_) no LayerNorm launches: the residual producers (conv2 /
+// the previous fc2, out-proj) also write x o gamma and per-row 32-column partials, and q/k/v / fc1
+// apply the normalisation in their epilogues through the fold tables.  The last layer's fc2 leaves x
+// for ln_post.  probe: 4 / 5 -> events e0 / e1 around fc1 / the attention (spt_probe_kernel).
+void Engine::enc_layer(int l, int Bg, int64_t r0, hipStream_t s, int probe, hipEvent_t e0, hipEvent_t e1) {
+    const int d = dm_.d, T = dm_.n_audio_ctx, H = dm_.n_head, M = Bg * T;
+    const EncL& e = enc_[l];
+    auto rows = [&](void* base, int64_t ld, int es) { return (void*)((char*)base + r0 * ld * es); };
+    float* x = (float*)rows(x_, d, 4);
+    void* xn = rows(xn_, d, esz_);
+    void* qkv = rows(qkv_, 3 * d, esz_);
+    void* ao = rows(ao_, d, esz_);
+    void* ff = rows(ff_, 4 * d, esz_);
+    float2* part = lnf_on_ ? lnf_part_ + r0 * (d / kLnfGroup) : nullptr;
+    const bool fold = lnf_on_;
+    const bool fold_next = fold && l + 1 < dm_.n_enc;
+    const float* tab = lnf_tab_ + (size_t)l * 14 * d;  // qkv gw | qkv bw | fc1 gw | fc1 bw
+    GemmArgs g{};
+    if (!fold) layernorm(dt_, x, M, d, e.ln1_w, e.ln1_b, xn, s);
+    g.A = xn; g.lda = d; g.W = e.qkv_w; g.ldw = d; g.M = M; g.N = 3 * d; g.K = d; g.bias = e.qkv_b;
+    g.C = qkv; g.ldc = 3 * d;
+    if (fold) { g.lnf_in = part; g.lnf_gw = tab; g.lnf_bw = tab + 3 * d; }
+    gemm_nt(dt_, EPI_BIAS, g, 1, s);
+    if (probe == 5) HIP_CHECK(hipEventRecord(e0, s));
+    enc_attention(dt_, qkv, Bg, T, H, ao, s);
+    if (probe == 5) HIP_CHECK(hipEventRecord(e1, s));
+    g = GemmArgs{};
+    g.A = ao; g.lda = d; g.W = e.o_w; g.ldw = d; g.M = M; g.N = d; g.K = d; g.bias = e.o_b;
+    g.C = x; g.ldc = d;
+    if (fold) { g.lnf_g = e.ln2_w; g.lnf_xg = xn; g.lnf_part = part; }
+    gemm_nt(dt_, EPI_BIAS_RESID, g, 1, s);
+    if (!fold) layernorm(dt_, x, M, d, e.ln2_w, e.ln2_b, xn, s);
+    g = GemmArgs{};
+    g.A = xn; g.lda = d; g.W = e.fc1_w; g.ldw = d; g.M = M; g.N = 4 * d; g.K = d; g.bias = e.fc1_b;
+    g.C = ff; g.ldc = 4 * d;
+    if (fold) { g.lnf_in = part; g.lnf_gw = tab + 6 * d; g.lnf_bw = tab + 10 * d; }
+    if (probe == 4) HIP_CHECK(hipEventRecord(e0, s));
+    gemm_nt(dt_, EPI_BIAS_GELU, g, 1, s);
+    if (probe == 4) HIP_CHECK(hipEventRecord(e1, s));
+    g = GemmArgs{};
+    g.A = ff; g.lda = 4 * d; g.W = e.fc2_w; g.ldw = 4 * d; g.M = M; g.N = d; g.K = 4 * d; g.bias = e.fc2_b;
+    g.C = x; g.ldc = d;
+    if (fold_next) { g.lnf_g = enc_[l + 1].ln1_w; g.lnf_xg = xn; g.lnf_part = part; }
+    gemm_nt(dt_, EPI_BIAS_RESID, g, 1, s);
+}
+
+// The LayerNorm fold's tables: per encoder layer, q/k/v's and fc1's
+// gw = W gamma and bw = b + W beta of the LayerNorm in front of them; rebuilt whenever the weights
+// change (load, import, commit), before any encoder launch that reads them.
+void Engine::ensure_lnf_tables() {
+    if (!lnf_on_ || lnf_ready_) return;
+    const int d = dm_.d;
+    for (int l = 0; l < dm_.n_enc; ++l) {
+        const EncL& e = enc_[l];
+        float* tab = lnf_tab_ + (size_t)l * 14 * d;
+        ln_fold_tables(dt_, e.qkv_w, 3 * d, d, e.ln1_w, e.ln1_b, e.qkv_b, tab, tab + 3 * d, st_);
+        ln_fold_tables(dt_, e.fc1_w, 4 * d, d, e.ln2_w, e.ln2_b, e.fc1_b, tab + 6 * d, tab + 10 * d, st_);
+    }
+    lnf_ready_ = true;
+}
+
 void Engine::run_encoder(int B) {
-    const int d = dm_.d, T = dm_.n_audio_ctx, H = dm_.n_head;
+    const int d = dm_.d, T = dm_.n_audio_ctx;
     GemmArgs g{};
     // conv1 (k3, s1, p1) + GELU -> y1p rows 1..3000
     g.A = mel_in_; g.lda = cp_; g.sA = (int64_t)MEL_ROWS * cp_;
@@ -797,6 +877,9 @@ void Engine::run_encoder(int B) {
     g.bias = conv2_b_;
     g.C = x_; g.ldc = d; g.sC = (int64_t)T * d;
     g.pos = enc_pos_;
+    if (lnf_on_) {  // LayerNorm fold: also layer 0's LN1 operand x o gamma and the row partials
+        g.lnf_g = enc_[0].ln1_w; g.lnf_xg = xn_; g.lnf_part = lnf_part_;
+    }
     gemm_nt(dt_, EPI_BIAS_GELU_POS, g, B, st_);
     // The layers run per window group, each group's rows (whole windows: every kernel below is
     // row-local or per window) on its own stream, so one group's kernels fill the CUs the other's
@@ -813,38 +896,9 @@ void Engine::run_encoder(int B) {
         for (int i = 1; i < G; ++i) HIP_CHECK(hipStreamWaitEvent(stream_of(i), enc_ev_[0], 0));
     }
     auto rows = [&](void* base, int64_t row, int64_t ld, int es) { return (char*)base + row * ld * es; };
-    for (int l = 0; l < dm_.n_enc; ++l) {
-        const EncL& e = enc_[l];
-        for (int i = 0; i < G; ++i) {  // layer l of every group before layer l + 1 of any
-            hipStream_t s = stream_of(i);
-            const int Bg = b0[i + 1] - b0[i], M = Bg * T;
-            const int64_t r0 = (int64_t)b0[i] * T;
-            float* x = (float*)rows(x_, r0, d, 4);
-            void* xn = rows(xn_, r0, d, esz_);
-            void* qkv = rows(qkv_, r0, 3 * d, esz_);
-            void* ao = rows(ao_, r0, d, esz_);
-            void* ff = rows(ff_, r0, 4 * d, esz_);
-            layernorm(dt_, x, M, d, e.ln1_w, e.ln1_b, xn, s);
-            g = GemmArgs{};
-            g.A = xn; g.lda = d; g.W = e.qkv_w; g.ldw = d; g.M = M; g.N = 3 * d; g.K = d; g.bias = e.qkv_b;
-            g.C = qkv; g.ldc = 3 * d;
-            gemm_nt(dt_, EPI_BIAS, g, 1, s);
-            enc_attention(dt_, qkv, Bg, T, H, ao, s);
-            g = GemmArgs{};
-            g.A = ao; g.lda = d; g.W = e.o_w; g.ldw = d; g.M = M; g.N = d; g.K = d; g.bias = e.o_b;
-            g.C = x; g.ldc = d;
-            gemm_nt(dt_, EPI_BIAS_RESID, g, 1, s);
-            layernorm(dt_, x, M, d, e.ln2_w, e.ln2_b, xn, s);
-            g = GemmArgs{};
-            g.A = xn; g.lda = d; g.W = e.fc1_w; g.ldw = d; g.M = M; g.N = 4 * d; g.K = d; g.bias = e.fc1_b;
-            g.C = ff; g.ldc = 4 * d;
-            gemm_nt(dt_, EPI_BIAS_GELU, g, 1, s);
-            g = GemmArgs{};
-            g.A = ff; g.lda = 4 * d; g.W = e.fc2_w; g.ldw = 4 * d; g.M = M; g.N = d; g.K = 4 * d; g.bias = e.fc2_b;
-            g.C = x; g.ldc = d;
-            gemm_nt(dt_, EPI_BIAS_RESID, g, 1, s);
-        }
-    }
+    for (int l = 0; l < dm_.n_enc; ++l)
+        for (int i = 0; i < G; ++i)  // layer l of every group before layer l + 1 of any
+            enc_layer(l, b0[i + 1] - b0[i], (int64_t)b0[i] * T, stream_of(i));
     for (int i = 0; i < G; ++i) {
         const int64_t r0 = (int64_t)b0[i] * T;
         layernorm(dt_, (float*)rows(x_, r0, d, 4), (b0[i + 1] - b0[i]) * T, d, lnp_w_, lnp_b_,
@@ -956,16 +1010,7 @@ float* Engine::enqueue_layers(DecGroup& g, int E, int Tq) {
         p.kvrow = mapped ? g.kvrow : nullptr;
         p.skv = g.skv; p.self_layer = self_layer;
         p.x = g.dx; p.xo = g.dx2; p.pend = g.pend; p.ds = g.ds; p.gran = g.gran; p.ctl = g.pctl;
-        if (!pd_stamp_path_.empty()) {
-            int ncu = 0;
-            HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev_));
-            if (!pd_stamps_) {
-                const size_t n = (size_t)ncu * kPdStampMax * kPdStampRec * 8;
-                HIP_CHECK(hipMalloc(&pd_stamps_, n));
-                HIP_CHECK(hipMemset(pd_stamps_, 0, n));
-            }
-            p.stamps = pd_stamps_;
-        }
+        p.stamps = pd_stamps_;  // SPT_PD_STAMP (allocated with the engine), else null
         pdec_launch(p, st);
         hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
         HIP_CHECK(hipStreamIsCapturing(st, &cap));
@@ -1665,6 +1710,7 @@ void Engine::debug_mel(const float* pcm_host, int n, int seek, float* out_host) 
 void Engine::debug_encode(const float* mel_host, float* out_host) {
     select();
     require_weights();
+    ensure_lnf_tables();
     const int nm = dm_.n_mels, d = dm_.d, T = dm_.n_audio_ctx;
     std::vector<char> img((size_t)MEL_ROWS * cp_ * esz_, 0);
     for (int t = 0; t < 3000; ++t)
@@ -1755,10 +1801,12 @@ double Engine::probe(int kind, int iters, double* work, int* is_flops) {
             break;
         }
         case 4: {
+            ensure_lnf_tables();
             launch = [&] {
                 GemmArgs a{};
                 a.A = xn_; a.lda = d; a.W = enc_[0].fc1_w; a.ldw = d; a.M = B * T; a.N = 4 * d; a.K = d;
                 a.bias = enc_[0].fc1_b; a.C = ff_; a.ldc = 4 * d;
+                if (lnf_on_) { a.lnf_in = lnf_part_; a.lnf_gw = lnf_tab_ + 6 * d; a.lnf_bw = lnf_tab_ + 10 * d; }
                 gemm_nt(dt_, EPI_BIAS_GELU, a, 1, st_);
             };
             *work = 2.0 * B * T * 4.0 * d * d;
@@ -1851,15 +1899,14 @@ double Engine::probe(int kind, int iters, double* work, int* is_flops) {
     }
     if (kind == 4 || kind == 5) {
         // encoder kernels inside the encoder's own sequence: `iters` back-to-back runs of encoder
-        // layer 0's eight launches on the last call's buffers (LayerNorm 1, q/k/v, attention, out,
-        // LayerNorm 2, fc1, fc2), with an event pair around the probed kernel of each run and one
+        // layer 0's launches on the last call's buffers (enc_layer: q/k/v, attention, out, fc1,
+        // fc2, with the LayerNorms folded or, SPT_LN_FOLD=0, in front of q/k/v and fc1), with an event pair around the probed kernel of each run and one
         // host wait at the end, so the kernel follows its producer, on a chip as busy (and as hot)
         // as inside the encoder.  r4's back-to-back repeats of the kernel alone read the attention
         // 10 % below its rocprofv3 average, r5's producer-then-kernel pairs with a host wait
         // between them 8 % below.  The residual rows x grow by one layer per run: the probe runs
         // after the timed calls, and every call recomputes them.
-        const EncL& e = enc_[0];
-        const int M = B * T;
+        ensure_lnf_tables();
         if ((int)probe_ev_.size() < 2 * iters) {
             for (int i = (int)probe_ev_.size(); i < 2 * iters; ++i) {
                 hipEvent_t ev;
@@ -1867,24 +1914,7 @@ double Engine::probe(int kind, int iters, double* work, int* is_flops) {
                 probe_ev_.push_back(ev);
             }
         }
-        auto gemm = [&](const void* A, int lda, const void* W, int N, int K, const float* bias, void* C, int ldc, int epi) {
-            GemmArgs a{};
-            a.A = A; a.lda = lda; a.W = W; a.ldw = K; a.M = M; a.N = N; a.K = K; a.bias = bias; a.C = C; a.ldc = ldc;
-            gemm_nt(dt_, epi, a, 1, st_);
-        };
-        for (int i = 0; i < iters; ++i) {
-            layernorm(dt_, x_, M, d, e.ln1_w, e.ln1_b, xn_, st_);
-            gemm(xn_, d, e.qkv_w, 3 * d, d, e.qkv_b, qkv_, 3 * d, EPI_BIAS);
-            if (kind == 5) HIP_CHECK(hipEventRecord(probe_ev_[2 * i], st_));
-            enc_attention(dt_, qkv_, B, T, H, ao_, st_);
-            if (kind == 5) HIP_CHECK(hipEventRecord(probe_ev_[2 * i + 1], st_));
-            gemm(ao_, d, e.o_w, d, d, e.o_b, x_, d, EPI_BIAS_RESID);
-            layernorm(dt_, x_, M, d, e.ln2_w, e.ln2_b, xn_, st_);
-            if (kind == 4) HIP_CHECK(hipEventRecord(probe_ev_[2 * i], st_));
-            gemm(xn_, d, e.fc1_w, 4 * d, d, e.fc1_b, ff_, 4 * d, EPI_BIAS_GELU);
-            if (kind == 4) HIP_CHECK(hipEventRecord(probe_ev_[2 * i + 1], st_));
-            gemm(ff_, 4 * d, e.fc2_w, d, 4 * d, e.fc2_b, x_, d, EPI_BIAS_RESID);
-        }
+        for (int i = 0; i < iters; ++i) enc_layer(0, B, 0, st_, kind, probe_ev_[2 * i], probe_ev_[2 * i + 1]);
         HIP_CHECK(hipStreamSynchronize(st_));
         double tot = 0.0;
         for (int i = 0; i < iters; ++i) {

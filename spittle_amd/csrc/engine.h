@@ -212,6 +212,13 @@ private:
     void upload_windows(const int* utt, const int* seek, int E);
     void finish_call_timing();
     void run_encoder(int B);
+    void enc_layer(int l, int Bg, int64_t r0, hipStream_t s, int probe = 0, hipEvent_t e0 = nullptr,
+                   hipEvent_t e1 = nullptr);
+    void ensure_lnf_tables();
+    // the encoder's LayerNorm fold: on unless SPT_LN_FOLD=0 (or the width does not fit)
+    bool lnf_on_ = false, lnf_ready_ = false;
+    float* lnf_tab_ = nullptr;      // [n_enc][qkv gw 3d | qkv bw 3d | fc1 gw 4d | fc1 bw 4d]
+    float2* lnf_part_ = nullptr;    // workspace: [B * T][d / 32] row partials
     void enqueue_encoder(int B);  // run_encoder, replayed from a per-B graph after the first call
     void run_cross_kv(int B);
     void run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1, float* top2, int* lang_out,

@@ -601,466 +601,6 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_q64_kernel(const bf16* __res
     }
 }
 
-// -------------------------------------------------------------------- bf16, 32 queries per wave
-// attn_bf16_q64_kernel<4, 3>'s arithmetic for one 32-query block per wave (a wave's softmax
-// decisions are per 32-query block in both, so the output is bitwise the same), with the fewer
-// registers that buys: up to three 4-wave workgroups per CU, three waves per SIMD to interleave
-// the per-tile dependency chain (QK^T -> softmax -> PV -> barrier) instead of two.  Every K and V
-// fragment feeds one MFMA instead of two (twice the LDS reads per flop).
-__global__ __launch_bounds__(256, 3) void attn_bf16_q32s_kernel(const bf16* __restrict__ qkv, int T, int H,
-                                                                bf16* __restrict__ out) {
-    constexpr int SW = 3;
-    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128];  // [buf][K|V][64 keys][128 B]
-    const int d = H * 64, ld = 3 * d;
-    const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int l32 = lane & 31, hf = lane >> 5;
-    const bf16* base = qkv + (size_t)b * T * ld;
-    const int q_abs = qt * 128 + wid * 32 + l32;
-
-    bf16x8 qf[4];
-    {
-        const bf16* qp = base + (size_t)min(q_abs, T - 1) * ld + h * 64;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            qf[s] = *(const bf16x8*)(qp + 16 * s + 8 * hf);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) qf[s][e] = (short)f2bf(bf2f((bf16)qf[s][e]) * kScaleLog2);
-        }
-    }
-    auto lds_k = [&](int buf) -> SPT_LDS char* { return (SPT_LDS char*)smem + (buf * 2 + 0) * 8192; };
-    auto lds_v = [&](int buf) -> SPT_LDS char* { return (SPT_LDS char*)smem + (buf * 2 + 1) * 8192; };
-    const int prow = lane >> 3, pch = lane & 7;
-    auto stage = [&](int buf, int kt) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int p = wid * 2 + i;
-            const int rt = 8 * p + prow;
-            const int key = min(kt * 64 + rt, T - 1);
-            const bf16* kr = base + (size_t)key * ld + d + h * 64;
-            glds16(kr + 8 * (pch ^ kswz<SW>(rt)), lds_k(buf) + p * 1024);
-            glds16(kr + d + 8 * (pch ^ vswz<SW>(rt)), lds_v(buf) + p * 1024);
-        }
-    };
-    const uint32_t lk0 = (uint32_t)(prow * ld * 2) + ((pch ^ (prow >> 1)) << 4);
-    const uint32_t lv0 = (uint32_t)(prow * ld * 2) + ((pch ^ ((prow & 2) << 1)) << 4);
-    auto stage_full = [&](int buf, int kt) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int p = wid * 2 + i;
-            const char* row = (const char*)(base + (size_t)(kt * 64 + 8 * p) * ld + d + h * 64);
-            glds16(row + (i ? (lk0 ^ 64u) : lk0), lds_k(buf) + p * 1024);
-            glds16(row + 2 * d + lv0, lds_v(buf) + p * 1024);
-        }
-    };
-
-    float m_run = -INFINITY, lsum = 0.f;
-    f32x16 o[2], cinit;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; cinit[i] = 0.f; }
-    const int nkt = cdiv(T, 64);
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    const int g = lane >> 4, i16 = lane & 15;
-    const int kl = 4 * hf + (i16 >> 2);
-    const int sb = (kl >> 1) & 1;
-    const int cl = 2 * (g & 1) + ((i16 & 3) >> 1), c8 = 8 * (i16 & 1);
-    auto tile = [&](const int kt, const int cur) __attribute__((always_inline)) {
-        if (kt + 1 < nkt) {
-            if ((kt + 1) * 64 + 64 <= T) stage_full(cur ^ 1, kt + 1);
-            else stage(cur ^ 1, kt + 1);
-        }
-        const SPT_LDS char* lk = lds_k(cur);
-        const SPT_LDS char* lv = lds_v(cur);
-        f32x16 s[2];
-#pragma unroll
-        for (int kt2 = 0; kt2 < 2; ++kt2) {
-            const int row = 32 * kt2 + l32;
-#pragma unroll
-            for (int st = 0; st < 4; ++st) {
-                const int c = 2 * st + hf;
-                const bf16x8 a = *(const SPT_LDS bf16x8*)(lk + row * 128 + ((c ^ kswz<SW>(row)) << 4));
-                s[kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[st], st == 0 ? cinit : s[kt2], 0, 0, 0);
-            }
-        }
-        if (kt * 64 + 64 > T) {
-#pragma unroll
-            for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    if (kt * 64 + key_of(kt2, r, hf) >= T) s[kt2][r] = -INFINITY;
-        }
-        union { bf16x8 v; uint32_t w[4]; } pu[2][2];
-        auto expo = [&](float sub) {
-            float l0 = 0.f, l1 = 0.f;
-#pragma unroll
-            for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                for (int r = 0; r < 16; r += 2) {
-                    const float p0 = __builtin_amdgcn_exp2f(s[kt2][r] - sub);
-                    const float p1 = __builtin_amdgcn_exp2f(s[kt2][r + 1] - sub);
-                    l0 += p0;
-                    l1 += p1;
-                    const f32x2 pv = {p0, p1};
-                    pu[kt2][r >> 3].w[(r & 7) >> 1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pv, bf16x2v));
-                }
-            return l0 + l1;
-        };
-        auto expo0 = [&]() {
-            float l0 = 0.f, l1 = 0.f;
-#pragma unroll
-            for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                for (int r = 0; r < 16; r += 2) {
-                    const float p0 = __builtin_amdgcn_exp2f(s[kt2][r]);
-                    const float p1 = __builtin_amdgcn_exp2f(s[kt2][r + 1]);
-                    l0 += p0;
-                    l1 += p1;
-                    const f32x2 pv = {p0, p1};
-                    pu[kt2][r >> 3].w[(r & 7) >> 1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pv, bf16x2v));
-                }
-            return l0 + l1;
-        };
-        float lt = kt > 0 ? expo0() : INFINITY;
-        if (__any(!(lt <= 4096.0f))) {
-            float mloc = -INFINITY;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) mloc = max3f(mloc, s[0][r], s[1][r]);
-            mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-            float delta, alpha;
-            if (kt == 0) {
-                delta = mloc;
-                alpha = 0.f;
-                m_run = mloc;
-            } else {
-                delta = fmaxf(mloc, 0.f);
-                alpha = __builtin_amdgcn_exp2f(-delta);
-                m_run += delta;
-            }
-#pragma unroll
-            for (int i = 0; i < 16; ++i) cinit[i] = -m_run;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
-            lsum *= alpha;
-            lt = expo(delta);
-        }
-        lsum += lt;
-        bf16x8 pf[2][2];
-#pragma unroll
-        for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-            for (int sp = 0; sp < 2; ++sp) pf[kt2][sp] = pu[kt2][sp].v;
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-            const SPT_LDS char* vb = lv + kl * 128 + ((4 * (dt ^ sb) + cl) << 4) + c8;
-            bf16x4v lo[2][2], hi[2][2];
-            lo[0][0] = ds_tr16_asm<0>(vb);
-            hi[0][0] = ds_tr16_asm<1024>(vb);
-            lo[0][1] = ds_tr16_asm<2048>(vb);
-            hi[0][1] = ds_tr16_asm<3072>(vb);
-            lo[1][0] = ds_tr16_asm<4096>(vb);
-            hi[1][0] = ds_tr16_asm<5120>(vb);
-            lo[1][1] = ds_tr16_asm<6144>(vb);
-            hi[1][1] = ds_tr16_asm<7168>(vb);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                for (int sp = 0; sp < 2; ++sp) {
-                    const bf16x8 va = __builtin_shufflevector(lo[kt2][sp], hi[kt2][sp], 0, 1, 2, 3, 4, 5, 6, 7);
-                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pf[kt2][sp], o[dt], 0, 0, 0);
-                }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    };
-    for (int kt = 0; kt < nkt; kt += 2) {
-        tile(kt, 0);
-        if (kt + 1 < nkt) tile(kt + 1, 1);
-    }
-    const float inv = 1.0f / (lsum + __shfl_xor(lsum, 32, 64));
-    if (q_abs < T) {
-        bf16* orow = out + ((size_t)b * T + q_abs) * d + h * 64;
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-            for (int gg = 0; gg < 4; ++gg) {
-                const int dd = 32 * dt + 8 * gg + 4 * hf;
-                *(uint2*)(orow + dd) = make_uint2(pack_bf2(o[dt][4 * gg + 0] * inv, o[dt][4 * gg + 1] * inv),
-                                                  pack_bf2(o[dt][4 * gg + 2] * inv, o[dt][4 * gg + 3] * inv));
-            }
-    }
-}
-
-// -------------------------------------------------------------------- bf16, ping-pong wave groups
-// attn_bf16_q64_kernel<4, 3, true>'s arithmetic, operation for operation (bitwise its output), in a
-// 512-thread workgroup whose two 4-wave groups (A = waves 0-3, B = waves 4-7; one of each per SIMD)
-// own 256 queries each and run one barrier interval apart, so on every SIMD one wave's MFMAs run
-// beside the other's softmax VALU (MI355X_MICROARCH "Two waves per SIMD").  Per K/V tile j a wave
-// runs two segments:
-//   S1(j): mask + online softmax of the scores s(j) -> bf16 probabilities p(j)      (VALU)
-//   S2(j): O += V(j) . p(j), then s(j + 1) = K(j + 1) . Q (from -m)                  (MFMA)
-// Interval t (between barriers t - 1 and t): A runs S1(j) at t = 2j + 1 and S2(j) at 2j + 2 (and
-// s(0) at t = 0); B runs everything one interval later.  K and V each have a 3-slot LDS ring; the
-// DMA batch of even interval 2i (every wave one K piece of tile i + 2 and one V piece of tile i + 1)
-// is waited for at the end of interval 2i + 3 (vmcnt(2): the batch of 2i + 2 stays in flight), so:
-//   K(m) lands in slot m % 3 at 2m - 4, after B's last read of K(m - 3) (S2(m - 4) at 2m - 5), and is
-//   complete before A's first read (S2(m - 1) at 2m);
-//   V(m) lands in slot m % 3 at 2m - 2, after B's last read of V(m - 3) (S2(m - 3) at 2m - 3), and is
-//   complete before A's first read (S2(m) at 2m + 2).
-// Each interval's LDS reads are consumed by MFMAs inside that interval, so they have completed at
-// its barrier, and every DMA is issued in the interval after the last read of the slot's previous
-// tile.  The softmax of tile j follows the product of tile j - 1 and precedes the scores of tile j + 1
-// in each wave, as in the one-group kernel: the same running maximum, sums and accumulator order.
-constexpr int PP_QPW = 64;  // queries per wave (two 32-query blocks)
-__global__ __launch_bounds__(512, 1) void attn_bf16_pp_kernel(const bf16* __restrict__ qkv, int T, int H,
-                                                              bf16* __restrict__ out) {
-    constexpr int SW = 3;
-    // [K slot 0..2][64 keys][128 B] [V slot 0..2][64 keys][128 B] [Q: wave][qb * 4 + s][lane] x 16 B
-    __shared__ __attribute__((aligned(16))) char smem[6 * 8192 + 8 * 8 * 64 * 16];
-    const int d = H * 64, ld = 3 * d;
-    const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int grp = __builtin_amdgcn_readfirstlane(wid >> 2);
-    const int l32 = lane & 31, hf = lane >> 5;
-    const bf16* base = qkv + (size_t)b * T * ld;
-
-    SPT_LDS bf16x8* qlds = (SPT_LDS bf16x8*)(smem + 6 * 8192) + wid * 8 * 64;
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-        const int q_abs = qt * 512 + wid * PP_QPW + 32 * qb + l32;
-        const bf16* qp = base + (size_t)min(q_abs, T - 1) * ld + h * 64;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            bf16x8 q = *(const bf16x8*)(qp + 16 * s + 8 * hf);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) q[e] = (short)f2bf(bf2f((bf16)q[e]) * kScaleLog2);
-            qlds[(qb * 4 + s) * 64 + lane] = q;
-        }
-    }
-    auto lds_k = [&](int slot) -> SPT_LDS char* { return (SPT_LDS char*)smem + slot * 8192; };
-    auto lds_v = [&](int slot) -> SPT_LDS char* { return (SPT_LDS char*)smem + (3 + slot) * 8192; };
-    const int prow = lane >> 3, pch = lane & 7;
-    const int rt = 8 * wid + prow;  // this wave's piece: rows 8 wid .. 8 wid + 7 of a tile
-    // slot = kt % 3, passed as a literal: every LDS address is a constant offset from one lane base
-    // sources: a wave-uniform base plus a 32-bit lane offset (a batch's q/k/v rows span < 2^31
-    // elements, checked by the launcher), so the DMA takes the scalar-base address form
-    const bf16* kbase = base + d + h * 64;
-    const bf16* vbase = base + 2 * d + h * 64;
-    const uint32_t kch = 8 * (pch ^ kswz<SW>(rt)), vch = 8 * (pch ^ vswz<SW>(rt));
-    auto stage_k = [&](int kt, const int slot) __attribute__((always_inline)) {
-        const uint32_t key = (uint32_t)min(kt * 64 + rt, T - 1);
-        glds16(kbase + (key * (uint32_t)ld + kch), lds_k(slot) + wid * 1024);
-    };
-    auto stage_v = [&](int kt, const int slot) __attribute__((always_inline)) {
-        const uint32_t key = (uint32_t)min(kt * 64 + rt, T - 1);
-        glds16(vbase + (key * (uint32_t)ld + vch), lds_v(slot) + wid * 1024);
-    };
-
-    float m_run[2] = {-INFINITY, -INFINITY}, lsum[2] = {0.f, 0.f};
-    f32x16 o[2][2], s[2][2], cinit[2];
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) { o[qb][0][i] = 0.f; o[qb][1][i] = 0.f; cinit[qb][i] = 0.f; }
-    bf16x8 pf[2][2][2];
-    const int nkt = cdiv(T, 64);
-
-    // s(kt) = K(kt) . Q^T from the chains' start cinit (-m; 0 before the first tile)
-    auto qk = [&](const int slot) __attribute__((always_inline)) {
-        const SPT_LDS char* lk = lds_k(slot);
-        // k-step major: the Q fragments of one k-step (8 VGPRs) at a time, each feeding 4 MFMAs
-#pragma unroll
-        for (int st = 0; st < 4; ++st) {
-            const bf16x8 q0 = qlds[st * 64 + lane], q1 = qlds[(4 + st) * 64 + lane];
-            const int c = 2 * st + hf;
-#pragma unroll
-            for (int kt2 = 0; kt2 < 2; ++kt2) {
-                const int row = 32 * kt2 + l32;
-                const bf16x8 a = *(const SPT_LDS bf16x8*)(lk + row * 128 + ((c ^ kswz<SW>(row)) << 4));
-                s[0][kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, q0, st == 0 ? cinit[0] : s[0][kt2], 0, 0, 0);
-                s[1][kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, q1, st == 0 ? cinit[1] : s[1][kt2], 0, 0, 0);
-            }
-        }
-    };
-    // mask + optimistic softmax of s(kt) -> pf (attn_bf16_q64_kernel's SUM == 4 path)
-    auto softmax = [&](int kt) __attribute__((always_inline)) {
-        if (kt * 64 + 64 > T) {
-#pragma unroll
-            for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-                for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r)
-                        if (kt * 64 + key_of(kt2, r, hf) >= T) s[qb][kt2][r] = -INFINITY;
-        }
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb) {
-            union { bf16x8 v; uint32_t w[4]; } pu[2][2];
-            auto expo = [&](float sub) {
-                float l0 = 0.f, l1 = 0.f;
-#pragma unroll
-                for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                    for (int r = 0; r < 16; r += 2) {
-                        const float p0 = __builtin_amdgcn_exp2f(s[qb][kt2][r] - sub);
-                        const float p1 = __builtin_amdgcn_exp2f(s[qb][kt2][r + 1] - sub);
-                        l0 += p0;
-                        l1 += p1;
-                        const f32x2 pv = {p0, p1};
-                        pu[kt2][r >> 3].w[(r & 7) >> 1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pv, bf16x2v));
-                    }
-                return l0 + l1;
-            };
-            auto expo0 = [&]() {
-                float l0 = 0.f, l1 = 0.f;
-#pragma unroll
-                for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                    for (int r = 0; r < 16; r += 2) {
-                        const float p0 = __builtin_amdgcn_exp2f(s[qb][kt2][r]);
-                        const float p1 = __builtin_amdgcn_exp2f(s[qb][kt2][r + 1]);
-                        l0 += p0;
-                        l1 += p1;
-                        const f32x2 pv = {p0, p1};
-                        pu[kt2][r >> 3].w[(r & 7) >> 1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pv, bf16x2v));
-                    }
-                return l0 + l1;
-            };
-            float lt = kt > 0 ? expo0() : INFINITY;
-            if (__any(!(lt <= 4096.0f))) {
-                float mloc = -INFINITY;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) mloc = max3f(mloc, s[qb][0][r], s[qb][1][r]);
-                mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-                float delta, alpha;
-                if (kt == 0) {
-                    delta = mloc;
-                    alpha = 0.f;
-                    m_run[qb] = mloc;
-                } else {
-                    delta = fmaxf(mloc, 0.f);
-                    alpha = __builtin_amdgcn_exp2f(-delta);
-                    m_run[qb] += delta;
-                }
-#pragma unroll
-                for (int i = 0; i < 16; ++i) cinit[qb][i] = -m_run[qb];
-#pragma unroll
-                for (int i = 0; i < 16; ++i) { o[qb][0][i] *= alpha; o[qb][1][i] *= alpha; }
-                lsum[qb] *= alpha;
-                lt = expo(delta);
-            }
-            lsum[qb] += lt;
-#pragma unroll
-            for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                for (int sp = 0; sp < 2; ++sp) pf[qb][kt2][sp] = pu[kt2][sp].v;
-        }
-    };
-    // O^T += V^T(kt) . P^T(kt) for both query blocks (the V^T reads as inline asm, one lgkmcnt(0)
-    // per 8, as in the one-group kernel)
-    auto pv = [&](const int slot) __attribute__((always_inline)) {
-        const SPT_LDS char* lv = lds_v(slot);
-        const int g = lane >> 4, i16 = lane & 15;
-        const int kl = 4 * hf + (i16 >> 2);
-        const int sb = (kl >> 1) & 1;
-        const int cl = 2 * (g & 1) + ((i16 & 3) >> 1), c8 = 8 * (i16 & 1);
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-            const SPT_LDS char* vb = lv + kl * 128 + ((4 * (dt ^ sb) + cl) << 4) + c8;
-            bf16x4v lo[2][2], hi[2][2];
-            lo[0][0] = ds_tr16_asm<0>(vb);
-            hi[0][0] = ds_tr16_asm<1024>(vb);
-            lo[0][1] = ds_tr16_asm<2048>(vb);
-            hi[0][1] = ds_tr16_asm<3072>(vb);
-            lo[1][0] = ds_tr16_asm<4096>(vb);
-            hi[1][0] = ds_tr16_asm<5120>(vb);
-            lo[1][1] = ds_tr16_asm<6144>(vb);
-            hi[1][1] = ds_tr16_asm<7168>(vb);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                for (int sp = 0; sp < 2; ++sp) {
-                    const bf16x8 va = __builtin_shufflevector(lo[kt2][sp], hi[kt2][sp], 0, 1, 2, 3, 4, 5, 6, 7);
-                    o[0][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pf[0][kt2][sp], o[0][dt], 0, 0, 0);
-                    o[1][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pf[1][kt2][sp], o[1][dt], 0, 0, 0);
-                }
-        }
-    };
-#define PP_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
-#define PP_WAIT() asm volatile("s_waitcnt vmcnt(2)" ::: "memory")
-    // prologue: K(0), K(1), V(0) and this wave's Q image
-    stage_k(0, 0);
-    stage_k(1, 1);
-    stage_v(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    PP_BARRIER();
-    // The loop body starts at the product of tile kt, so the scores s (64 VGPRs) live only inside an
-    // iteration and the probabilities pf (32) cross its back edge.
-    // One instruction stream for both groups (two divergent bodies made the register allocator
-    // spill): only the counted waits differ.  B issues its DMA share of a batch at the start of its
-    // own product interval, one interval after A: K(m) and V(m - 1) land in their slots after B's
-    // last read of the previous tile there (interval 2m - 5 / 2m - 3) and each group waits for its
-    // share by the end of interval 2m - 1, before A's first read.
-    // interval 0: DMA batch 0 (K(2), V(1)); A computes s(0)
-    stage_k(2, 2);
-    stage_v(1, 1);
-    if (grp == 0) qk(0);
-    PP_BARRIER();
-    if (grp == 1) {  // interval 1: B's s(0)
-        qk(0);
-        PP_WAIT();
-        PP_BARRIER();
-    }
-    softmax(0);  // A: interval 1, B: 2
-    if (grp == 0) PP_WAIT();
-    PP_BARRIER();
-    // iteration kt (c = kt % 3 as a literal): A runs intervals 2 kt + 2 (its share of DMA batch kt + 1:
-    // K(kt + 3) into slot c, V(kt + 2) into slot c + 2; O += V(kt) p(kt); s(kt + 1)) and 2 kt + 3
-    // (softmax(kt + 1)); B the next two
-    auto iter = [&](int kt, const int c) __attribute__((always_inline)) {
-        stage_k(kt + 3, c);
-        stage_v(kt + 2, (c + 2) % 3);
-        pv(c);
-        __builtin_amdgcn_sched_barrier(0);
-        qk((c + 1) % 3);  // unconditional: past the last tile, unused scores of the staged clamped rows
-        if (grp == 1) PP_WAIT();
-        PP_BARRIER();
-        if (kt + 1 < nkt) softmax(kt + 1);
-        if (grp == 0) PP_WAIT();
-        PP_BARRIER();
-    };
-    for (int kt = 0; kt < nkt; kt += 3) {
-        iter(kt, 0);
-        if (kt + 1 < nkt) iter(kt + 1, 1);
-        if (kt + 2 < nkt) iter(kt + 2, 2);
-    }
-    if (grp == 0) PP_BARRIER();  // both groups have passed the same barriers
-#undef PP_BARRIER
-#undef PP_WAIT
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-        const float inv = 1.0f / (lsum[qb] + __shfl_xor(lsum[qb], 32, 64));
-        const int q_abs = qt * 512 + wid * PP_QPW + 32 * qb + l32;
-        if (q_abs < T) {
-            bf16* orow = out + ((size_t)b * T + q_abs) * d + h * 64;
-#pragma unroll
-            for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-                for (int gg = 0; gg < 4; ++gg) {
-                    const int dd = 32 * dt + 8 * gg + 4 * hf;
-                    *(uint2*)(orow + dd) = make_uint2(pack_bf2(o[qb][dt][4 * gg + 0] * inv, o[qb][dt][4 * gg + 1] * inv),
-                                                      pack_bf2(o[qb][dt][4 * gg + 2] * inv, o[qb][dt][4 * gg + 3] * inv));
-                }
-        }
-    }
-}
-
 // -------------------------------------------------------------------- f32
 __global__ __launch_bounds__(256, 1) void attn_f32_kernel(const float* __restrict__ qkv, int T, int H,
                                                           float* __restrict__ out) {
@@ -1193,27 +733,8 @@ void enc_attention(int dtype, const void* qkv, int B, int T, int H, void* out, h
     // per-tile address arithmetic of r4); read per launch, as sum
     const char* fd_env = getenv("SPT_ATTN_FULLDMA");
     const int fulldma = !(fd_env && atoi(fd_env) == 0);
-    // 1: the ping-pong wave groups (attn_bf16_pp_kernel, bitwise the SUM = 4 / SWZ = 3 / QL kernel's
-    // output); read per launch, as sum
-    const char* pp_env = getenv("SPT_ATTN_PP");
-    const bool pp = pp_env && atoi(pp_env) != 0;
-    const bool fits32 = (int64_t)T * 3 * H * 64 < (1ll << 31);
-    if (dtype == DT_BF16 && !q32 && pp && sum == 4 && ql && swz == 3 && fits32) {
-        hipLaunchKernelGGL(attn_bf16_pp_kernel, dim3(cdiv(T, 512), H, B), dim3(512), 0, st, (const bf16*)qkv, T, H,
-                           (bf16*)out);
-        return;
-    }
-    // 1: 32 queries per wave, up to three workgroups per CU (attn_bf16_q32s_kernel, bitwise the
-    // 64-query kernel's output).  r5 exp_attn_q32s.txt: alone 3 % faster per layer (121.4-122.4 vs
-    // 125.7-126.7 us), and the encoder 1 % faster with one window group, but 1.5 % slower beside the
-    // other group's kernels (the default two groups at C3), so opt-in.  Read per launch, as sum
-    const char* q32s_env = getenv("SPT_ATTN_Q32S");
-    const bool q32s = q32s_env && atoi(q32s_env) != 0;
-    if (dtype == DT_BF16 && !q32 && q32s && ql && sum == 4 && swz == 3 && fulldma && fits32) {
-        hipLaunchKernelGGL(attn_bf16_q32s_kernel, dim3(cdiv(T, 128), H, B), dim3(256), 0, st, (const bf16*)qkv, T, H,
-                           (bf16*)out);
-        return;
-    }
+    // (r5's opt-in ping-pong wave groups and 32-query-per-wave kernels measured slower in situ and were
+    // removed in r6: DESIGN.md 4.1g keeps their numbers)
     if (dtype == DT_BF16 && !q32) {
         dim3 g(cdiv(T, 256), H, B);
         if (sum == 1) hipLaunchKernelGGL(attn_bf16_q64_kernel<1>, g, dim3(256), 0, st, (const bf16*)qkv, T, H, (bf16*)out, fulldma);

@@ -109,6 +109,114 @@ __device__ __forceinline__ void epi_store(const GemmArgs& g, int bz, int row, co
     }
 }
 
+// the f32 value epi_store writes for the f32-output epilogues that feed a LayerNorm (producers of
+// the LayerNorm fold): the same operations in the same order
+template <int EPI>
+__device__ __forceinline__ float epi_value(const GemmArgs& g, const EpiCol& e, float acc, float y) {
+#pragma clang fp contract(off)
+    const float v = acc + e.bv;
+    if constexpr (EPI == EPI_BIAS_GELU_POS) return gelu_tanh(v) + y;
+    else return y + g.alpha * v;
+}
+
+// ---- LayerNorm fold (GemmArgs lnf_*) ------------------------------------------
+// Producer: every 32-column group of a row gets {sum, sum of squared deviations from the group mean}
+// in one canonical order -- each quad of 4 consecutive columns as (c0 + c1) + (c2 + c3), then
+// pairwise over the quads (q ^ 1, q ^ 2, q ^ 4) -- whichever lanes hold the columns (float addition
+// commutes, so both partners of a butterfly step hold the same bits), so every tile shape writes the
+// same partials.  Consumer: the row's groups merged in group order.
+template <int EPI> constexpr bool lnf_producer() { return EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU_POS; }
+template <int EPI> constexpr bool lnf_consumer() { return EPI == EPI_BIAS || EPI == EPI_BIAS_GELU; }
+// the kernels' epilogue template argument: the GemmArgs epilogue, | EPI_LNF for its LayerNorm-fold
+// form (a separate instantiation: the plain kernels stay exactly as they were)
+constexpr int EPI_LNF = 16;
+constexpr int epi_base(int e) { return e & (EPI_LNF - 1); }
+constexpr int kLnfMaxG = 40;  // groups per row: d <= 1280
+
+// the 8 quads of a group in 8 lanes (quad index = lane bits 0..2): {sum, M2}, the same in every lane
+__device__ __forceinline__ float2 lnf_group8(float4 o) {
+#pragma clang fp contract(off)
+    float s = (o.x + o.y) + (o.z + o.w);
+    s = s + __shfl_xor(s, 1, 64);
+    s = s + __shfl_xor(s, 2, 64);
+    s = s + __shfl_xor(s, 4, 64);
+    const float mean = s * (1.0f / kLnfGroup);
+    const float a = o.x - mean, b = o.y - mean, c = o.z - mean, e = o.w - mean;
+    const float a2 = a * a, b2 = b * b, c2 = c * c, e2 = e * e;
+    float m = (a2 + b2) + (c2 + e2);
+    m = m + __shfl_xor(m, 1, 64);
+    m = m + __shfl_xor(m, 2, 64);
+    m = m + __shfl_xor(m, 4, 64);
+    return make_float2(s, m);
+}
+// MFMA-layout form: one column per lane (lane bits 0..1 = column within the quad, 2..3 = quad bits 0..1)
+// and the two fragments lo / hi of the group (quad bit 2) in registers
+__device__ __forceinline__ float2 lnf_group16(float lo, float hi) {
+#pragma clang fp contract(off)
+    float s0 = lo + __shfl_xor(lo, 1, 64), s1 = hi + __shfl_xor(hi, 1, 64);
+    s0 = s0 + __shfl_xor(s0, 2, 64); s1 = s1 + __shfl_xor(s1, 2, 64);
+    s0 = s0 + __shfl_xor(s0, 4, 64); s1 = s1 + __shfl_xor(s1, 4, 64);
+    s0 = s0 + __shfl_xor(s0, 8, 64); s1 = s1 + __shfl_xor(s1, 8, 64);
+    const float s = s0 + s1;
+    const float mean = s * (1.0f / kLnfGroup);
+    const float a = lo - mean, b = hi - mean;
+    float m0 = a * a, m1 = b * b;
+    m0 = m0 + __shfl_xor(m0, 1, 64); m1 = m1 + __shfl_xor(m1, 1, 64);
+    m0 = m0 + __shfl_xor(m0, 2, 64); m1 = m1 + __shfl_xor(m1, 2, 64);
+    m0 = m0 + __shfl_xor(m0, 4, 64); m1 = m1 + __shfl_xor(m1, 4, 64);
+    m0 = m0 + __shfl_xor(m0, 8, 64); m1 = m1 + __shfl_xor(m1, 8, 64);
+    return make_float2(s, m0 + m1);
+}
+__device__ __forceinline__ size_t lnf_part_index(const GemmArgs& g, int bz, int row, int col) {
+    return ((size_t)bz * g.M + row) * (size_t)(g.N / kLnfGroup) + col / kLnfGroup;
+}
+// consumer: {mean, rstd} of an A row from its G = K / 32 partials, by 4 lanes (4 r + q): lane q
+// holds groups [q G / 4, (q + 1) G / 4) (lnf_load, issued ahead of the first DMA) and sums them in
+// order; the 4 quarter sums combine as (q0 + q1) + (q2 + q3) -- one fixed order in every tile shape
+constexpr int kLnfQ = kLnfMaxG / 4;  // groups per quarter, at most
+__device__ __forceinline__ void lnf_load(const float2* part_row, int K, int q, float2 (&v)[kLnfQ]) {
+    const int gq = K / kLnfGroup / 4;
+#pragma unroll
+    for (int i = 0; i < kLnfQ; ++i) v[i] = part_row[q * gq + min(i, gq - 1)];
+}
+__device__ __forceinline__ float2 lnf_merge(const float2 (&v)[kLnfQ], int K) {
+#pragma clang fp contract(off)
+    const int gq = K / kLnfGroup / 4;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < kLnfQ; ++i)
+        if (i < gq) s = s + v[i].x;
+    s = s + __shfl_xor(s, 1, 64);
+    s = s + __shfl_xor(s, 2, 64);
+    const float mean = s / (float)K;
+    float m2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < kLnfQ; ++i)
+        if (i < gq) {
+            const float dm = v[i].x * (1.0f / kLnfGroup) - mean;
+            float t = dm * dm;
+            t = t * (float)kLnfGroup;
+            m2 = m2 + v[i].y;
+            m2 = m2 + t;
+        }
+    m2 = m2 + __shfl_xor(m2, 1, 64);
+    m2 = m2 + __shfl_xor(m2, 2, 64);
+    return make_float2(mean, 1.0f / sqrtf(m2 / (float)K + 1e-5f));
+}
+// consumer output element before the activation: (acc - mean gw) rstd + bw
+__device__ __forceinline__ float lnf_apply(float acc, float2 mr, float gw, float bw) {
+#pragma clang fp contract(off)
+    const float t = mr.x * gw;
+    float v = acc - t;
+    v = v * mr.y;
+    return v + bw;
+}
+template <typename T> __device__ __forceinline__ uint32_t lnf_pack2(float a, float b);
+template <> __device__ __forceinline__ uint32_t lnf_pack2<bf16>(float a, float b) { return pack_bf2(a, b); }
+template <> __device__ __forceinline__ uint32_t lnf_pack2<f16>(float a, float b) {
+    return (uint32_t)__builtin_bit_cast(unsigned short, (f16)a) | ((uint32_t)__builtin_bit_cast(unsigned short, (f16)b) << 16);
+}
+
 // ST-slot LDS ring (ST x 32 KiB, dynamic for ST > 2): ST - 1 K-slabs in flight while one is
 // computed.  The 16-slab GEMMs of a Parakeet streaming pass (M = 832, K = 1024) and Whisper's
 // smaller shapes give about one workgroup per CU and no other wave to cover a slab's load
@@ -116,8 +224,10 @@ __device__ __forceinline__ void epi_store(const GemmArgs& g, int bz, int row, co
 // BMT = 64 halves the tile's rows (each wave 32 x 64 of C), BNT = 64 its columns: at M = 832 a
 // 128 x 128 tile gives at most one workgroup per CU, so one wave per SIMD with every LDS read and
 // DMA wait of a k-step exposed.  Every C element is the same MFMA chain in every tile shape.
-template <typename T, int EPI, int ST, int BMT = BM, int BNT = BN>
+template <typename T, int EPIX, int ST, int BMT = BM, int BNT = BN>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256, 1) put the accumulators in AGPRs + ~90 copies per k-step
+    constexpr int EPI = epi_base(EPIX);
+    constexpr bool LNF = EPIX != EPI;
     static_assert((BMT == 64 || BMT == 128) && (BNT == 64 || BNT == 128), "tile shape");
     static_assert(ST == 2 || (BMT == 128 && BNT == 128), "deeper rings: 128 x 128 only");
     constexpr int MI = BMT / 32;      // 16-row A fragments per wave
@@ -176,10 +286,28 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256,
     const int nkt = Kc * (int)sizeof(T) / SLAB;
     const int fr = lane & 15, fq = lane >> 4;
 
+    // LayerNorm fold, consumer: {mean, rstd} of the tile's A rows into LDS behind the ring (the
+    // partials are loaded ahead of the first slab's DMA, merged after it is issued)
+    constexpr int STAT_OFF = ST * (BMT + BNT) * SLAB;
+    constexpr int LNF_P = BMT / 64;  // rows per thread (4 lanes per row)
+    constexpr bool lnf_c = LNF && lnf_consumer<EPI>();
+    float2 lv[LNF_P][kLnfQ];
+    if (lnf_c)
+#pragma unroll
+        for (int p = 0; p < LNF_P; ++p)
+            lnf_load(g.lnf_in + ((size_t)bz * g.M + min(m0 + 64 * p + (tid >> 2), g.M - 1)) * (g.K / kLnfGroup), g.K,
+                     tid & 3, lv[p]);
+
     // prologue: slabs 0 .. ST - 2.  Every iteration issues exactly one slab (past the end: the last
     // slab again, into a free slot), so each wave's vmcnt counts the same instructions everywhere.
 #pragma unroll
     for (int p = 0; p < ST - 1; ++p) stage(p, min(p, nkt - 1));
+    if (lnf_c)
+#pragma unroll
+        for (int p = 0; p < LNF_P; ++p) {
+            const float2 mr = lnf_merge(lv[p], g.K);
+            if (!(tid & 3)) *(float2*)(smem + STAT_OFF + (64 * p + (tid >> 2)) * 8) = mr;
+        }
     for (int kt = 0; kt < nkt; ++kt) {
         const int cur = kt % ST;
         // slab kt landed (8 DMA instructions per slab and wave; ST - 2 younger slabs may fly on),
@@ -260,7 +388,35 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256,
                 for (int r = 0; r < 4; ++r)
                     y[i][j][r] = epi_y<EPI>(g, bz, min(m0 + wm * (BMT / 2) + 16 * i + 4 * fq + r, g.M - 1), ec[j]);
     }
+    // LayerNorm fold operands: the next LayerNorm's gamma of this lane's columns (producer), the
+    // fold tables of its columns (consumer)
+    constexpr bool lnf_p = LNF && lnf_producer<EPI>();
+    float lg[NJ], lgw[NJ], lbw[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        lg[j] = lnf_p ? g.lnf_g[ec[j].col] : 0.f;
+        lgw[j] = lnf_c ? g.lnf_gw[ec[j].col] : 0.f;
+        lbw[j] = lnf_c ? g.lnf_bw[ec[j].col] : 0.f;
+    }
     epi_loads_landed();
+    if constexpr (lnf_c) {
+        {
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int rl = wm * (BMT / 2) + 16 * i + 4 * fq + r, row = m0 + rl;
+                    const float2 mr = *(const float2*)(smem + STAT_OFF + rl * 8);
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) {
+                        float v = lnf_apply(acc[i][j][r], mr, lgw[j], lbw[j]);
+                        if constexpr (EPI == EPI_BIAS_GELU) v = gelu_tanh(v);
+                        if (row < g.M) ((T*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + ec[j].col] = from_f<T>(v);
+                    }
+                }
+            return;
+        }
+    }
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
@@ -270,6 +426,40 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256,
                 const int row = m0 + wm * (BMT / 2) + 16 * i + 4 * fq + r;
                 if (row < g.M) epi_store<T, EPI>(g, bz, row, ec[j], acc[i][j][r], y[epi_reads_y<EPI>() ? i : 0][j][r]);
             }
+    if constexpr (lnf_p) {
+        {
+            // x o gamma (model dtype; lane pairs fr, fr ^ 1 store two adjacent columns) and the
+            // partials of each 32-column group (fragments 2 jp, 2 jp + 1)
+            T* xg = (T*)g.lnf_xg + (size_t)bz * g.sC;
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = m0 + wm * (BMT / 2) + 16 * i + 4 * fq + r;
+#pragma unroll
+                    for (int jp = 0; jp < NJ / 2; ++jp) {
+                        float o[2];
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const int j = 2 * jp + h;
+                            o[h] = epi_value<EPI>(g, ec[j], acc[i][j][r], y[i][j][r]);
+                            const float xv = o[h] * lg[j];
+                            if constexpr (sizeof(T) == 4) {
+                                const float nb = __shfl_xor(xv, 1, 64);
+                                if (!(fr & 1) && row < g.M)
+                                    *(float2*)(xg + (size_t)row * g.ldc + ec[j].col) = make_float2(xv, nb);
+                            } else {
+                                const float nb = __shfl_xor(xv, 1, 64);
+                                if (!(fr & 1) && row < g.M)
+                                    *(uint32_t*)(xg + (size_t)row * g.ldc + ec[j].col) = lnf_pack2<T>(xv, nb);
+                            }
+                        }
+                        const float2 st = lnf_group16(o[0], o[1]);
+                        if (fr == 0 && row < g.M) g.lnf_part[lnf_part_index(g, bz, row, ec[2 * jp].col)] = st;
+                    }
+                }
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -296,7 +486,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256,
 constexpr int G2_BM = 256, G2_BN = 256, G2_ROW = 128;  // G2_ROW: bytes of K per row per K-tile
 constexpr int G2_BUF = 2 * 256 * G2_ROW;               // one buffer: A + W
 constexpr int G2_LDS = 2 * G2_BUF;                     // 128 KiB
-constexpr int G2_LDS_ALL = 8 * 128 * (128 + 16) > G2_LDS ? 8 * 128 * (128 + 16) : G2_LDS;  // + epilogue staging
+constexpr int G2_STAT = 8 * 128 * (128 + 16) > G2_LDS ? 8 * 128 * (128 + 16) : G2_LDS;  // + epilogue staging
+constexpr int G2_LDS_ALL = G2_STAT + 256 * 8;  // + the LayerNorm fold's {mean, rstd} of the tile's rows
 
 // STG: the wave groups wr = 0 (waves 0-3) and wr = 1 (waves 4-7; each SIMD holds one wave of each)
 // run one phase apart -- group 1 passes one extra barrier first, group 0 one extra at the end --
@@ -305,19 +496,15 @@ constexpr int G2_LDS_ALL = 8 * 128 * (128 + 16) > G2_LDS ? 8 * 128 * (128 + 16) 
 // wave must have waited for a half-tile by the end of the phase two before its read, so the
 // waits become vmcnt(8) at the ends of P1 / P3 / P4 (4 half-tiles in flight; see the schedule
 // below).  The MFMA order per accumulator is unchanged: results are bitwise those of STG = false.
-// RM: C rows per tile, 256 or 240.  M = 12000 (eight 30 s windows) is 50 tiles of 240 rows against
-// 46.9 of 256: the four encoder GEMMs then fill their last round of 256 CUs almost whole (qkv 750
-// tiles = 2.93 rounds, fc1 1000 = 3.91, out / fc2 250 = 0.98), and a 240-row tile does 15/16 of the
-// 256-row tile's work -- its last 16-row fragment row (waves 4-7, rows 240..255) is neither read
-// from LDS nor multiplied, and each SIMD runs one wave of each half, so the MFMA pipe time drops
-// with it.  Every C element is the same MFMA chain in either tile: results are bitwise equal.
 // PP (with STG): every phase gets a second barrier between its fragment reads / DMA issue and its
 // MFMAs, so the two groups' half-phase lag alternates them: on each SIMD one wave reads while the
 // other multiplies.  The restaging and wait rules above hold unchanged (a read completes before its
 // phase's MFMAs; a half-tile is restaged >= 2 phases after its last read and read >= 2 phases after
 // every wave's wait for it), and the MFMA order per accumulator is the same: bitwise equal results.
-template <int EPI, bool F16, bool STG = false, int RM = 256, bool PP = false>
+template <int EPIX, bool F16, bool STG = false, bool PP = false>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
+    constexpr int EPI = epi_base(EPIX);
+    constexpr bool LNF = EPIX != EPI;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wr = wid >> 2, wc = wid & 3;
@@ -327,10 +514,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     const int tm = wg / nnt, tn = wg - tm * nnt;
-    const int m0 = tm * RM, n0 = tn * G2_BN;
+    const int m0 = tm * G2_BM, n0 = tn * G2_BN;
     const int bz = blockIdx.z;
-    // RM = 240: waves 4-7 skip their last fragment row (tile rows 240..255 belong to the next tile)
-    const bool skip7 = RM == 240 && wr == 1;
     const int Kc = g.K / g.ksplit;
     const bf16* A = (const bf16*)g.A + (size_t)bz * g.sA + (size_t)blockIdx.y * Kc;
     const bf16* W = (const bf16*)g.W + (size_t)blockIdx.y * Kc;
@@ -378,7 +563,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
         for (int s = 0; s < 2; ++s)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                if (rh == 1 && i == 3 && skip7) continue;
                 const int r = wr * 128 + rh * 64 + 16 * i + fr;
                 const int c = 4 * s + fq;
                 af[i][s] = *(const SPT_LDS bf16x8*)(la + r * G2_ROW + ((c ^ swz(r)) << 4));
@@ -408,8 +592,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
-                    if (rh == 1 && i == 3 && skip7) continue;
-                    else if constexpr (F16)
+                    if constexpr (F16)
                         acc[rh * 4 + i][ch * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
                             __builtin_bit_cast(f16x8, af[i][s]), __builtin_bit_cast(f16x8, bw[ch][j][s]),
                             acc[rh * 4 + i][ch * 2 + j], 0, 0, 0);
@@ -421,9 +604,25 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
 #define G2_BARRIER() asm volatile("s_barrier" ::: "memory")
 #define G2_VMWAIT() asm volatile("s_waitcnt vmcnt(10)" ::: "memory")
 
+    // LayerNorm fold, consumer: {mean, rstd} of the tile's 256 A rows into LDS after the epilogue's
+    // staging region (partials loaded ahead of the prologue's DMA, merged after it is issued)
+    constexpr bool lnf_c = LNF && lnf_consumer<EPI>();
+    float2 lv[2][kLnfQ];  // rows tid / 4 and 128 + tid / 4, quarter tid % 4
+    if (lnf_c)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+            lnf_load(g.lnf_in + ((size_t)bz * g.M + min(m0 + 128 * p + (tid >> 2), g.M - 1)) * (g.K / kLnfGroup), g.K,
+                     tid & 3, lv[p]);
+
     // prologue: K-tile 0 whole, K-tile 1 but its A1 (issued by K-tile 0's P1)
     stageA(0, 0, 0); stageW(0, 0, 0); stageW(0, 0, 1); stageA(0, 0, 1);
     stageA(1, 1, 0); stageW(1, 1, 0); stageW(1, 1, 1);
+    if (lnf_c)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const float2 mr = lnf_merge(lv[p], g.K);
+            if (!(tid & 3)) *(float2*)(smem + G2_STAT + (128 * p + (tid >> 2)) * 8) = mr;
+        }
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     G2_BARRIER();
     if constexpr (STG) {
@@ -507,9 +706,17 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     constexpr int CPR = 64 * ESZ / 16;         // 16-byte chunks per row (8 or 16)
     constexpr int RPI = 64 / CPR;              // rows per wave-instruction (8 or 4)
     char* wreg = smem + wid * (PR * RS);
-    float bv[4];
+    float bv[4], lgw[4], lbw[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bv[j] = g.bias ? g.bias[n0 + wc * 64 + 16 * j + fr] : 0.0f;
+    for (int j = 0; j < 4; ++j) {
+        bv[j] = g.bias ? g.bias[n0 + wc * 64 + 16 * j + fr] : 0.0f;
+        lgw[j] = lnf_c ? g.lnf_gw[n0 + wc * 64 + 16 * j + fr] : 0.0f;
+        lbw[j] = lnf_c ? g.lnf_bw[n0 + wc * 64 + 16 * j + fr] : 0.0f;
+    }
+    // LayerNorm fold, producer: the next LayerNorm's gamma of this lane's 4 columns (16-byte chunk ch)
+    constexpr bool lnf_p = LNF && lnf_producer<EPI>();
+    float4 lg = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (lnf_p) lg = *(const float4*)(g.lnf_g + n0 + wc * 64 + (lane % CPR) * (16 / ESZ));
 #pragma unroll
     for (int pass = 0; pass < 128 / PR; ++pass) {
         const int ch = lane % CPR, rsub = lane / CPR;
@@ -538,7 +745,12 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int rl = 16 * ii + 4 * fq + r, cl = 16 * j + fr;
-                    float v = acc[i][j][r] + bv[j];
+                    float v;
+                    if constexpr (lnf_c)
+                        v = lnf_apply(acc[i][j][r], *(const float2*)(smem + G2_STAT + (wr * 128 + 16 * i + 4 * fq + r) * 8),
+                                      lgw[j], lbw[j]);
+                    else
+                        v = acc[i][j][r] + bv[j];
                     if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_POS) v = gelu_tanh(v);
                     if constexpr (EPI == EPI_BIAS_SWISH) v = swish(v);
                     if constexpr (EPI == EPI_BIAS_RELU) v = fmaxf(v, 0.0f);
@@ -555,7 +767,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
             const int rl = it * RPI + rsub;
             const int row = m0 + wr * 128 + pass * PR + rl;
             const uint4 v = *(const uint4*)(wreg + rl * RS + ch * 16);
-            if (row >= g.M || (RM < 256 && wr * 128 + pass * PR + rl >= RM)) continue;
+            if (!lnf_p && row >= g.M) continue;  // (fold producers: lanes of every row shuffle below)
+            const bool rv = row < g.M;
             const int col = n0 + wc * 64 + ch * (16 / ESZ);
             if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_SWISH || EPI == EPI_BIAS_RELU) {
                 *(uint4*)((bf16*)g.C + (size_t)bz * g.sC + (size_t)row * g.ldc + col) = v;
@@ -574,182 +787,24 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
                 if constexpr (YIN) y = ypre[it];
                 else y = make_float4(0.f, 0.f, 0.f, 0.f);
                 o.x += y.x; o.y += y.y; o.z += y.z; o.w += y.w;
-                *(float4*)cp = o;
+                if (rv) *(float4*)cp = o;
+                if constexpr (lnf_p) {
+                    {
+                        // x o gamma, 8 columns per even lane (16-byte stores), and the partials of the
+                        // lane's 32-column group (lanes ch & ~7 .. + 7)
+                        typedef typename std::conditional<F16, f16, bf16>::type T;
+                        const uint32_t p0 = lnf_pack2<T>(o.x * lg.x, o.y * lg.y), p1 = lnf_pack2<T>(o.z * lg.z, o.w * lg.w);
+                        const uint32_t q0 = __shfl_xor(p0, 1, 64), q1 = __shfl_xor(p1, 1, 64);
+                        if (rv && !(ch & 1))
+                            *(uint4*)((T*)g.lnf_xg + (size_t)bz * g.sC + (size_t)row * g.ldc + col) = make_uint4(p0, p1, q0, q1);
+                        const float2 st = lnf_group8(o);
+                        if (rv && !(ch & 7)) g.lnf_part[lnf_part_index(g, bz, row, col)] = st;
+                    }
+                }
             }
         }
         __builtin_amdgcn_wave_barrier();
     }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Ring GEMM for a few hundred rows (Parakeet's streaming pass: 64 one-second windows, M = 832).
-// There every tile shape is one round of workgroups with 16 K-steps, and the 64 x 64 tile's cost
-// is what each CU takes in: 3.25 workgroups x (64 + 64) rows x K x 2 B = 852 KB per CU at K = 1024,
-// ~56 GB/s.  Here one workgroup per CU owns a 208-row x 64-column tile (557 KB at K = 1024) and
-// splits its waves by role (MI355X_MICROARCH.md, ring-gemm):
-//   waves 4-7 (loaders): LDS-DMA the tile's 272 slab rows (208 A + 64 W, 128 B = one 64-deep K-step
-//     each) into a 4-slot ring, two K-steps in flight, and publish a slot with a FULL word once
-//     their own DMA into it has landed (counted vmcnt);
-//   waves 0-3 (consumers, one per SIMD): all 13 row fragments x one 16-column fragment each; read a
-//     slot's fragments as two 32-deep halves, the next half's reads in flight under the current
-//     half's 13 MFMAs, and hand the slot back with a FREE word once both halves are in registers.
-// No barrier inside the K loop: a loader waits only for the four FREE words of the slot it refills,
-// a consumer only for the four FULL words of the slot it reads.  Every C element is the same
-// v_mfma_f32_16x16x32 chain over K as in the other tiles (k-step order, lane group fq = k chunk),
-// so the results are bitwise those of the 64 x 64 tile at the same split.
-constexpr int RG_RF = 13, RG_RT = 16 * RG_RF, RG_CT = 64;  // tile: 208 rows x 64 columns
-constexpr int RG_NS = 4;                                    // ring slots (K-steps in flight per loader: template D, 2 or 3)
-constexpr int RG_ROWS = RG_RT + RG_CT;                      // 272 slab rows per slot
-constexpr int RG_SLOT = RG_ROWS * SLAB;                     // 34,816 B
-constexpr int RG_NI = (RG_ROWS / 8 + 3) / 4;                // 9 DMA instructions per loader wave per slot
-constexpr int RG_LDS = RG_NS * RG_SLOT + 2 * RG_NS * 4 * 4; // + FULL [slot][loader], FREE [slot][consumer]
-static_assert(RG_NI == 9, "the loader's counted waits below assume 9 instructions per slot");
-
-__device__ __forceinline__ void rg_wait(const SPT_LDS int* w, int target) {
-    while (true) {
-        const int a = *(volatile const SPT_LDS int*)(w + 0), b = *(volatile const SPT_LDS int*)(w + 1);
-        const int c = *(volatile const SPT_LDS int*)(w + 2), d = *(volatile const SPT_LDS int*)(w + 3);
-        if (min(min(a, b), min(c, d)) >= target) break;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    asm volatile("" ::: "memory");  // no slot read moves above the wait
-}
-__device__ __forceinline__ void rg_post(SPT_LDS int* w, int v) {
-    asm volatile("" ::: "memory");
-    *(volatile SPT_LDS int*)w = v;
-}
-
-template <typename T, int EPI, int RG_D = 2>
-__global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs g) {
-    static_assert(RG_D == 2 || RG_D == 3, "K-steps in flight");
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    SPT_LDS char* lds = (SPT_LDS char*)smem;
-    SPT_LDS int* full = (SPT_LDS int*)(lds + RG_NS * RG_SLOT);  // [slot][loader wave]
-    SPT_LDS int* freew = full + RG_NS * 4;                       // [slot][consumer wave]
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    // bijective XCD-aware remap; row blocks fastest, so the workgroups streaming the same W
-    // columns are neighbours in one XCD's run (share its L2)
-    const int nrb = cdiv(g.M, RG_RT);
-    const int nwg = gridDim.x, bid = blockIdx.x;
-    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-    const int tn = wg / nrb, tm = wg - tn * nrb;
-    const int m0 = tm * RG_RT, n0 = tn * RG_CT;
-    const int bz = blockIdx.z;
-    const int Kc = g.K / g.ksplit;
-    const T* A = (const T*)g.A + (size_t)bz * g.sA + (size_t)blockIdx.y * Kc;
-    const T* W = (const T*)g.W + (size_t)blockIdx.y * Kc;
-    const int nkt = Kc * (int)sizeof(T) / SLAB;
-    if (tid < 2 * RG_NS * 4) full[tid] = 0;  // FULL and FREE words are contiguous
-    __syncthreads();
-
-    if (wid >= 4) {
-        // ------------------------------------------------------------ loaders
-        const int lw = wid - 4, prow = lane >> 3, pch = lane & 7;
-        const char* src[RG_NI];
-        int dst[RG_NI];
-#pragma unroll
-        for (int i = 0; i < RG_NI; ++i) {
-            // 34 instructions of 8 rows per slot over 4 waves; the two spare issues repeat the last
-            // group (same bytes to the same LDS, landed before their wave's FULL word like the rest)
-            const int j = min(lw + 4 * i, RG_ROWS / 8 - 1);
-            const int r = 8 * j + prow;
-            const int c = (pch ^ swz(r)) << 4;
-            src[i] = r < RG_RT ? (const char*)(A + (size_t)min(m0 + r, g.M - 1) * g.lda) + c
-                               : (const char*)(W + (size_t)(n0 + r - RG_RT) * g.ldw) + c;
-            dst[i] = 8 * j * SLAB;
-        }
-        for (int k = 0; k < nkt; ++k) {
-            const int s = k % RG_NS;
-            if (k >= RG_NS) rg_wait(freew + 4 * s, k - RG_NS + 1);  // the slot's last occupant is in registers
-            const size_t ko = (size_t)k * SLAB;
-#pragma unroll
-            for (int i = 0; i < RG_NI; ++i)
-                __builtin_amdgcn_global_load_lds((const void*)(src[i] + ko), (SPT_LDS void*)(lds + s * RG_SLOT + dst[i]), 16, 0, 0);
-            if (k >= RG_D) {
-                // K-step k - D landed (RG_NI * RG_D younger instructions)
-                if constexpr (RG_D == 2) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(27)" ::: "memory");
-                rg_post(full + 4 * ((k - RG_D) % RG_NS) + lw, k - RG_D + 1);
-            }
-        }
-        if constexpr (RG_D == 3) {
-            if (nkt >= 3) {
-                asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
-                rg_post(full + 4 * ((nkt - 3) % RG_NS) + lw, nkt - 2);
-            }
-        }
-        if (nkt >= 2) {
-            asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-            rg_post(full + 4 * ((nkt - 2) % RG_NS) + lw, nkt - 1);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        rg_post(full + 4 * ((nkt - 1) % RG_NS) + lw, nkt);
-        return;
-    }
-
-    // ---------------------------------------------------------------- consumers
-    const int cw = wid, fr = lane & 15, fq = lane >> 4;
-    f32x4 acc[RG_RF];
-#pragma unroll
-    for (int i = 0; i < RG_RF; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    bf16x8 fa0[RG_RF], fa1[RG_RF], fw0, fw1;
-    auto rd = [&](int s, int half, bf16x8 (&a)[RG_RF], bf16x8& w) {
-        const SPT_LDS char* sl = lds + s * RG_SLOT;
-        const int c = 4 * half + fq;
-#pragma unroll
-        for (int i = 0; i < RG_RF; ++i) {
-            const int r = 16 * i + fr;
-            a[i] = *(const SPT_LDS bf16x8*)(sl + r * SLAB + ((c ^ swz(r)) << 4));
-        }
-        const int r = RG_RT + 16 * cw + fr;
-        w = *(const SPT_LDS bf16x8*)(sl + r * SLAB + ((c ^ swz(r)) << 4));
-    };
-    auto mm = [&](const bf16x8 (&a)[RG_RF], const bf16x8& w) {
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < RG_RF; ++i) {
-            if constexpr (TypeTag<T>::id == 2)
-                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a[i]), __builtin_bit_cast(f16x8, w),
-                                                                acc[i], 0, 0, 0);
-            else
-                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], w, acc[i], 0, 0, 0);
-        }
-        __builtin_amdgcn_s_setprio(0);
-    };
-    // Straight-line LDS traffic in the loop (the FREE word written by every lane, the next slot's
-    // first half read even after the last K-step: unused) so the compiler's lgkmcnt waits before
-    // the MFMAs stay counted instead of draining to 0 at a merge
-    rg_wait(full, 1);
-    rd(0, 0, fa0, fw0);
-    for (int k = 0; k < nkt; ++k) {
-        const int s = k % RG_NS;
-        rd(s, 1, fa1, fw1);
-        mm(fa0, fw0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // both halves of slot s are in registers
-        rg_post(freew + 4 * s + cw, k + 1);
-        if (k + 1 < nkt) rg_wait(full + 4 * ((k + 1) % RG_NS), k + 2);
-        rd((k + 1) % RG_NS, 0, fa0, fw0);
-        mm(fa1, fw1);
-    }
-
-    // ---------------------------------------------------------------- epilogue
-    const EpiCol ec = epi_col<EPI>(g, n0 + 16 * cw + fr);
-    float y[epi_reads_y<EPI>() ? RG_RF : 1][4];
-    if constexpr (epi_reads_y<EPI>()) {
-#pragma unroll
-        for (int i = 0; i < RG_RF; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) y[i][r] = epi_y<EPI>(g, bz, min(m0 + 16 * i + 4 * fq + r, g.M - 1), ec);
-    }
-    epi_loads_landed();
-#pragma unroll
-    for (int i = 0; i < RG_RF; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int row = m0 + 16 * i + 4 * fq + r;
-            if (row < g.M) epi_store<T, EPI>(g, bz, row, ec, acc[i][r], y[epi_reads_y<EPI>() ? i : 0][r]);
-        }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -834,18 +889,6 @@ void launch_skinny(const GemmArgs& g, hipStream_t st) {
     SPT_LAUNCH_CHECK();
 }
 
-// rows per tile: 256; SPT_G2_ROWS=240 selects the 240-row tile.  Priced as rounds of one tile per
-// CU times 15/16 of a tile's work it looked 4-6 % cheaper at M = 12000, but it measured slower in
-// every encoder GEMM (r5, profiles/r5/exp_gemm240.txt: qkv 127.4 -> 134.7 us, fc1 194.8 -> 197.4,
-// fc2 147.8 -> 154.7, out 51.5 -> 53.6 standalone; in situ fc1 166.8 -> 181.2): a 240-row tile still
-// stages 256 A rows and writes its epilogue at the 256-row tile's cost, so it is not 15/16 of one
-int g2_rows(const GemmArgs& g, int batch) {
-    (void)g;
-    (void)batch;
-    static const int force = getenv("SPT_G2_ROWS") ? atoi(getenv("SPT_G2_ROWS")) : 0;
-    return force == 240 ? 240 : 256;
-}
-
 template <int EPI, bool F16>
 void launch_256(const GemmArgs& g, int batch, hipStream_t st) {
     // staggered wave groups: bitwise-identical results, encoder 21.54 -> 21.28 ms (r2, two A/B pairs);
@@ -857,23 +900,15 @@ void launch_256(const GemmArgs& g, int batch, hipStream_t st) {
     // > 64 KiB dynamic LDS: per kernel and device (gemm_prepare sets them before any capture)
     ensure_lds_attr((const void*)gemm256_kernel<EPI, F16, false>, G2_LDS_ALL);
     ensure_lds_attr((const void*)gemm256_kernel<EPI, F16, true>, G2_LDS_ALL);
-    ensure_lds_attr((const void*)gemm256_kernel<EPI, F16, false, 240>, G2_LDS_ALL);
-    ensure_lds_attr((const void*)gemm256_kernel<EPI, F16, true, 240>, G2_LDS_ALL);
-    ensure_lds_attr((const void*)gemm256_kernel<EPI, F16, true, 256, true>, G2_LDS_ALL);
+    ensure_lds_attr((const void*)gemm256_kernel<EPI, F16, true, true>, G2_LDS_ALL);
     // ping-pong phases (a barrier between each phase's reads and its MFMAs; r5: q/k/v 125.4 -> 119.4 us,
     // 4096^3 1182 -> 1246 TF/s standalone, encoder 20.4 -> 20.2 ms, bitwise equal); SPT_G2_PP=0: off
     const char* pp_env = getenv("SPT_G2_PP");
     const bool pp = !pp_env || atoi(pp_env) != 0;
-    const int rm = g2_rows(g, batch);
-    dim3 grid(cdiv(g.M, rm) * (g.N / G2_BN), g.ksplit, batch);
-    if (rm == 240) {
-        if (stg) hipLaunchKernelGGL((gemm256_kernel<EPI, F16, true, 240>), grid, dim3(512), G2_LDS_ALL, st, g);
-        else hipLaunchKernelGGL((gemm256_kernel<EPI, F16, false, 240>), grid, dim3(512), G2_LDS_ALL, st, g);
-    } else {
-        if (stg && pp) hipLaunchKernelGGL((gemm256_kernel<EPI, F16, true, 256, true>), grid, dim3(512), G2_LDS_ALL, st, g);
-        else if (stg) hipLaunchKernelGGL((gemm256_kernel<EPI, F16, true>), grid, dim3(512), G2_LDS_ALL, st, g);
-        else hipLaunchKernelGGL((gemm256_kernel<EPI, F16, false>), grid, dim3(512), G2_LDS_ALL, st, g);
-    }
+    dim3 grid(cdiv(g.M, G2_BM) * (g.N / G2_BN), g.ksplit, batch);
+    if (stg && pp) hipLaunchKernelGGL((gemm256_kernel<EPI, F16, true, true>), grid, dim3(512), G2_LDS_ALL, st, g);
+    else if (stg) hipLaunchKernelGGL((gemm256_kernel<EPI, F16, true>), grid, dim3(512), G2_LDS_ALL, st, g);
+    else hipLaunchKernelGGL((gemm256_kernel<EPI, F16, false>), grid, dim3(512), G2_LDS_ALL, st, g);
     SPT_LAUNCH_CHECK();
 }
 
@@ -890,7 +925,7 @@ void launch_t_st(const GemmArgs& g0, int batch, hipStream_t st) {
     static const int nmajor = getenv("SPT_GEMM_NT_RASTER") ? atoi(getenv("SPT_GEMM_NT_RASTER")) : 0;
     GemmArgs g = g0;
     g.nmajor = nmajor;
-    constexpr int lds = ST * 2 * BM * SLAB;
+    constexpr int lds = ST * 2 * BM * SLAB + BM * 8;  // + the LayerNorm fold's row statistics
     if (lds > 64 * 1024) ensure_lds_attr((const void*)gemm_nt_kernel<T, EPI, ST>, lds);
     dim3 grid(cdiv(g.M, BM) * (g.N / BN), g.ksplit, batch);
     hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, ST>), grid, dim3(256), lds, st, g);
@@ -902,27 +937,11 @@ void launch_small(const GemmArgs& g0, int batch, hipStream_t st) {  // 64 x 128 
     GemmArgs g = g0;
     g.nmajor = nmajor;
     dim3 grid(cdiv(g.M, BMT) * (g.N / BNT), g.ksplit, batch);
-    hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, 2, BMT, BNT>), grid, dim3(256), 2 * (BMT + BNT) * SLAB, st, g);
-}
-
-template <typename T, int EPI>
-void launch_ring(const GemmArgs& g, int batch, hipStream_t st) {
-    if constexpr (sizeof(T) == 2) {
-        // SPT_RING_D = 3: three K-steps in flight per loader (default 2)
-        static const int d3 = getenv("SPT_RING_D") && atoi(getenv("SPT_RING_D")) == 3;
-        ensure_lds_attr((const void*)gemm_ring_kernel<T, EPI, 2>, RG_LDS);
-        ensure_lds_attr((const void*)gemm_ring_kernel<T, EPI, 3>, RG_LDS);
-        dim3 grid(cdiv(g.M, RG_RT) * (g.N / RG_CT), g.ksplit, batch);
-        if (d3) hipLaunchKernelGGL((gemm_ring_kernel<T, EPI, 3>), grid, dim3(512), RG_LDS, st, g);
-        else hipLaunchKernelGGL((gemm_ring_kernel<T, EPI, 2>), grid, dim3(512), RG_LDS, st, g);
-    } else {
-        throw std::runtime_error("gemm_nt: the ring variant needs a 16-bit dtype");
-    }
+    hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, 2, BMT, BNT>), grid, dim3(256), 2 * (BMT + BNT) * SLAB + BMT * 8, st, g);
 }
 
 template <typename T, int EPI>
 void launch_t(const GemmArgs& g, int batch, int variant, hipStream_t st) {
-    if (variant == 6) return launch_ring<T, EPI>(g, batch, st);
     if (variant == 4) return launch_small<T, EPI, 64, 128>(g, batch, st);
     if (variant == 5) return launch_small<T, EPI, 64, 64>(g, batch, st);
     switch (nt_stages()) {
@@ -938,22 +957,14 @@ void prepare_epi() {
     ensure_lds_attr((const void*)gemm256_kernel<EPI, false, true>, G2_LDS_ALL);
     ensure_lds_attr((const void*)gemm256_kernel<EPI, true, false>, G2_LDS_ALL);
     ensure_lds_attr((const void*)gemm256_kernel<EPI, true, true>, G2_LDS_ALL);
-    ensure_lds_attr((const void*)gemm256_kernel<EPI, false, false, 240>, G2_LDS_ALL);
-    ensure_lds_attr((const void*)gemm256_kernel<EPI, false, true, 240>, G2_LDS_ALL);
-    ensure_lds_attr((const void*)gemm256_kernel<EPI, true, false, 240>, G2_LDS_ALL);
-    ensure_lds_attr((const void*)gemm256_kernel<EPI, true, true, 240>, G2_LDS_ALL);
-    ensure_lds_attr((const void*)gemm256_kernel<EPI, false, true, 256, true>, G2_LDS_ALL);
-    ensure_lds_attr((const void*)gemm256_kernel<EPI, true, true, 256, true>, G2_LDS_ALL);
-    ensure_lds_attr((const void*)gemm_ring_kernel<bf16, EPI, 2>, RG_LDS);
-    ensure_lds_attr((const void*)gemm_ring_kernel<f16, EPI, 2>, RG_LDS);
-    ensure_lds_attr((const void*)gemm_ring_kernel<bf16, EPI, 3>, RG_LDS);
-    ensure_lds_attr((const void*)gemm_ring_kernel<f16, EPI, 3>, RG_LDS);
-    ensure_lds_attr((const void*)gemm_nt_kernel<bf16, EPI, 3>, 3 * 2 * BM * SLAB);
-    ensure_lds_attr((const void*)gemm_nt_kernel<f16, EPI, 3>, 3 * 2 * BM * SLAB);
-    ensure_lds_attr((const void*)gemm_nt_kernel<float, EPI, 3>, 3 * 2 * BM * SLAB);
-    ensure_lds_attr((const void*)gemm_nt_kernel<bf16, EPI, kNtStages>, kNtStages * 2 * BM * SLAB);
-    ensure_lds_attr((const void*)gemm_nt_kernel<f16, EPI, kNtStages>, kNtStages * 2 * BM * SLAB);
-    ensure_lds_attr((const void*)gemm_nt_kernel<float, EPI, kNtStages>, kNtStages * 2 * BM * SLAB);
+    ensure_lds_attr((const void*)gemm256_kernel<EPI, false, true, true>, G2_LDS_ALL);
+    ensure_lds_attr((const void*)gemm256_kernel<EPI, true, true, true>, G2_LDS_ALL);
+    ensure_lds_attr((const void*)gemm_nt_kernel<bf16, EPI, 3>, 3 * 2 * BM * SLAB + BM * 8);
+    ensure_lds_attr((const void*)gemm_nt_kernel<f16, EPI, 3>, 3 * 2 * BM * SLAB + BM * 8);
+    ensure_lds_attr((const void*)gemm_nt_kernel<float, EPI, 3>, 3 * 2 * BM * SLAB + BM * 8);
+    ensure_lds_attr((const void*)gemm_nt_kernel<bf16, EPI, kNtStages>, kNtStages * 2 * BM * SLAB + BM * 8);
+    ensure_lds_attr((const void*)gemm_nt_kernel<f16, EPI, kNtStages>, kNtStages * 2 * BM * SLAB + BM * 8);
+    ensure_lds_attr((const void*)gemm_nt_kernel<float, EPI, kNtStages>, kNtStages * 2 * BM * SLAB + BM * 8);
 }
 
 }  // namespace
@@ -970,6 +981,10 @@ void ensure_lds_attr(const void* kernel, int bytes) {
 }
 
 void gemm_prepare() {
+    prepare_epi<EPI_BIAS | EPI_LNF>();
+    prepare_epi<EPI_BIAS_GELU | EPI_LNF>();
+    prepare_epi<EPI_BIAS_GELU_POS | EPI_LNF>();
+    prepare_epi<EPI_BIAS_RESID | EPI_LNF>();
     prepare_epi<EPI_BIAS>();
     prepare_epi<EPI_BIAS_GELU>();
     prepare_epi<EPI_BIAS_GELU_POS>();
@@ -985,11 +1000,15 @@ void gemm_nt(int dtype, int epi, const GemmArgs& g, int batch, hipStream_t st) {
 
 void gemm_nt_variant(int dtype, int epi, const GemmArgs& g, int batch, int variant, hipStream_t st) {
     const int esz = dtype == DT_F32 ? 4 : 2;
+    // the LayerNorm fold's kernels (kernels.h GemmArgs lnf_*)
+    if ((g.lnf_in && (epi == EPI_BIAS || epi == EPI_BIAS_GELU)) || (g.lnf_g && (epi == EPI_BIAS_RESID || epi == EPI_BIAS_GELU_POS))) {
+        if (g.K > 40 * kLnfGroup || g.K % (4 * kLnfGroup) || g.N % 64 || variant == 3)
+            throw std::runtime_error("gemm_nt: LayerNorm fold needs K <= 1280, K % 128, N % 64, a tile kernel");
+        epi |= EPI_LNF;
+    }
     if (g.ksplit < 1 || g.K % g.ksplit || (g.ksplit > 1 && epi != EPI_PARTIAL))
         throw std::runtime_error("gemm_nt: split-K needs EPI_PARTIAL and K % ksplit == 0");
-    if (variant == 6 && (dtype == DT_F32 || g.N % RG_CT != 0 || (g.K / g.ksplit) % 64 != 0 || g.M <= 0))
-        throw std::runtime_error("gemm_nt: the ring variant needs a 16-bit dtype, N % 64, (K / ksplit) % 64");
-    if (variant != 3 && variant != 6 && (g.N % (variant == 5 ? 64 : BN) != 0 || (g.K / g.ksplit * esz) % SLAB != 0 || g.M <= 0))
+    if (variant != 3 && (g.N % (variant == 5 ? 64 : BN) != 0 || (g.K / g.ksplit * esz) % SLAB != 0 || g.M <= 0))
         throw std::runtime_error("gemm_nt: unsupported shape M=" + std::to_string(g.M) + " N=" +
                                  std::to_string(g.N) + " K=" + std::to_string(g.K));
 #define SPT_GEMM_CASES(T)                                                          \
@@ -1003,6 +1022,10 @@ void gemm_nt_variant(int dtype, int epi, const GemmArgs& g, int batch, int varia
         case EPI_BIAS_RELU: launch_t<T, EPI_BIAS_RELU>(g, batch, variant, st); return; \
         case EPI_BIAS_F32: launch_t<T, EPI_BIAS_F32>(g, batch, variant, st); return; \
         case EPI_PARTIAL: launch_t<T, EPI_PARTIAL>(g, batch, variant, st); return; \
+        case EPI_BIAS | EPI_LNF: launch_t<T, EPI_BIAS | EPI_LNF>(g, batch, variant, st); return; \
+        case EPI_BIAS_GELU | EPI_LNF: launch_t<T, EPI_BIAS_GELU | EPI_LNF>(g, batch, variant, st); return; \
+        case EPI_BIAS_GELU_POS | EPI_LNF: launch_t<T, EPI_BIAS_GELU_POS | EPI_LNF>(g, batch, variant, st); return; \
+        case EPI_BIAS_RESID | EPI_LNF: launch_t<T, EPI_BIAS_RESID | EPI_LNF>(g, batch, variant, st); return; \
     }
 #define SPT_GEMM256_CASES(F)                                                       \
     switch (epi) {                                                                 \
@@ -1015,6 +1038,10 @@ void gemm_nt_variant(int dtype, int epi, const GemmArgs& g, int batch, int varia
         case EPI_BIAS_RELU: launch_256<EPI_BIAS_RELU, F>(g, batch, st); return;    \
         case EPI_BIAS_F32: launch_256<EPI_BIAS_F32, F>(g, batch, st); return;      \
         case EPI_PARTIAL: launch_256<EPI_PARTIAL, F>(g, batch, st); return;        \
+        case EPI_BIAS | EPI_LNF: launch_256<EPI_BIAS | EPI_LNF, F>(g, batch, st); return; \
+        case EPI_BIAS_GELU | EPI_LNF: launch_256<EPI_BIAS_GELU | EPI_LNF, F>(g, batch, st); return; \
+        case EPI_BIAS_GELU_POS | EPI_LNF: launch_256<EPI_BIAS_GELU_POS | EPI_LNF, F>(g, batch, st); return; \
+        case EPI_BIAS_RESID | EPI_LNF: launch_256<EPI_BIAS_RESID | EPI_LNF, F>(g, batch, st); return; \
     }
 #define SPT_GEMM_SKINNY_CASES(F)                                                   \
     switch (epi) {                                                                 \

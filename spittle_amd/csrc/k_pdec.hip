@@ -130,6 +130,13 @@ __device__ __forceinline__ void stamp(const PdArgs& a, int wg, int k, int f, u64
     if (lane == 0 && k < kPdStampMax) a.stamps[((size_t)wg * kPdStampMax + k) * kPdStampRec + f] = v;
 }
 
+// The loop barriers between gather and compute waves hand over LDS only.  __syncthreads() carries a
+// release fence, before which the compiler drains every outstanding vector-memory op (vmcnt(0)):
+// the compute waves' prefetch of the NEXT unit's weights / K/V, issued just before barrier B to run
+// under the next edge, was waited for there instead (r6 stage stamps: 20.7 us of a 67 us layer at
+// B = 1 sat in barrier B).  So: the wave's own LDS ops (lgkmcnt(0)), then a bare s_barrier.
+#define PD_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+
 // ------------------------------------------------------------------ geometry helpers
 struct Cur { int l, s, u; };
 
@@ -551,7 +558,7 @@ __device__ __forceinline__ void gather_loop(const PdArgs& a, const Smem& sm, uns
             const int n0 = c.s == S_H ? 16 * (c.u >> 1) : 16 * c.u;
             bv = (bias && !(c.s == S_H && (c.u & 1))) ? bias[n0 + fr] : 0.f;  // fc2: slab 0 carries the bias
         }
-        __syncthreads();  // A: inputs in LDS
+        PD_BARRIER();  // A: inputs in LDS
         if (sm.misc[0]) break;
         if (is_gemv(c.s)) img_key = key;
         if (c.s == S_E2 && wave == 0) {  // attn_part_merge_kernel's operations (no compute waves)
@@ -582,8 +589,8 @@ __device__ __forceinline__ void gather_loop(const PdArgs& a, const Smem& sm, uns
                     gran_put(a.gran, a.go[G_M] + (int64_t)b * (a.d / 2) + 32 * h + e / 2, ep, mine | (nb << 16));
                 }
         }
-        if (c.s == S_E) __syncthreads();  // E mid: the first halves' softmax state in LDS
-        __syncthreads();  // B: chain partials / attention partials in LDS
+        if (c.s == S_E) PD_BARRIER();  // E mid: the first halves' softmax state in LDS
+        PD_BARRIER();  // B: chain partials / attention partials in LDS
         if (stp) stamp(a, wg, nk, 5, wall_clock64(), lane);
         // ---------------- epilogue + publish (gather wave 0)
         if (wave == 0) {
@@ -728,7 +735,7 @@ __device__ __forceinline__ void compute_loop(const PdArgs& a, const Smem& sm, un
         const unsigned ep = ep_of(launch, L, c.l, c.s);
         Cur nx = c;
         const bool nhas = advance(a, wg, nx);
-        __syncthreads();  // A: inputs in LDS
+        PD_BARRIER();  // A: inputs in LDS
         if (sm.misc[0]) break;
         if (stp) {  // after barrier A, then once this unit's prefetched operands have landed
             stamp(a, wg, nk, 3, wall_clock64(), lane);
@@ -843,7 +850,7 @@ __device__ __forceinline__ void compute_loop(const PdArgs& a, const Smem& sm, un
                 for (int i = 0; i < 8; ++i) st[64 * (1 + i) + lane] = aw.o[0][i];
                 if (lane == 0) st[9 * 64] = aw.m[0];
             }
-            __syncthreads();  // E mid
+            PD_BARRIER();  // E mid
             if (on && e.half == 1) {
                 aw.l[0] = st[lane];
 #pragma unroll
@@ -863,7 +870,7 @@ __device__ __forceinline__ void compute_loop(const PdArgs& a, const Smem& sm, un
         if (stp) stamp(a, wg, nk, 6, wall_clock64(), lane);
         ++nk;
         if (nhas) prefetch(a, nx, cw, lane, pos0, pre);
-        __syncthreads();  // B: chain partials / attention partials in LDS; the image is free again
+        PD_BARRIER();  // B: chain partials / attention partials in LDS; the image is free again
         c = nx;
         has = nhas;
     }

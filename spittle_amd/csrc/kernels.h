@@ -37,13 +37,25 @@ struct GemmArgs {
     float alpha = 1.0f;                   // EPI_BIAS_RESID / EPI_BIAS_F32 scale
     int ksplit = 1; int64_t c_split = 0;  // EPI_PARTIAL: K split over grid.y, slab stride (elements)
     int nmajor = 0;                       // 128 x 128 tile: raster tiles N-major (set by the launcher)
+    // LayerNorm fold (encoder, r6).  A producer (EPI_BIAS_RESID / EPI_BIAS_GELU_POS,
+    // f32 rows x) with lnf_g set also writes lnf_xg = x o lnf_g in the model dtype (same addressing
+    // as C) and, per row and 32-column group, lnf_part = {sum, sum of squared deviations from the
+    // group's mean} (canonical pairwise order, the same bits in every tile shape).  A consumer
+    // (EPI_BIAS / EPI_BIAS_GELU over A = lnf_xg) with lnf_in set merges the row's groups in order into
+    // mean and rstd and writes (acc - mean gw[n]) rstd + bw[n] (then GELU): LN(x) W^T + b, with
+    // gw = W gamma and bw = b + W beta precomputed (ln_fold_tables); g.bias is not read.
+    const float* lnf_g = nullptr; void* lnf_xg = nullptr; float2* lnf_part = nullptr;
+    const float2* lnf_in = nullptr; const float* lnf_gw = nullptr; const float* lnf_bw = nullptr;
 };
+constexpr int kLnfGroup = 32;  // columns per LayerNorm-fold partial
+// gw[n] = sum_c gamma_c W[n][c], bw[n] = b[n] + sum_c beta_c W[n][c] (f32, fixed order), W [N][K] of dtype
+void ln_fold_tables(int dtype, const void* W, int N, int K, const float* gamma, const float* beta, const float* b,
+                    float* gw, float* bw, hipStream_t st);
 void gemm_nt(int dtype, int epi, const GemmArgs& g, int batch, hipStream_t st);
 // variant 0: automatic (bf16 N % 256 == 0 -> 256 x 256 tile); 1: 128 x 128 tile; 2: prefer 256 x 256;
 // 3: skinny (M <= 64, 16-bit dtypes: 16 columns per workgroup, the weight stream spread over the grid)
 // 4: 64 x 128 tile (16-bit or f32; small M: two workgroups per CU where the 128-row tile gives one)
 // 5: 64 x 64 tile (N % 64; up to four workgroups per CU)
-// 6: ring (16-bit, N % 64: 208 x 64 tile, one workgroup per CU, loader / consumer waves; M of a few hundred)
 // sets the > 64 KiB dynamic-LDS attribute of every GEMM kernel on the current device (engine
 // constructors call it before any stream capture; launches check it too)
 void gemm_prepare();

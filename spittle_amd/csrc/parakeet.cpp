@@ -501,19 +501,8 @@ int ParakeetEngine::gemm(int dt, int epi, const void* A, int lda, const void* W,
     const char* t64e = getenv("SPT_GEMM_T64");
     const bool t64_ok = !(t64e && atoi(t64e) == 0);
     const bool no_skinny = getenv("SPT_NO_SKINNY") != nullptr;
-    // the 208 x 64 ring (variant 6) is opt-in: SPT_GEMM_RING=1.  At C5 it measured slower than the
-    // 64-row tiles (ff-up 17.7 vs 15.7 us, encoder 4.49 vs 4.34 ms)
-    const char* ringe = getenv("SPT_GEMM_RING");
-    const bool ring_ok = ringe && atoi(ringe) != 0;
     int variant = 1, ks = 1;
-    if (dt != DT_F32 && M > 64 && M <= 5 * 208 && N % 64 == 0 && K % 64 == 0 && ring_ok) {
-        // ring: one 208 x 64 workgroup per CU; residual products split K toward 256 workgroups,
-        // keeping >= 4 K-steps per split
-        variant = 6;
-        const int64_t t = (int64_t)cdiv(M, 208) * (N / 64);
-        if (epi == EPI_PARTIAL)
-            while (ks < 8 && t * ks * 2 <= 256 && K % (2 * ks) == 0 && (K / (2 * ks)) % 64 == 0 && K / (2 * ks) >= 256) ks *= 2;
-    } else if (dt != DT_F32 && M <= 64 && N % 16 == 0 && K % 128 == 0 && !no_skinny) {
+    if (dt != DT_F32 && M <= 64 && N % 16 == 0 && K % 128 == 0 && !no_skinny) {
         // skinny: >= 256 workgroups of 16 columns (residual products split K to get there)
         variant = 3;
         if (epi == EPI_PARTIAL)
