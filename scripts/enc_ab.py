@@ -16,9 +16,10 @@ import spittle_amd  # noqa: E402
 from spittle_amd import WhisperEngine, WhisperInferenceParams, WhisperModelParams  # noqa: E402
 from spittle_amd.synth import synth_audio  # noqa: E402
 
-e = WhisperEngine(WhisperModelParams(dtype="bf16", max_batch=8))
+nb = int(os.environ.get("ENC_AB_B", "8"))  # windows per call (1: the app's single-window call)
+e = WhisperEngine(WhisperModelParams(dtype="bf16", max_batch=nb))
 e.load_model("synthetic:large-v3")
-xs = [synth_audio(i) for i in range(8)]
+xs = [synth_audio(i) for i in range(nb)]
 p = WhisperInferenceParams(language="en", no_timestamps=True, temperature_inc=0.0, ignore_eot=True, max_new_tokens=4)
 for _ in range(2):
     e.transcribe_batch(xs, p)

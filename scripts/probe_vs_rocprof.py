@@ -1,0 +1,39 @@
+"""Agreement of bench.py's HIP-event kernel probes with rocprofv3: one bench run
+under rocprofv3 --kernel-trace (SPT_ENC_GROUPS=1, so each encoder kernel is one full-batch launch),
+then for every probed kernel: the probe's average (the bench line's `kernels`), rocprofv3's average
+over the same launches (the probe's own dispatches: the last `iters` + 1 warm-up of that kernel in
+the trace), and rocprofv3's average over the timed calls' launches.
+usage: probe_vs_rocprof.py RESULTS_DB BENCH_LINE_JSON [ITERS]"""
+import json
+import sqlite3
+import sys
+
+db = sqlite3.connect(sys.argv[1])
+line = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
+iters = int(sys.argv[3]) if len(sys.argv) > 3 else 50
+cols = [r[1] for r in db.execute("pragma table_info(kernels)")]
+name = "kernel_name" if "kernel_name" in cols else "name"
+# encoder probes (kind 4 / 5): `iters` runs of encoder layer 0 in sequence after the timed calls; the
+# kernel names: fc1 with the LayerNorm fold (EPI_BIAS_GELU | EPI_LNF = 17) or without (1)
+PAT = {"enc_fc1_gemm": ["gemm256_kernel<17,", "gemm256_kernel<1,"], "enc_attn": ["attn_bf16_q64_kernel<"]}
+out = {}
+for k, pats in PAT.items():
+    if k not in (line.get("kernels") or {}):
+        continue
+    rows = []
+    for pat in pats:
+        rows = db.execute(f"select start, end from kernels where {name} like ? order by start", ("%" + pat + "%",)).fetchall()
+        if rows:
+            break
+    if not rows:
+        continue
+    d = [(e - s) / 1e3 for s, e in rows]
+    probe = line["kernels"][k]["avg_us"]
+    n_probe = iters
+    last = d[-n_probe:]
+    body = d[:-(n_probe + 1)] if len(d) > n_probe + 1 else d
+    out[k] = {"probe_avg_us": probe, "rocprof_same_launches_avg_us": round(sum(last) / len(last), 3),
+              "rocprof_timed_calls_avg_us": round(sum(body) / len(body), 3), "dispatches": len(d),
+              "probe_vs_same_launches_pct": round(100.0 * (probe / (sum(last) / len(last)) - 1.0), 2),
+              "probe_vs_timed_calls_pct": round(100.0 * (probe / (sum(body) / len(body)) - 1.0), 2)}
+print(json.dumps(out, indent=1))

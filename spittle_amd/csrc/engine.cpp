@@ -100,9 +100,12 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     if (const char* v = getenv("SPT_XATTN_SPLIT")) xsplit_ = std::max(1, std::min(4, atoi(v)));
     if (const char* v = getenv("SPT_PERSISTENT")) pd_env_ = atoi(v) != 0;
     if (const char* v = getenv("SPT_PD_STAMP")) pd_stamp_path_ = v;
+    if (const char* v = getenv("SPT_PD_FORCE_GIVEUP")) pd_force_giveup_ = atoi(v);  // test hook
     // the encoder's LayerNorm fold (SPT_LN_FOLD=0: separate LayerNorm launches)
     lnf_on_ = dm_.n_enc > 0 && dm_.d % 64 == 0 && dm_.d <= 1280 && !(getenv("SPT_LN_FOLD") && atoi(getenv("SPT_LN_FOLD")) == 0);
-    pd_able_ = pdec_unsupported(dt_, dm_.d, dm_.n_head, 1, dm_.n_text_ctx, dm_.n_audio_ctx).empty();
+    // the persistent pass's resources (kernel attributes, layer table, granule arenas) only when it is
+    // asked for (every bf16 engine paid for the opt-in pass)
+    pd_able_ = pd_env_ && pdec_unsupported(dt_, dm_.d, dm_.n_head, 1, dm_.n_text_ctx, dm_.n_audio_ctx).empty();
     // cross-attention key split: fixed per engine (never per batch).  The fc2 K split (2; r1
     // exp14 measured 2 slightly faster per layer than 4: the next QKV LayerNorm prologue sums
     // fewer slabs) is fixed per engine too; the pending-slab count a LayerNorm prologue sums is
@@ -626,6 +629,7 @@ void Engine::alloc_workspace() {
             g.done = (int*)c.take(B * 4);
             g.forced = (int*)c.take(B * ctx * 4);
             g.ds = (DecState*)c.take(sizeof(DecState));
+            g.ds_save = (DecState*)c.take(sizeof(DecState));
             g.dx2 = (float*)c.take(R * d * 4);
             g.pend = (float*)c.take((int64_t)kMaxPend * R * d * 4);
             g.xpart = (float*)c.take((int64_t)R * dm_.n_head * 8 * 66 * 4);
@@ -1011,6 +1015,7 @@ float* Engine::enqueue_layers(DecGroup& g, int E, int Tq) {
         p.skv = g.skv; p.self_layer = self_layer;
         p.x = g.dx; p.xo = g.dx2; p.pend = g.pend; p.ds = g.ds; p.gran = g.gran; p.ctl = g.pctl;
         p.stamps = pd_stamps_;  // SPT_PD_STAMP (allocated with the engine), else null
+        p.force_giveup = pd_force_giveup_;
         pdec_launch(p, st);
         hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
         HIP_CHECK(hipStreamIsCapturing(st, &cap));
@@ -1467,6 +1472,7 @@ void Engine::decode(int B, const DecodeRequest& rq, int* tokens, float* top1, fl
     HIP_CHECK(hipEventRecord(ev_[6], st_));  // the decode groups wait for the encoded windows here
     pd_err_host_ = 0;
     bool gave_up = false;
+    const int pd0 = cs_.pd_passes;
     try {
         run_decode(B, rq, tokens, top1, top2, lang_out, ts_state_out);
     } catch (const PdGaveUp&) {
@@ -1485,6 +1491,7 @@ void Engine::decode(int B, const DecodeRequest& rq, int* tokens, float* top1, fl
         for (DecGroup& g : groups_) HIP_CHECK(hipStreamSynchronize(g.st));
         pd_fallback_ = true;
         cs_.pd_fallbacks++;
+        cs_.pd_passes = pd0;  // the failed attempt's passes re-run on the chain
         try {
             HIP_CHECK(hipEventRecord(ev_[6], st_));
             run_decode(B, rq, tokens, top1, top2, lang_out, ts_state_out);
@@ -1646,7 +1653,11 @@ void Engine::beam_next(const int* src, const int* tokens, const int* rowstate, i
         enqueue_head(g, 1, beam_rq_, beam_rq_.n_steps, x, suppress_, (beam_rq_.flags & 1u) != 0);
     };
     static const bool no_graph = getenv("SPT_NO_GRAPH") != nullptr;
+    // the step's head advances the decoder state (DecState) even when the persistent pass in front of
+    // it gave up: keep the starting state so the re-run starts where this step did
+    if (pd_active_) HIP_CHECK(hipMemcpyAsync(g.ds_save, g.ds, sizeof(DecState), hipMemcpyDeviceToDevice, g.st));
     for (;;) {
+        const int pd0 = cs_.pd_passes;  // an eager persistent launch counts itself; set below either way
         HIP_CHECK(hipEventRecord(ev_[8], g.st));
         if (no_graph) {
             beam_pass();
@@ -1667,12 +1678,14 @@ void Engine::beam_next(const int* src, const int* tokens, const int* rowstate, i
                 it = g.graphs.emplace(key, exec).first;
             }
             HIP_CHECK(hipGraphLaunch(it->second, g.st));
-            if (pd_active_) cs_.pd_passes++;
         }
         HIP_CHECK(hipEventRecord(ev_[9], g.st));
         pd_err_host_ = 0;
         if (pd_active_) HIP_CHECK(hipMemcpyAsync(&pd_err_host_, g.pctl + 2, 4, hipMemcpyDeviceToHost, g.st));
         read_cands(B, out);  // synchronises g.st
+        // a persistent step counts once it is known not to have given up (a step re-run
+        // on the chain was counted as persistent too)
+        cs_.pd_passes = pd0 + (pd_active_ && pd_err_host_ == 0 ? 1 : 0);
         if (!pd_active_ || pd_err_host_ == 0) break;
         // the persistent pass gave up (decode()): this step again, and the rest of the search, on
         // the launch chain (the step is idempotent: the gather, the appends and the candidates are
@@ -1680,6 +1693,7 @@ void Engine::beam_next(const int* src, const int* tokens, const int* rowstate, i
         fprintf(stderr, "[spt] persistent decoder pass gave up in a beam step (code %u); launch chain\n", pd_err_host_);
         pd_active_ = false;
         cs_.pd_fallbacks++;
+        HIP_CHECK(hipMemcpyAsync(g.ds, g.ds_save, sizeof(DecState), hipMemcpyDeviceToDevice, g.st));
     }
     beam_side_ ^= 1;
     float ms = 0.0f;

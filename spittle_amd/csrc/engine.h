@@ -181,6 +181,7 @@ private:
         int *tok_in = nullptr, *out_tok = nullptr, *done = nullptr, *forced = nullptr;
         float *out_t1 = nullptr, *out_t2 = nullptr;
         DecState* ds = nullptr;
+        DecState* ds_save = nullptr;  // beam_next: the step's starting state (a persistent step that gave up re-runs from it)
         float* dx2 = nullptr;         // second residual buffer (ping-pong with dx)
         float* pend = nullptr;        // pending partial slabs [kMaxPend][R][d]
         float* xpart = nullptr;       // cross-attention chunk partials [R][H][<=4][66]
@@ -241,6 +242,7 @@ private:
     // SPT_PD_STAMP=<file>: per-unit stage stamps of every persistent pass (k_pdec.hip), the last
     // pass of each decode call written to <file> (u64 [CUs][kPdStampMax][kPdStampRec])
     unsigned long long* pd_stamps_ = nullptr;
+    int pd_force_giveup_ = -1;  // SPT_PD_FORCE_GIVEUP=<launch index>: test hook for the give-up path
     std::string pd_stamp_path_;
     void dump_pd_stamps();
 

@@ -133,38 +133,56 @@ constexpr int EPI_LNF = 16;
 constexpr int epi_base(int e) { return e & (EPI_LNF - 1); }
 constexpr int kLnfMaxG = 40;  // groups per row: d <= 1280
 
+// the value of lane ^ X (X = 1, 2, 4, 8; within a 16-lane DPP row) by DPP moves: VALU-side, so the
+// epilogues' LDS staging traffic (in-order with ds_bpermute) does not wait behind the butterflies
+template <int X>
+__device__ __forceinline__ float xor_dpp(float v) {
+    const int i = __builtin_bit_cast(int, v);
+    if constexpr (X == 1) return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, i, 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
+    else if constexpr (X == 2) return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, i, 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
+    else if constexpr (X == 8) return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, i, 0x128, 0xF, 0xF, false));  // row_ror 8
+    else {  // lanes 0-3 of each 8 take lane + 4 (row_ror 12), lanes 4-7 take lane - 4 (row_ror 4)
+        const int up = __builtin_amdgcn_update_dpp(0, i, 0x12C, 0xF, 0xF, false);
+        const int dn = __builtin_amdgcn_update_dpp(0, i, 0x124, 0xF, 0xF, false);
+        return __builtin_bit_cast(float, (__lane_id() & 4) ? dn : up);
+    }
+}
+__device__ __forceinline__ uint32_t xor1_dpp_u(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+}
+
 // the 8 quads of a group in 8 lanes (quad index = lane bits 0..2): {sum, M2}, the same in every lane
 __device__ __forceinline__ float2 lnf_group8(float4 o) {
 #pragma clang fp contract(off)
     float s = (o.x + o.y) + (o.z + o.w);
-    s = s + __shfl_xor(s, 1, 64);
-    s = s + __shfl_xor(s, 2, 64);
-    s = s + __shfl_xor(s, 4, 64);
+    s = s + xor_dpp<1>(s);
+    s = s + xor_dpp<2>(s);
+    s = s + xor_dpp<4>(s);
     const float mean = s * (1.0f / kLnfGroup);
     const float a = o.x - mean, b = o.y - mean, c = o.z - mean, e = o.w - mean;
     const float a2 = a * a, b2 = b * b, c2 = c * c, e2 = e * e;
     float m = (a2 + b2) + (c2 + e2);
-    m = m + __shfl_xor(m, 1, 64);
-    m = m + __shfl_xor(m, 2, 64);
-    m = m + __shfl_xor(m, 4, 64);
+    m = m + xor_dpp<1>(m);
+    m = m + xor_dpp<2>(m);
+    m = m + xor_dpp<4>(m);
     return make_float2(s, m);
 }
 // MFMA-layout form: one column per lane (lane bits 0..1 = column within the quad, 2..3 = quad bits 0..1)
 // and the two fragments lo / hi of the group (quad bit 2) in registers
 __device__ __forceinline__ float2 lnf_group16(float lo, float hi) {
 #pragma clang fp contract(off)
-    float s0 = lo + __shfl_xor(lo, 1, 64), s1 = hi + __shfl_xor(hi, 1, 64);
-    s0 = s0 + __shfl_xor(s0, 2, 64); s1 = s1 + __shfl_xor(s1, 2, 64);
-    s0 = s0 + __shfl_xor(s0, 4, 64); s1 = s1 + __shfl_xor(s1, 4, 64);
-    s0 = s0 + __shfl_xor(s0, 8, 64); s1 = s1 + __shfl_xor(s1, 8, 64);
+    float s0 = lo + xor_dpp<1>(lo), s1 = hi + xor_dpp<1>(hi);
+    s0 = s0 + xor_dpp<2>(s0); s1 = s1 + xor_dpp<2>(s1);
+    s0 = s0 + xor_dpp<4>(s0); s1 = s1 + xor_dpp<4>(s1);
+    s0 = s0 + xor_dpp<8>(s0); s1 = s1 + xor_dpp<8>(s1);
     const float s = s0 + s1;
     const float mean = s * (1.0f / kLnfGroup);
     const float a = lo - mean, b = hi - mean;
     float m0 = a * a, m1 = b * b;
-    m0 = m0 + __shfl_xor(m0, 1, 64); m1 = m1 + __shfl_xor(m1, 1, 64);
-    m0 = m0 + __shfl_xor(m0, 2, 64); m1 = m1 + __shfl_xor(m1, 2, 64);
-    m0 = m0 + __shfl_xor(m0, 4, 64); m1 = m1 + __shfl_xor(m1, 4, 64);
-    m0 = m0 + __shfl_xor(m0, 8, 64); m1 = m1 + __shfl_xor(m1, 8, 64);
+    m0 = m0 + xor_dpp<1>(m0); m1 = m1 + xor_dpp<1>(m1);
+    m0 = m0 + xor_dpp<2>(m0); m1 = m1 + xor_dpp<2>(m1);
+    m0 = m0 + xor_dpp<4>(m0); m1 = m1 + xor_dpp<4>(m1);
+    m0 = m0 + xor_dpp<8>(m0); m1 = m1 + xor_dpp<8>(m1);
     return make_float2(s, m0 + m1);
 }
 __device__ __forceinline__ size_t lnf_part_index(const GemmArgs& g, int bz, int row, int col) {
@@ -186,8 +204,8 @@ __device__ __forceinline__ float2 lnf_merge(const float2 (&v)[kLnfQ], int K) {
 #pragma unroll
     for (int i = 0; i < kLnfQ; ++i)
         if (i < gq) s = s + v[i].x;
-    s = s + __shfl_xor(s, 1, 64);
-    s = s + __shfl_xor(s, 2, 64);
+    s = s + xor_dpp<1>(s);
+    s = s + xor_dpp<2>(s);
     const float mean = s / (float)K;
     float m2 = 0.f;
 #pragma unroll
@@ -199,17 +217,14 @@ __device__ __forceinline__ float2 lnf_merge(const float2 (&v)[kLnfQ], int K) {
             m2 = m2 + v[i].y;
             m2 = m2 + t;
         }
-    m2 = m2 + __shfl_xor(m2, 1, 64);
-    m2 = m2 + __shfl_xor(m2, 2, 64);
+    m2 = m2 + xor_dpp<1>(m2);
+    m2 = m2 + xor_dpp<2>(m2);
     return make_float2(mean, 1.0f / sqrtf(m2 / (float)K + 1e-5f));
 }
-// consumer output element before the activation: (acc - mean gw) rstd + bw
+// consumer output element before the activation: (acc - mean gw) rstd + bw, as two explicit FMAs
+// (the same bits in every tile shape)
 __device__ __forceinline__ float lnf_apply(float acc, float2 mr, float gw, float bw) {
-#pragma clang fp contract(off)
-    const float t = mr.x * gw;
-    float v = acc - t;
-    v = v * mr.y;
-    return v + bw;
+    return __builtin_fmaf(__builtin_fmaf(-mr.x, gw, acc), mr.y, bw);
 }
 template <typename T> __device__ __forceinline__ uint32_t lnf_pack2(float a, float b);
 template <> __device__ __forceinline__ uint32_t lnf_pack2<bf16>(float a, float b) { return pack_bf2(a, b); }
@@ -401,12 +416,17 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256,
     epi_loads_landed();
     if constexpr (lnf_c) {
         {
+            float2 mrv[MI][4];
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) mrv[i][r] = *(const float2*)(smem + STAT_OFF + (wm * (BMT / 2) + 16 * i + 4 * fq + r) * 8);
 #pragma unroll
             for (int i = 0; i < MI; ++i)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int rl = wm * (BMT / 2) + 16 * i + 4 * fq + r, row = m0 + rl;
-                    const float2 mr = *(const float2*)(smem + STAT_OFF + rl * 8);
+                    const float2 mr = mrv[i][r];
 #pragma unroll
                     for (int j = 0; j < NJ; ++j) {
                         float v = lnf_apply(acc[i][j][r], mr, lgw[j], lbw[j]);
@@ -445,11 +465,11 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256,
                             o[h] = epi_value<EPI>(g, ec[j], acc[i][j][r], y[i][j][r]);
                             const float xv = o[h] * lg[j];
                             if constexpr (sizeof(T) == 4) {
-                                const float nb = __shfl_xor(xv, 1, 64);
+                                const float nb = xor_dpp<1>(xv);
                                 if (!(fr & 1) && row < g.M)
                                     *(float2*)(xg + (size_t)row * g.ldc + ec[j].col) = make_float2(xv, nb);
                             } else {
-                                const float nb = __shfl_xor(xv, 1, 64);
+                                const float nb = xor_dpp<1>(xv);
                                 if (!(fr & 1) && row < g.M)
                                     *(uint32_t*)(xg + (size_t)row * g.ldc + ec[j].col) = lnf_pack2<T>(xv, nb);
                             }
@@ -713,6 +733,15 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
         lgw[j] = lnf_c ? g.lnf_gw[n0 + wc * 64 + 16 * j + fr] : 0.0f;
         lbw[j] = lnf_c ? g.lnf_bw[n0 + wc * 64 + 16 * j + fr] : 0.0f;
     }
+    // LayerNorm fold, consumer: {mean, rstd} of this lane's 32 accumulator rows, read from LDS once
+    // (inside the staging loop each read waited behind the staging writes before it)
+    float2 mrv[lnf_c ? 8 : 1][4];
+    if constexpr (lnf_c) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) mrv[i][r] = *(const float2*)(smem + G2_STAT + (wr * 128 + 16 * i + 4 * fq + r) * 8);
+    }
     // LayerNorm fold, producer: the next LayerNorm's gamma of this lane's 4 columns (16-byte chunk ch)
     constexpr bool lnf_p = LNF && lnf_producer<EPI>();
     float4 lg = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -747,8 +776,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
                     const int rl = 16 * ii + 4 * fq + r, cl = 16 * j + fr;
                     float v;
                     if constexpr (lnf_c)
-                        v = lnf_apply(acc[i][j][r], *(const float2*)(smem + G2_STAT + (wr * 128 + 16 * i + 4 * fq + r) * 8),
-                                      lgw[j], lbw[j]);
+                        v = lnf_apply(acc[i][j][r], mrv[lnf_c ? i : 0][r], lgw[j], lbw[j]);
                     else
                         v = acc[i][j][r] + bv[j];
                     if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_POS) v = gelu_tanh(v);
@@ -794,7 +822,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
                         // lane's 32-column group (lanes ch & ~7 .. + 7)
                         typedef typename std::conditional<F16, f16, bf16>::type T;
                         const uint32_t p0 = lnf_pack2<T>(o.x * lg.x, o.y * lg.y), p1 = lnf_pack2<T>(o.z * lg.z, o.w * lg.w);
-                        const uint32_t q0 = __shfl_xor(p0, 1, 64), q1 = __shfl_xor(p1, 1, 64);
+                        const uint32_t q0 = xor1_dpp_u(p0), q1 = xor1_dpp_u(p1);
                         if (rv && !(ch & 1))
                             *(uint4*)((T*)g.lnf_xg + (size_t)bz * g.sC + (size_t)row * g.ldc + col) = make_uint4(p0, p1, q0, q1);
                         const float2 st = lnf_group8(o);
@@ -1001,9 +1029,13 @@ void gemm_nt(int dtype, int epi, const GemmArgs& g, int batch, hipStream_t st) {
 void gemm_nt_variant(int dtype, int epi, const GemmArgs& g, int batch, int variant, hipStream_t st) {
     const int esz = dtype == DT_F32 ? 4 : 2;
     // the LayerNorm fold's kernels (kernels.h GemmArgs lnf_*)
-    if ((g.lnf_in && (epi == EPI_BIAS || epi == EPI_BIAS_GELU)) || (g.lnf_g && (epi == EPI_BIAS_RESID || epi == EPI_BIAS_GELU_POS))) {
-        if (g.K > 40 * kLnfGroup || g.K % (4 * kLnfGroup) || g.N % 64 || variant == 3)
-            throw std::runtime_error("gemm_nt: LayerNorm fold needs K <= 1280, K % 128, N % 64, a tile kernel");
+    const bool lnf_cons = g.lnf_in && (epi == EPI_BIAS || epi == EPI_BIAS_GELU);
+    const bool lnf_prod = g.lnf_g && (epi == EPI_BIAS_RESID || epi == EPI_BIAS_GELU_POS);
+    if (lnf_cons || lnf_prod) {
+        if (variant == 3 || g.ksplit != 1 || (lnf_cons && (g.K > 40 * kLnfGroup || g.K % (4 * kLnfGroup))) ||
+            (lnf_prod && (g.N > 40 * kLnfGroup || g.N % 64)))
+            throw std::runtime_error("gemm_nt: LayerNorm fold needs a tile kernel, no split-K, a consumer K <= 1280 "
+                                     "with K % 128 == 0, a producer N <= 1280 with N % 64 == 0");
         epi |= EPI_LNF;
     }
     if (g.ksplit < 1 || g.K % g.ksplit || (g.ksplit > 1 && epi != EPI_PARTIAL))

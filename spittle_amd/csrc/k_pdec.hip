@@ -60,8 +60,12 @@ constexpr int L_QKV = L_ATT + (16 + 8 * 64) * 4;           // q, k, v rows (bf16
 constexpr int L_RES = L_QKV + 8 * 66 * 4;                  // residual columns [R][16] f32
 constexpr int L_EST = L_RES + PMAXR * 16 * 4;              // cross-attention state after 3 blocks [2][9][64] + m
 constexpr int L_MISC = L_EST + 2 * (9 * 64 + 4) * 4;         // [0] abort, [1] launch index
-constexpr int L_TOTAL = L_MISC + 64;
+constexpr int PMAXL = 32;                                    // decoder layers (the layer table below)
+constexpr int L_LAYERS = L_MISC + 64;                        // the layers' weight pointers (PdLayer [L])
+constexpr int L_KVROW = L_LAYERS + PMAXL * (int)sizeof(PdLayer);  // the rows' windows (a.kvrow) [PMAXR]
+constexpr int L_TOTAL = L_KVROW + 64;
 static_assert(L_TOTAL > 80 * 1024 && L_TOTAL <= 160 * 1024, "one workgroup per CU");
+static_assert(sizeof(PdLayer) % 8 == 0, "layer table copy in 8-byte words");
 static_assert((L_RED % 16) == 0 && (L_ATT % 16) == 0 && (L_QKV % 16) == 0 && (L_RES % 16) == 0 && (L_EST % 16) == 0 &&
                   (L_MISC % 16) == 0, "align");
 
@@ -74,6 +78,17 @@ __device__ __forceinline__ void st_rlx(unsigned* p, unsigned v) {
 // one granule: ONE 8-byte write-through store {value (low word), epoch (high word)}
 __device__ __forceinline__ void gran_put(u64* base, int64_t i, unsigned ep, unsigned v) {
     __hip_atomic_store((gu64*)(base + i), ((u64)ep << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// pointers read from the LDS layer table are generic to the compiler (flat loads: counted on both
+// vmcnt and lgkmcnt and waited for with both at 0); the weights and LayerNorm / bias vectors are
+// global memory, so say so
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* gp(const void* p) {
+    return (const __attribute__((address_space(1))) T*)p;
+}
+// float4 (a HIP struct) has no assignment from an address-space-qualified reference: load the bits
+__device__ __forceinline__ float4 gp_f4(const float* p) {
+    return __builtin_bit_cast(float4, *gp<u32x4>(p));
 }
 __device__ __forceinline__ unsigned fbits(float f) { return __builtin_bit_cast(unsigned, f); }
 __device__ __forceinline__ float bitsf(unsigned u) { return __builtin_bit_cast(float, u); }
@@ -137,17 +152,52 @@ __device__ __forceinline__ void stamp(const PdArgs& a, int wg, int k, int f, u64
 // B = 1 sat in barrier B).  So: the wave's own LDS ops (lgkmcnt(0)), then a bare s_barrier.
 #define PD_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
+// Kernel-argument arrays by constant index only: a runtime index into a.go / a.n / a.pre made the
+// compiler copy the whole argument block to scratch and read EVERY field of `a` from there (scratch
+// loads count on vmcnt, so each one also waited behind the weight stream in flight; r6: 376 B of
+// scratch per lane).  A switch keeps each access a constant-offset argument load.
+__device__ __forceinline__ int64_t go_of(const PdArgs& a, int i) {
+    switch (i) {
+        case 0: return a.go[0]; case 1: return a.go[1]; case 2: return a.go[2]; case 3: return a.go[3];
+        case 4: return a.go[4]; case 5: return a.go[5]; case 6: return a.go[6]; case 7: return a.go[7];
+        case 8: return a.go[8]; case 9: return a.go[9]; case 10: return a.go[10]; default: return a.go[11];
+    }
+}
+__device__ __forceinline__ int n_of(const PdArgs& a, int s) {
+    switch (s) {
+        case 0: return a.n[0]; case 1: return a.n[1]; case 2: return a.n[2]; case 3: return a.n[3]; case 4: return a.n[4];
+        case 5: return a.n[5]; case 6: return a.n[6]; case 7: return a.n[7]; default: return a.n[8];
+    }
+}
+__device__ __forceinline__ int pre_of(const PdArgs& a, int s) {
+    switch (s) {
+        case 0: return a.pre[0]; case 1: return a.pre[1]; case 2: return a.pre[2]; case 3: return a.pre[3]; case 4: return a.pre[4];
+        case 5: return a.pre[5]; case 6: return a.pre[6]; case 7: return a.pre[7]; default: return a.pre[8];
+    }
+}
+
 // ------------------------------------------------------------------ geometry helpers
 struct Cur { int l, s, u; };
 
 __device__ __forceinline__ int unit0(const PdArgs& a, int l, int s, int wg) {
-    const int base = (int)(((int64_t)l * a.U + a.pre[s]) % a.nwg);
+    const int base = (int)(((int64_t)l * a.U + pre_of(a, s)) % a.nwg);
     return (wg - base + a.nwg) % a.nwg;
 }
-// this workgroup's next unit in (layer, stage, unit) order
+// this workgroup's next unit in (layer, stage, unit) order.  The cursor is wave-uniform; readfirstlane
+// says so to the compiler, so the per-stage branches are scalar (as exec-masked branches their joins
+// merged the prefetch registers and waited vmcnt(0) for the loads just issued: r6 stamps, 2-3 us of
+// "prefetch issue" per unit)
+__device__ __forceinline__ bool advance_(const PdArgs& a, int wg, Cur& c);
 __device__ __forceinline__ bool advance(const PdArgs& a, int wg, Cur& c) {
+    const bool r = advance_(a, wg, c);
+    c.l = __builtin_amdgcn_readfirstlane(c.l);
+    c.s = __builtin_amdgcn_readfirstlane(c.s);
+    c.u = __builtin_amdgcn_readfirstlane(c.u);
+    return __builtin_amdgcn_readfirstlane((int)r) != 0;
+}
+__device__ __forceinline__ bool advance_(const PdArgs& a, int wg, Cur& c) {
     c.u += a.nwg;
-    while (c.u >= a.n[c.s]) {
+    while (c.u >= n_of(a, c.s)) {
         if (++c.s == kPdStages) {
             c.s = 0;
             if (++c.l == a.L) return false;
@@ -171,15 +221,17 @@ __device__ __forceinline__ Gv gv_of(const PdArgs& a, const PdLayer& Lw, int s, i
     g.K = a.d;
     g.s0 = 0;
     g.s1 = a.d / 128;
-    g.ks = a.ks[s];
+    // constant indices into the kernel arguments (a dynamic a.ks[s] was a vector load of the argument
+    // block that the prefetch's address arithmetic waited for)
     switch (s) {
-        case S_A: g.W = (const bf16*)Lw.qkv_w; break;
-        case S_C: g.W = (const bf16*)Lw.so_w; break;
-        case S_D: g.W = (const bf16*)Lw.cq_w; break;
-        case S_F: g.W = (const bf16*)Lw.co_w; break;
-        case S_G: g.W = (const bf16*)Lw.fc1_w; break;
+        case S_A: g.W = (const bf16*)Lw.qkv_w; g.ks = a.ks[S_A]; break;
+        case S_C: g.W = (const bf16*)Lw.so_w; g.ks = a.ks[S_C]; break;
+        case S_D: g.W = (const bf16*)Lw.cq_w; g.ks = a.ks[S_D]; break;
+        case S_F: g.W = (const bf16*)Lw.co_w; g.ks = a.ks[S_F]; break;
+        case S_G: g.W = (const bf16*)Lw.fc1_w; g.ks = a.ks[S_G]; break;
         default: {  // S_H
             const int nss = 4 * (a.d / 128), per = (nss + 1) / 2, z = u & 1;
+            g.ks = a.ks[S_H];
             g.W = (const bf16*)Lw.fc2_w;
             g.n0 = 16 * (u >> 1);
             g.K = 4 * a.d;
@@ -222,15 +274,15 @@ __device__ __forceinline__ void e_block_load(const PdArgs& a, const bf16* Kb, in
     for (int i = 0; i < 4; ++i) {
         const int key = min(blk * 32 + 8 * i + slot, a.T_enc - 1);
         const uint32_t off = (uint32_t)((key >> 5) * bstride + (key & 31) * 64);
-        kc[i] = *(const u32x4*)(Kb + off);
-        vc[i] = *(const u32x4*)(Kb + off + 2048);
+        kc[i] = *gp<u32x4>(Kb + off);
+        vc[i] = *gp<u32x4>(Kb + off + 2048);
     }
 }
 // cross-attention unit u: e_vw virtual waves (of the 8-wave kernel) of one (row, head); compute
 // wave cw takes virtual wave vw of it, key blocks 3 * half .. + 2 (half = cw & 1: the second half
 // continues the first half's online-softmax state, handed over in LDS)
 struct Eu { int bh, vw, vi, half; const bf16* Kb; };
-__device__ __forceinline__ Eu e_unit(const PdArgs& a, int l, int u, int cw, int lane) {
+__device__ __forceinline__ Eu e_unit(const PdArgs& a, const int* kvrow, int l, int u, int cw, int lane) {
     Eu e;
     const int per_bh = 8 / a.e_vw;
     e.bh = u / per_bh;
@@ -238,25 +290,30 @@ __device__ __forceinline__ Eu e_unit(const PdArgs& a, int l, int u, int cw, int 
     e.half = cw & 1;
     e.vw = (u - e.bh * per_bh) * a.e_vw + e.vi;
     const int b = e.bh / a.H, h = e.bh - b * a.H;
-    const int kb = a.kvrow ? a.kvrow[b] : b;
+    const int kb = kvrow ? kvrow[b] : b;  // the window map, copied to LDS at kernel start
     e.Kb = (const bf16*)a.ckv + a.cross_layer * l + ((size_t)kb * a.H + h) * 4096 + 8 * (lane & 7);
     return e;
 }
 
-__device__ __forceinline__ void prefetch(const PdArgs& a, const Cur& c, int cw, int lane, int pos0, u32x4 (&pre)[PNPRE]) {
+__device__ __forceinline__ void prefetch(const PdArgs& a, const PdLayer* layers, const int* kvrow, const Cur& c, int cw,
+                                         int lane, int pos0, u32x4 (&pre)[PNPRE]) {
     const u32x4 z = {0u, 0u, 0u, 0u};
-    const PdLayer& Lw = a.layers[c.l];
+    const PdLayer& Lw = layers[c.l];
     const int fr = lane & 15, fq = lane >> 4;
     const int slot = lane >> 3;
     if (is_gemv(c.s)) {
         const Gv g = gv_of(a, Lw, c.s, c.u);
         int ss[PMAXSS], gc[PMAXSS];
         gv_plan(g, cw, ss, gc);
-        const bf16* wrow = g.W + (size_t)(g.n0 + fr) * g.K + fq * 8;
+        const __attribute__((address_space(1))) bf16* wrow = gp<bf16>(g.W) + (size_t)(g.n0 + fr) * g.K + fq * 8;
+        // unconditional loads (a super-step the wave does not own reads super-step 0 and is never
+        // used): a load under a condition made hipcc wait vmcnt(0) for each before the next (r6 stamps:
+        // the prefetch "issue" took 2-3 us per unit, a round trip per load)
 #pragma unroll
         for (int k = 0; k < PMAXSS; ++k)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) pre[4 * k + i] = ss[k] >= 0 ? *(const u32x4*)(wrow + ss[k] * 128 + i * 32) : z;
+            for (int i = 0; i < 4; ++i)
+                pre[4 * k + i] = *(const __attribute__((address_space(1))) u32x4*)(wrow + max(ss[k], 0) * 128 + i * 32);
 #pragma unroll
         for (int k = 4 * PMAXSS; k < PNPRE; ++k) pre[k] = z;
         return;
@@ -264,7 +321,7 @@ __device__ __forceinline__ void prefetch(const PdArgs& a, const Cur& c, int cw, 
     if (c.s == S_B) {  // the first self K/V block of virtual waves cw, cw + 4 (positions < 256; a
                        // second block, positions 256..447, is loaded when the unit runs)
         const int b = c.u / a.H, h = c.u - b * a.H;
-        const int nk = pos0 + 1, nblk = cdiv(nk, 32);
+        const int nk = pos0 + 1;
         const bf16* kv = (const bf16*)a.skv + a.self_layer * c.l;
         const bf16* Kb = kv + (((size_t)0 * a.R + b) * a.H + h) * (size_t)a.ctx * 64 + 8 * (lane & 7);
         const bf16* Vb = kv + (((size_t)1 * a.R + b) * a.H + h) * (size_t)a.ctx * 64 + 8 * (lane & 7);
@@ -272,10 +329,10 @@ __device__ __forceinline__ void prefetch(const PdArgs& a, const Cur& c, int cw, 
         for (int v = 0; v < 2; ++v) {
             const int blk = cw + 4 * v;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < 4; ++i) {  // unconditional (clamped key; a block past nblk is never used)
                 const int key = min(blk * 32 + 8 * i + slot, nk - 1);
-                pre[(v * 4 + i) * 2 + 0] = blk < nblk ? *(const u32x4*)(Kb + key * 64) : z;
-                pre[(v * 4 + i) * 2 + 1] = blk < nblk ? *(const u32x4*)(Vb + key * 64) : z;
+                pre[(v * 4 + i) * 2 + 0] = *gp<u32x4>(Kb + key * 64);
+                pre[(v * 4 + i) * 2 + 1] = *gp<u32x4>(Vb + key * 64);
             }
         }
 #pragma unroll
@@ -283,17 +340,17 @@ __device__ __forceinline__ void prefetch(const PdArgs& a, const Cur& c, int cw, 
         return;
     }
     if (c.s == S_E && (cw >> 1) < a.e_vw) {  // cross K/V blocks 3 half .. 3 half + 2 of virtual wave vw
-        const Eu e = e_unit(a, c.l, c.u, cw, lane);
+        const Eu e = e_unit(a, kvrow, c.l, c.u, cw, lane);
         const int nblk = cdiv(a.T_enc, 32);
 #pragma unroll
-        for (int t = 0; t < 3; ++t) {
+        for (int t = 0; t < 3; ++t) {  // unconditional (e_block_load clamps the key; unused past nblk)
             const int blk = e.vw + 8 * (3 * e.half + t);
             u32x4 kc[4], vc[4];
-            if (blk < nblk) e_block_load(a, e.Kb, blk, slot, kc, vc);
+            e_block_load(a, e.Kb, min(blk, nblk - 1), slot, kc, vc);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                pre[(t * 4 + i) * 2 + 0] = blk < nblk ? kc[i] : z;
-                pre[(t * 4 + i) * 2 + 1] = blk < nblk ? vc[i] : z;
+                pre[(t * 4 + i) * 2 + 0] = kc[i];
+                pre[(t * 4 + i) * 2 + 1] = vc[i];
             }
         }
 #pragma unroll
@@ -316,8 +373,8 @@ __device__ __forceinline__ bool gather_ln(const PdArgs& a, __amdgpu_buffer_rsrc_
     for (int i = 0; i < NC; ++i) {
         const int k = lane * 4 + 256 * i;
         if (k < K) {
-            lnw_pre[i] = *(const float4*)(ln_w + k);
-            lnb_pre[i] = *(const float4*)(ln_b + k);
+            lnw_pre[i] = gp_f4(ln_w + k);
+            lnb_pre[i] = gp_f4(ln_b + k);
         }
     }
     for (int r = gw; r < a.R; r += 4) {
@@ -334,7 +391,7 @@ __device__ __forceinline__ bool gather_ln(const PdArgs& a, __amdgpu_buffer_rsrc_
 #pragma unroll
             for (int i = 0; i < NC; ++i) {
                 const int k = lane * 4 + 256 * i;
-                const unsigned o = (unsigned)((a.go[src] + (int64_t)r * K + k) * 8);
+                const unsigned o = (unsigned)((go_of(a, src) + (int64_t)r * K + k) * 8);
                 off[2 * i] = o;
                 off[2 * i + 1] = o + 16;
                 if (k < K) valid |= 3u << (2 * i);
@@ -389,7 +446,7 @@ __device__ __forceinline__ bool gather_img(const PdArgs& a, __amdgpu_buffer_rsrc
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const int p = p0 + k * 256 + gt;
-            off[k] = (unsigned)((a.go[src] + 2 * (int64_t)p) * 8);
+            off[k] = (unsigned)((go_of(a, src) + 2 * (int64_t)p) * 8);
             if (p < pieces) valid |= 1u << k;
         }
         u32x4 v[16];
@@ -419,7 +476,7 @@ __device__ __forceinline__ bool gather_cols(const PdArgs& a, __amdgpu_buffer_rsr
         }
         return true;
     }
-    unsigned off[1] = {(unsigned)((a.go[src] + (int64_t)r * a.d + n0 + 2 * pc) * 8)};
+    unsigned off[1] = {(unsigned)((go_of(a, src) + (int64_t)r * a.d + n0 + 2 * pc) * 8)};
     u32x4 v[1];
     if (!poll<1>(a, rs, off, r < a.R ? 1u : 0u, ep, v)) return false;
     if (r < a.R) {
@@ -433,7 +490,7 @@ __device__ __forceinline__ bool gather_cols(const PdArgs& a, __amdgpu_buffer_rsr
 __device__ __forceinline__ bool gather_head(const PdArgs& a, __amdgpu_buffer_rsrc_t rs, const int* srcs, int nsrc,
                                             int b, int h, unsigned ep, bf16* dst, int lane) {
     const int j = lane >> 4, pc = lane & 15;  // buffer, piece of 4 bf16
-    unsigned off[1] = {(unsigned)((a.go[j < nsrc ? srcs[j] : 0] + (int64_t)b * (a.d / 2) + 32 * h + 2 * pc) * 8)};
+    unsigned off[1] = {(unsigned)((go_of(a, j < nsrc ? srcs[j] : 0) + (int64_t)b * (a.d / 2) + 32 * h + 2 * pc) * 8)};
     u32x4 v[1];
     if (!poll<1>(a, rs, off, j < nsrc ? 1u : 0u, ep, v)) return false;
     if (j < nsrc) *(uint2*)(dst + j * 64 + 4 * pc) = uint2{v[0].x, v[0].z};
@@ -445,7 +502,7 @@ __device__ __forceinline__ bool gather_part(const PdArgs& a, __amdgpu_buffer_rsr
                                             float* part, int gt) {
     unsigned off[2];
     unsigned valid = 0;
-    const int64_t base = a.go[G_PART] + ((int64_t)b * a.H + h) * 8 * 66;
+    const int64_t base = go_of(a, G_PART) + ((int64_t)b * a.H + h) * 8 * 66;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const int p = gt + 256 * k;  // 264 pieces
@@ -468,6 +525,9 @@ __device__ __forceinline__ bool gather_part(const PdArgs& a, __amdgpu_buffer_rsr
 // ------------------------------------------------------------------ the kernel
 struct Smem {
     volatile unsigned* misc;
+    const int* kvrow;       // LDS copy of a.kvrow (null: row b -> window b)
+    const PdLayer* layers;  // LDS copy of a.layers (r6 stamps: the prefetch's scalar loads of the global
+                            // table stalled its issue 2-3 us per unit)
     bf16* img;
     f32x4* red;
     float (*s_m)[1];
@@ -496,7 +556,7 @@ __device__ __forceinline__ void gather_loop(const PdArgs& a, const Smem& sm, uns
     const bool stp = a.stamps != nullptr && wave == 0;
     int nk = 0;  // units this workgroup has run (stamp record index)
     while (has) {
-        const PdLayer& Lw = a.layers[c.l];
+        const PdLayer& Lw = sm.layers[c.l];
         const int key = (c.l << 4) | c.s;
         if (stp) {
             stamp(a, wg, nk, 0, (u64)c.l | ((u64)c.s << 8) | ((u64)c.u << 16), lane);
@@ -556,7 +616,7 @@ __device__ __forceinline__ void gather_loop(const PdArgs& a, const Smem& sm, uns
             const float* bias = c.s == S_A ? Lw.qkv_b : c.s == S_C ? Lw.so_b : c.s == S_D ? Lw.cq_b
                               : c.s == S_F ? Lw.co_b : c.s == S_G ? Lw.fc1_b : Lw.fc2_b;
             const int n0 = c.s == S_H ? 16 * (c.u >> 1) : 16 * c.u;
-            bv = (bias && !(c.s == S_H && (c.u & 1))) ? bias[n0 + fr] : 0.f;  // fc2: slab 0 carries the bias
+            bv = (bias && !(c.s == S_H && (c.u & 1))) ? gp<float>(bias)[n0 + fr] : 0.f;  // fc2: slab 0 carries the bias
         }
         PD_BARRIER();  // A: inputs in LDS
         if (sm.misc[0]) break;
@@ -586,7 +646,7 @@ __device__ __forceinline__ void gather_loop(const PdArgs& a, const Smem& sm, uns
                 const unsigned nb = __shfl_xor(mine, 1, 64);
                 if (!(e & 1)) {
                     const int b = c.u / a.H, h = c.u - b * a.H;
-                    gran_put(a.gran, a.go[G_M] + (int64_t)b * (a.d / 2) + 32 * h + e / 2, ep, mine | (nb << 16));
+                    gran_put(a.gran, go_of(a, G_M) + (int64_t)b * (a.d / 2) + 32 * h + e / 2, ep, mine | (nb << 16));
                 }
         }
         if (c.s == S_E) PD_BARRIER();  // E mid: the first halves' softmax state in LDS
@@ -626,7 +686,7 @@ __device__ __forceinline__ void gather_loop(const PdArgs& a, const Smem& sm, uns
                             }
                             const unsigned nb = __shfl_xor((unsigned)yb, 1, 64);
                             if (!(fr & 1) && row < a.R)
-                                gran_put(a.gran, a.go[gsrc] + (int64_t)row * (a.d / 2) + rem / 2, ep, (unsigned)yb | (nb << 16));
+                                gran_put(a.gran, go_of(a, gsrc) + (int64_t)row * (a.d / 2) + rem / 2, ep, (unsigned)yb | (nb << 16));
                         }
                         break;
                     }
@@ -638,7 +698,7 @@ __device__ __forceinline__ void gather_loop(const PdArgs& a, const Smem& sm, uns
                             if (row >= a.R) continue;
                             const float y = v0[r] + bv;
                             const float o = resv[r] + y;
-                            gran_put(a.gran, a.go[c.s == S_C ? G_XC : G_XF] + (int64_t)row * a.d + n, ep, fbits(o));
+                            gran_put(a.gran, go_of(a, c.s == S_C ? G_XC : G_XF) + (int64_t)row * a.d + n, ep, fbits(o));
                             if (c.s == S_F && last) a.xo[(size_t)row * a.d + n] = o;
                         }
                         break;
@@ -653,7 +713,7 @@ __device__ __forceinline__ void gather_loop(const PdArgs& a, const Smem& sm, uns
                             const bf16 yb = from_f<bf16>(c.s == S_D ? y : gelu_tanh(y));
                             const unsigned nb = __shfl_xor((unsigned)yb, 1, 64);
                             if (!(fr & 1) && row < a.R)
-                                gran_put(a.gran, a.go[c.s == S_D ? G_QX : G_H] + (int64_t)row * (N / 2) + n / 2, ep,
+                                gran_put(a.gran, go_of(a, c.s == S_D ? G_QX : G_H) + (int64_t)row * (N / 2) + n / 2, ep,
                                          (unsigned)yb | (nb << 16));
                         }
                         break;
@@ -664,7 +724,7 @@ __device__ __forceinline__ void gather_loop(const PdArgs& a, const Smem& sm, uns
                         float p0v[4] = {0.f, 0.f, 0.f, 0.f};
                         if (z1 && !last) {  // slab 0's columns (its unit runs beside this one)
                             const int r8 = lane >> 3, pc = lane & 7;
-                            unsigned off[1] = {(unsigned)((a.go[G_P0] + (int64_t)r8 * a.d + g.n0 + 2 * pc) * 8)};
+                            unsigned off[1] = {(unsigned)((go_of(a, G_P0) + (int64_t)r8 * a.d + g.n0 + 2 * pc) * 8)};
                             u32x4 pv[1];
                             if (!poll<1>(a, rs, off, r8 < a.R ? 1u : 0u, ep_of(launch, L, c.l, S_H), pv)) {
                                 sm.misc[0] = 1u;  // seen by every wave at the next barrier A
@@ -687,12 +747,12 @@ __device__ __forceinline__ void gather_loop(const PdArgs& a, const Smem& sm, uns
                             if (last) {
                                 a.pend[((size_t)(z1 ? a.R : 0) + row) * a.d + n] = p;
                             } else if (!z1) {
-                                gran_put(a.gran, a.go[G_P0] + (int64_t)row * a.d + n, ep, fbits(p));
+                                gran_put(a.gran, go_of(a, G_P0) + (int64_t)row * a.d + n, ep, fbits(p));
                             } else {
                                 float xn = resv[r];
                                 xn += p0v[r];
                                 xn += p;
-                                gran_put(a.gran, a.go[G_X] + (int64_t)row * a.d + n, ep, fbits(xn));
+                                gran_put(a.gran, go_of(a, G_X) + (int64_t)row * a.d + n, ep, fbits(xn));
                             }
                         }
                         break;
@@ -704,7 +764,7 @@ __device__ __forceinline__ void gather_loop(const PdArgs& a, const Smem& sm, uns
                 attn_merge<1>(sm.s_m, sm.s_l, sm.s_o, 0, lane, M, Ls, O);
                 const unsigned mine = (unsigned)from_f<bf16>(O / Ls);
                 const unsigned nb = __shfl_xor(mine, 1, 64);
-                if (!(lane & 1)) gran_put(a.gran, a.go[G_A] + (int64_t)b * (a.d / 2) + 32 * h + lane / 2, ep, mine | (nb << 16));
+                if (!(lane & 1)) gran_put(a.gran, go_of(a, G_A) + (int64_t)b * (a.d / 2) + 32 * h + lane / 2, ep, mine | (nb << 16));
             }
         }
         if (stp) {  // the publish has landed (diagnostic builds of a pass only: waits for the stores)
@@ -719,7 +779,7 @@ __device__ __forceinline__ void gather_loop(const PdArgs& a, const Smem& sm, uns
 // waves 4-7: per unit, barrier A, the unit's arithmetic and the next unit's prefetch, barrier B
 __device__ __forceinline__ void compute_loop(const PdArgs& a, const Smem& sm, unsigned launch, int wg, int pos0) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int cw = wave - 4;
+    const int cw = __builtin_amdgcn_readfirstlane(wave - 4);  // wave-uniform for the compiler too
     const int fr = lane & 15, fq = lane >> 4;
     const int L = a.L;
     bf16* img = sm.img;
@@ -729,9 +789,9 @@ __device__ __forceinline__ void compute_loop(const PdArgs& a, const Smem& sm, un
     u32x4 pre[PNPRE];
     const bool stp = a.stamps != nullptr && cw == 0;
     int nk = 0;
-    if (has) prefetch(a, c, cw, lane, pos0, pre);
+    if (has) prefetch(a, sm.layers, sm.kvrow, c, cw, lane, pos0, pre);
     while (has) {
-        const PdLayer& Lw = a.layers[c.l];
+        const PdLayer& Lw = sm.layers[c.l];
         const unsigned ep = ep_of(launch, L, c.l, c.s);
         Cur nx = c;
         const bool nhas = advance(a, wg, nx);
@@ -817,7 +877,7 @@ __device__ __forceinline__ void compute_loop(const PdArgs& a, const Smem& sm, un
                 aw.to_lds(sm.s_m, sm.s_l, sm.s_o, vw, lane);
             }
         } else if (c.s == S_E) {
-            const Eu e = e_unit(a, c.l, c.u, cw, lane);
+            const Eu e = e_unit(a, sm.kvrow, c.l, c.u, cw, lane);
             const bool on = e.vi < a.e_vw;
             const int g8 = lane & 7;
             float qv[1][8];
@@ -859,7 +919,7 @@ __device__ __forceinline__ void compute_loop(const PdArgs& a, const Smem& sm, un
                 run3();
                 aw.to_lds(sm.s_m, sm.s_l, sm.s_o, e.vi, lane);
                 // partial vw of (b, h): {o[64], m, l}, as cross_attn_vw_kernel writes it
-                const int64_t pb = a.go[G_PART] + ((int64_t)e.bh * 8 + e.vw) * 66;
+                const int64_t pb = go_of(a, G_PART) + ((int64_t)e.bh * 8 + e.vw) * 66;
                 gran_put(a.gran, pb + lane, ep, fbits(sm.s_o[e.vi][0][lane]));
                 if (lane == 0) {
                     gran_put(a.gran, pb + 64, ep, fbits(sm.s_m[e.vi][0]));
@@ -868,9 +928,11 @@ __device__ __forceinline__ void compute_loop(const PdArgs& a, const Smem& sm, un
             }
         }
         if (stp) stamp(a, wg, nk, 6, wall_clock64(), lane);
-        ++nk;
-        if (nhas) prefetch(a, nx, cw, lane, pos0, pre);
+        if (nhas) prefetch(a, sm.layers, sm.kvrow, nx, cw, lane, pos0, pre);
+        if (stp) stamp(a, wg, nk, 8, wall_clock64(), lane);
         PD_BARRIER();  // B: chain partials / attention partials in LDS; the image is free again
+        if (stp) stamp(a, wg, nk, 9, wall_clock64(), lane);
+        ++nk;
         c = nx;
         has = nhas;
     }
@@ -881,6 +943,11 @@ __global__ __launch_bounds__(PT, 1) void pdec_kernel(PdArgs a) {
     const int tid = threadIdx.x;
     Smem sm;
     sm.misc = (volatile unsigned*)(smem + L_MISC);
+    sm.layers = (const PdLayer*)(smem + L_LAYERS);
+    sm.kvrow = a.kvrow ? (const int*)(smem + L_KVROW) : nullptr;
+    if (a.kvrow && tid < a.R) ((int*)(smem + L_KVROW))[tid] = a.kvrow[tid];
+    for (int i = tid; i < a.L * (int)(sizeof(PdLayer) / 8); i += PT)
+        ((unsigned long long*)(smem + L_LAYERS))[i] = ((const unsigned long long*)a.layers)[i];
     sm.img = (bf16*)(smem + L_IMG);
     sm.red = (f32x4*)(smem + L_RED);
     sm.s_m = (float (*)[1])(smem + L_ATT);
@@ -892,15 +959,20 @@ __global__ __launch_bounds__(PT, 1) void pdec_kernel(PdArgs a) {
     sm.est = (float*)(smem + L_EST);
     volatile unsigned* misc = sm.misc;
     if (tid == 0) {
-        const unsigned err = ld_rlx(a.ctl + 2);
+        unsigned err = ld_rlx(a.ctl + 2);
+        const unsigned li = ld_rlx(a.ctl + 3);
+        if (!err && (int)li == a.force_giveup) {  // test hook: this launch gives up as a starved one would
+            st_rlx(a.ctl + 2, 3u);
+            err = 3u;
+        }
         misc[0] = err;
-        misc[1] = ld_rlx(a.ctl + 3);
+        misc[1] = li;
         if (!err) __hip_atomic_fetch_add((gu32*)a.ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     if (misc[0]) return;
-    const unsigned launch = misc[1];
-    const int pos0 = a.ds->pos0;
+    const unsigned launch = __builtin_amdgcn_readfirstlane(misc[1]);  // uniform (see advance)
+    const int pos0 = __builtin_amdgcn_readfirstlane(a.ds->pos0);
     if ((tid >> 6) < 4) gather_loop(a, sm, launch, blockIdx.x, pos0);
     else compute_loop(a, sm, launch, blockIdx.x, pos0);
     __syncthreads();
@@ -950,6 +1022,7 @@ void pdec_prepare() { ensure_lds_attr((const void*)pdec_kernel, L_TOTAL); }
 void pdec_launch(PdArgs a, hipStream_t st) {
     const std::string why = pdec_unsupported(DT_BF16, a.d, a.H, a.R, a.ctx, a.T_enc);
     if (!why.empty()) throw std::runtime_error("persistent decoder pass: unsupported " + why);
+    if (a.L < 1 || a.L > PMAXL) throw std::runtime_error("persistent decoder pass: unsupported layer count");
     int dev = 0;
     HIP_CHECK(hipGetDevice(&dev));
     a.nwg = cu_count(dev);

@@ -244,6 +244,8 @@ struct PdArgs {
     const DecState* ds;
     unsigned long long* gran;                 // granule arena: pdec_granules() words, zeroed per call
     unsigned* ctl;                            // [4] census, exits, error, launch index (zeroed per call)
+    int force_giveup;                         // test hook (SPT_PD_FORCE_GIVEUP): the launch of this
+                                              // index within a call gives up (-1: never)
     unsigned long long* stamps;               // diagnostics (SPT_PD_STAMP): per workgroup kPdStampMax
                                               // records of kPdStampRec s_memrealtime words, or null
     // geometry (pdec_launch fills it)
@@ -255,8 +257,9 @@ int64_t pdec_granules(int R, int d, int H);
 constexpr int kPdCtlWords = 4;
 // per-unit stage stamps (100 MHz s_memrealtime) of one pass, record = {meta = l | s << 8 | u << 16,
 // gather start, gather wave 0 inputs ready, compute after barrier A, compute weights landed, gather
-// after barrier B, compute done, publish landed}
-constexpr int kPdStampRec = 8, kPdStampMax = 512;
+// after barrier B, compute done, publish landed, compute after issuing the next unit's prefetch,
+// compute after barrier B}
+constexpr int kPdStampRec = 10, kPdStampMax = 512;
 // empty string if the persistent pass can run this geometry, else why not
 std::string pdec_unsupported(int dtype, int d, int H, int R, int ctx, int T_enc);
 void pdec_launch(PdArgs a, hipStream_t st);

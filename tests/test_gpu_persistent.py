@@ -105,3 +105,30 @@ def test_full_depth_large_v3_bitwise(B, monkeypatch):
     ref, got, cs = _both("synthetic:large-v3", 8, xs, _fast(n), monkeypatch)
     assert cs["pd_passes"] == n - 1 and cs["pd_fallbacks"] == 0, cs
     _assert_bitwise(ref, got)
+
+
+@pytest.mark.parametrize("case", ["fast_b1", "fast_b8", "beam5", "best_of5"])
+def test_forced_give_up_reruns_bitwise(case, monkeypatch):
+    """The give-up path: SPT_PD_FORCE_GIVEUP=k makes the k-th persistent launch of every
+    call set the error word, as a pass starved of CUs would.  The fast path then re-runs the whole
+    call on the launch chain (Engine::decode), a beam search re-runs the step and continues on the
+    chain (beam_next); the persistent attempt's later launches leave at once.  Tokens, top-1 / top-2
+    and segments must still be the chain's bit for bit, with pd_fallbacks counted and no give-up
+    counted as a persistent pass."""
+    monkeypatch.setenv("SPT_PD_FORCE_GIVEUP", "3")
+    if case.startswith("fast"):
+        B = 1 if case == "fast_b1" else 8
+        xs = [O.synth_audio(230 + i, (10 + i) * 16000) for i in range(B)]
+        p = _fast(12)
+    else:
+        xs = [O.synth_audio(240, 12 * 16000), O.synth_audio(241, 35 * 16000)]
+        kw = dict(beam_size=5, max_new_tokens=10) if case == "beam5" else \
+            dict(temperature_inc=0.2, logprob_thold=10.0, best_of=5, max_new_tokens=10, seed=22)
+        p = _full(**kw)
+    ref, got, cs = _both("synthetic:large-v3:enc=2:dec=2", 8, xs, p, monkeypatch)
+    assert cs["pd_fallbacks"] >= 1, cs
+    if case.startswith("fast"):
+        assert cs["pd_passes"] == 0, cs  # the re-run call ran on the chain only
+    _assert_bitwise(ref, got)
+    for a, b in zip(ref, got):
+        assert [(s.start, s.end, s.text) for s in a.segments] == [(s.start, s.end, s.text) for s in b.segments]
