@@ -186,12 +186,9 @@ spt_status spt_get_timings(const spt_ctx* ctx, spt_timings* t);
  * own reflective head, the utterance's global max - 8 clamp) and encodes each 30 s window at
  * `seek` once (whisper_encode_internal), shared by every temperature fallback and by the
  * utterance's beam / best_of decoders: encoder_windows counts those encoder runs.
- * ABI 12: opt-in (SPT_PERSISTENT=1 in the environment, read when a context is created): one-token
- * decoder passes of up to 8 rows run every decoder layer as ONE persistent launch (bitwise the
- * per-stage launch chain, measured slower: DESIGN.md 4.1f); pd_passes counts them.  It needs every
- * CU: when another context's or process's kernels hold some, the pass gives up and the call is
- * re-run on the launch chain (pd_fallbacks; the result is the same).  Default: the launch chain,
- * both counters 0.
+ * ABI 12: pd_passes / pd_fallbacks counted round 5's opt-in persistent decoder pass; round 6
+ * measured it at the persistent-kernel price list's cost, slower than the launch chain at every
+ * batch, and deleted it: both counters are always 0 (kept for layout).
  * device_ms (and spt_timings.total_ms) sum the stage intervals (mel, window norm, encoder, cross
  * K/V, decode); host time between the stages is not in them. */
 typedef struct {
@@ -204,8 +201,8 @@ typedef struct {
     double device_ms;         /* device time of those runs and steps (HIP events) */
     double encoder_ms;
     double decode_ms;         /* decoder passes incl. prompt prefill and sampling */
-    int32_t pd_passes;        /* ABI 12: decoder passes that ran as one persistent launch */
-    int32_t pd_fallbacks;     /* ABI 12: calls / beam steps re-run on the launch chain */
+    int32_t pd_passes;        /* ABI 12: always 0 (the persistent decoder pass was deleted) */
+    int32_t pd_fallbacks;     /* ABI 12: always 0 */
 } spt_call_stats;
 
 spt_status spt_get_call_stats(const spt_ctx* ctx, spt_call_stats* s);

@@ -117,9 +117,9 @@ pub struct spt_call_stats {
     pub device_ms: f64,
     pub encoder_ms: f64,
     pub decode_ms: f64,
-    /// ABI 12: decoder passes run as one persistent launch
+    /// ABI 12: always 0 (the persistent decoder pass was deleted in round 6)
     pub pd_passes: i32,
-    /// ABI 12: calls / beam steps re-run on the launch chain after the persistent pass gave up
+    /// ABI 12: always 0
     pub pd_fallbacks: i32,
 }
 

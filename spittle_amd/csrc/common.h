@@ -73,8 +73,8 @@ template <> __device__ inline f16 from_f<f16>(float v) { return (f16)v; }  // RN
 // GELU, tanh form (ggml / whisper.cpp): 0.5 x (1 + tanh(u)), u = sqrt(2/pi) (x + 0.044715 x^3),
 // evaluated as x * sigmoid(2u) = x / (1 + 2^(-2u log2 e)): one v_exp_f32 + one v_rcp_f32
 // instead of tanhf (the same function; differs from libm tanhf by a few f32 ulp)
-// (contraction off: every kernel that inlines it -- the decoder's fc1 GEMV and its persistent pass,
-// the encoder's GEMM epilogues -- computes the same bits, whatever the surrounding code)
+// (contraction off: every kernel that inlines it -- the decoder's fc1 GEMV, the encoder's GEMM
+// epilogues -- computes the same bits, whatever the surrounding code)
 __device__ inline float gelu_tanh(float x) {
 #pragma clang fp contract(off)
     const float c2 = -2.0f * 0.7978845608028654f * 1.4426950408889634f;
@@ -82,8 +82,8 @@ __device__ inline float gelu_tanh(float x) {
     return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
 
-// the decoder rows' LayerNorm arithmetic (gemv_kernel's A_LN prologue, the persistent pass), spelled
-// out with contraction off so both compute the same bits: the squared deviations of four elements,
+// the decoder rows' LayerNorm arithmetic (gemv_kernel's A_LN prologue), spelled out with
+// contraction off so every instance computes the same bits: the squared deviations of four elements,
 // and one normalised element
 __device__ inline float ln_sq4(float4 v, float mean) {
 #pragma clang fp contract(off)

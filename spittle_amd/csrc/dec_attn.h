@@ -1,6 +1,6 @@
-// dec_attn.h -- the decode-step attention arithmetic shared by the per-stage kernels (k_dec.hip)
-// and the persistent decoder pass (k_pdec.hip): one definition, so every instance computes the
-// same bits (AttnWave's online softmax and attn_merge are spelled out: contraction off, explicit
+// dec_attn.h -- the decode-step attention arithmetic of the per-stage kernels (k_dec.hip; round 5's
+// persistent decoder pass shared it until round 6 deleted that pass): one definition, so every
+// instance computes the same bits (AttnWave's online softmax and attn_merge are spelled out: contraction off, explicit
 // fmaf).
 #pragma once
 #include "common.h"

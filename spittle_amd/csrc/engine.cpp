@@ -98,14 +98,6 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     if ((3 * cp_ * esz_) % 128) cp_ = ((dm_.n_mels + 127) / 128) * 128;
     if (const char* g = getenv("SPT_DECODE_GROUPS")) n_groups_ = std::max(1, std::min(4, atoi(g)));
     if (const char* v = getenv("SPT_XATTN_SPLIT")) xsplit_ = std::max(1, std::min(4, atoi(v)));
-    if (const char* v = getenv("SPT_PERSISTENT")) pd_env_ = atoi(v) != 0;
-    if (const char* v = getenv("SPT_PD_STAMP")) pd_stamp_path_ = v;
-    if (const char* v = getenv("SPT_PD_FORCE_GIVEUP")) pd_force_giveup_ = atoi(v);  // test hook
-    // the encoder's LayerNorm fold (SPT_LN_FOLD=0: separate LayerNorm launches)
-    lnf_on_ = dm_.n_enc > 0 && dm_.d % 64 == 0 && dm_.d <= 1280 && !(getenv("SPT_LN_FOLD") && atoi(getenv("SPT_LN_FOLD")) == 0);
-    // the persistent pass's resources (kernel attributes, layer table, granule arenas) only when it is
-    // asked for (every bf16 engine paid for the opt-in pass)
-    pd_able_ = pd_env_ && pdec_unsupported(dt_, dm_.d, dm_.n_head, 1, dm_.n_text_ctx, dm_.n_audio_ctx).empty();
     // cross-attention key split: fixed per engine (never per batch).  The fc2 K split (2; r1
     // exp14 measured 2 slightly faster per layer than 4: the next QKV LayerNorm prologue sums
     // fewer slabs) is fixed per engine too; the pending-slab count a LayerNorm prologue sums is
@@ -129,25 +121,7 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
     try {
         gemv_prepare(dt_);
         gemm_prepare();  // > 64 KiB LDS attributes on this device, before any capture
-        if (pd_able_) pdec_prepare();
-        if (pd_able_ && !pd_stamp_path_.empty()) {
-            int ncu = 0;
-            HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev_));
-            const size_t n = (size_t)ncu * kPdStampMax * kPdStampRec * 8;
-            HIP_CHECK(hipMalloc(&pd_stamps_, n));
-            HIP_CHECK(hipMemset(pd_stamps_, 0, n));
-        }
         alloc_weights();
-        if (pd_able_) {  // the persistent pass reads each layer's weight pointers from device memory
-            std::vector<PdLayer> t(dm_.n_dec);
-            for (int l = 0; l < dm_.n_dec; ++l) {
-                const DecL& e = dec_[l];
-                t[l] = PdLayer{e.ln1_w, e.ln1_b, e.qkv_w, e.qkv_b, e.so_w, e.so_b, e.ln2_w, e.ln2_b, e.cq_w, e.cq_b,
-                               e.co_w, e.co_b, e.ln3_w, e.ln3_b, e.fc1_w, e.fc1_b, e.fc2_w, e.fc2_b};
-            }
-            HIP_CHECK(hipMalloc(&pd_layers_, t.size() * sizeof(PdLayer)));
-            HIP_CHECK(hipMemcpy(pd_layers_, t.data(), t.size() * sizeof(PdLayer), hipMemcpyHostToDevice));
-        }
         if (external_weights) {
             // filled later by import_weights; clear it so a premature use reads zeros, not garbage
             HIP_CHECK(hipMemsetAsync(warena_, 0, wbytes_, st_));
@@ -157,8 +131,6 @@ Engine::Engine(const ModelDims& dm, int dtype, int device, int max_batch, uint64
             generate_weights();
         }
         weights_ready_ = !external_weights;
-        lnf_ready_ = false;
-        if (lnf_on_) HIP_CHECK(hipMalloc(&lnf_tab_, (size_t)dm_.n_enc * 14 * dm_.d * 4));
         upload_tables(src ? &src->mel_filters() : nullptr);
         alloc_workspace();
         HIP_CHECK(hipStreamSynchronize(st_));
@@ -193,12 +165,6 @@ void Engine::release() {
     if (warena_) (void)hipFree(warena_);
     if (aarena_) (void)hipFree(aarena_);
     if (kvtmp_) (void)hipFree(kvtmp_);
-    if (pd_layers_) (void)hipFree(pd_layers_);
-    pd_layers_ = nullptr;
-    if (pd_stamps_) (void)hipFree(pd_stamps_);
-    pd_stamps_ = nullptr;
-    if (lnf_tab_) (void)hipFree(lnf_tab_);
-    lnf_tab_ = nullptr;
     for (void* p : {(void*)upcm_, (void*)umel_, (void*)uinfo_})
         if (p) (void)hipFree(p);
     upcm_ = umel_ = nullptr;
@@ -245,14 +211,12 @@ void Engine::import_weights(const void* dev_src, int64_t bytes) {
     HIP_CHECK(hipMemcpyAsync(warena_, dev_src, (size_t)wbytes_, hipMemcpyDeviceToDevice, st_));
     HIP_CHECK(hipStreamSynchronize(st_));
     weights_ready_ = true;
-    lnf_ready_ = false;
 }
 
 void Engine::commit_weights() {
     select();
     HIP_CHECK(hipDeviceSynchronize());  // the writer may have used any stream of this device
     weights_ready_ = true;
-    lnf_ready_ = false;
 }
 
 void Engine::alloc_weights() {
@@ -608,7 +572,6 @@ void Engine::alloc_workspace() {
         ao_ = A(B * T * d);
         ff_ = A(B * T * 4 * d);
         enc_out_ = A(B * T * d);
-        lnf_part_ = (float2*)c.take(B * T * (d / kLnfGroup) * 8);
         ckv_ = A(L * kv_layer_elems((int)B, dm_.n_head, (int)T));
         suppress_ = (uint32_t*)c.take((V / 32 + 1) * 4);
         suppress_lang_ = (uint32_t*)c.take((V / 32 + 1) * 4);
@@ -629,7 +592,6 @@ void Engine::alloc_workspace() {
             g.done = (int*)c.take(B * 4);
             g.forced = (int*)c.take(B * ctx * 4);
             g.ds = (DecState*)c.take(sizeof(DecState));
-            g.ds_save = (DecState*)c.take(sizeof(DecState));
             g.dx2 = (float*)c.take(R * d * 4);
             g.pend = (float*)c.take((int64_t)kMaxPend * R * d * 4);
             g.xpart = (float*)c.take((int64_t)R * dm_.n_head * 8 * 66 * 4);
@@ -646,11 +608,6 @@ void Engine::alloc_workspace() {
             g.cand_lp = (float*)c.take(B * 8 * 4);
             g.beam_tid = (int*)c.take(B * 4);
             g.kvrow = (int*)c.take(B * 4);
-            if (pd_able_) {
-                g.pctl = (unsigned*)c.take(64);
-                g.gran_bytes = pdec_granules((int)std::min<int64_t>(8, B), (int)d, dm_.n_head) * 8;
-                g.gran = (unsigned long long*)c.take(g.gran_bytes);
-            }
         }
         zero_ = (float*)c.take(R * d * 4);  // never written: the "no pending slab" operand
         if (!pass) {
@@ -786,7 +743,6 @@ void Engine::upload_windows(const int* utt, const int* seek, int E) {
 void Engine::encode_windows(const int* utt, const int* seek, int E) {
     select();
     require_weights();
-    ensure_lnf_tables();
     upload_windows(utt, seek, E);
     HIP_CHECK(hipEventRecord(ev_[2], st_));
     mel_norm(dt_, umel_, umax_, mu_, win_utt_, win_seek_, E, dm_.n_mels, cp_, mel_in_, nullptr, st_);
@@ -801,11 +757,8 @@ void Engine::encode_windows(const int* utt, const int* seek, int E) {
 }
 
 // One encoder layer over the Bg windows starting at row r0 (whisper_build_graph_encoder's block:
-// LN1 -> q/k/v -> attention -> out-proj + residual -> LN2 -> fc1 + GELU -> fc2 + residual).  With the
-// LayerNorm fold (lnf_on_) no LayerNorm launches: the residual producers (conv2 /
-// the previous fc2, out-proj) also write x o gamma and per-row 32-column partials, and q/k/v / fc1
-// apply the normalisation in their epilogues through the fold tables.  The last layer's fc2 leaves x
-// for ln_post.  probe: 4 / 5 -> events e0 / e1 around fc1 / the attention (spt_probe_kernel).
+// LN1 -> q/k/v -> attention -> out-proj + residual -> LN2 -> fc1 + GELU -> fc2 + residual).
+// probe: 4 / 5 -> events e0 / e1 around fc1 / the attention (spt_probe_kernel).
 void Engine::enc_layer(int l, int Bg, int64_t r0, hipStream_t s, int probe, hipEvent_t e0, hipEvent_t e1) {
     const int d = dm_.d, T = dm_.n_audio_ctx, H = dm_.n_head, M = Bg * T;
     const EncL& e = enc_[l];
@@ -815,15 +768,10 @@ void Engine::enc_layer(int l, int Bg, int64_t r0, hipStream_t s, int probe, hipE
     void* qkv = rows(qkv_, 3 * d, esz_);
     void* ao = rows(ao_, d, esz_);
     void* ff = rows(ff_, 4 * d, esz_);
-    float2* part = lnf_on_ ? lnf_part_ + r0 * (d / kLnfGroup) : nullptr;
-    const bool fold = lnf_on_;
-    const bool fold_next = fold && l + 1 < dm_.n_enc;
-    const float* tab = lnf_tab_ + (size_t)l * 14 * d;  // qkv gw | qkv bw | fc1 gw | fc1 bw
     GemmArgs g{};
-    if (!fold) layernorm(dt_, x, M, d, e.ln1_w, e.ln1_b, xn, s);
+    layernorm(dt_, x, M, d, e.ln1_w, e.ln1_b, xn, s);
     g.A = xn; g.lda = d; g.W = e.qkv_w; g.ldw = d; g.M = M; g.N = 3 * d; g.K = d; g.bias = e.qkv_b;
     g.C = qkv; g.ldc = 3 * d;
-    if (fold) { g.lnf_in = part; g.lnf_gw = tab; g.lnf_bw = tab + 3 * d; }
     gemm_nt(dt_, EPI_BIAS, g, 1, s);
     if (probe == 5) HIP_CHECK(hipEventRecord(e0, s));
     enc_attention(dt_, qkv, Bg, T, H, ao, s);
@@ -831,36 +779,18 @@ void Engine::enc_layer(int l, int Bg, int64_t r0, hipStream_t s, int probe, hipE
     g = GemmArgs{};
     g.A = ao; g.lda = d; g.W = e.o_w; g.ldw = d; g.M = M; g.N = d; g.K = d; g.bias = e.o_b;
     g.C = x; g.ldc = d;
-    if (fold) { g.lnf_g = e.ln2_w; g.lnf_xg = xn; g.lnf_part = part; }
     gemm_nt(dt_, EPI_BIAS_RESID, g, 1, s);
-    if (!fold) layernorm(dt_, x, M, d, e.ln2_w, e.ln2_b, xn, s);
+    layernorm(dt_, x, M, d, e.ln2_w, e.ln2_b, xn, s);
     g = GemmArgs{};
     g.A = xn; g.lda = d; g.W = e.fc1_w; g.ldw = d; g.M = M; g.N = 4 * d; g.K = d; g.bias = e.fc1_b;
     g.C = ff; g.ldc = 4 * d;
-    if (fold) { g.lnf_in = part; g.lnf_gw = tab + 6 * d; g.lnf_bw = tab + 10 * d; }
     if (probe == 4) HIP_CHECK(hipEventRecord(e0, s));
     gemm_nt(dt_, EPI_BIAS_GELU, g, 1, s);
     if (probe == 4) HIP_CHECK(hipEventRecord(e1, s));
     g = GemmArgs{};
     g.A = ff; g.lda = 4 * d; g.W = e.fc2_w; g.ldw = 4 * d; g.M = M; g.N = d; g.K = 4 * d; g.bias = e.fc2_b;
     g.C = x; g.ldc = d;
-    if (fold_next) { g.lnf_g = enc_[l + 1].ln1_w; g.lnf_xg = xn; g.lnf_part = part; }
     gemm_nt(dt_, EPI_BIAS_RESID, g, 1, s);
-}
-
-// The LayerNorm fold's tables: per encoder layer, q/k/v's and fc1's
-// gw = W gamma and bw = b + W beta of the LayerNorm in front of them; rebuilt whenever the weights
-// change (load, import, commit), before any encoder launch that reads them.
-void Engine::ensure_lnf_tables() {
-    if (!lnf_on_ || lnf_ready_) return;
-    const int d = dm_.d;
-    for (int l = 0; l < dm_.n_enc; ++l) {
-        const EncL& e = enc_[l];
-        float* tab = lnf_tab_ + (size_t)l * 14 * d;
-        ln_fold_tables(dt_, e.qkv_w, 3 * d, d, e.ln1_w, e.ln1_b, e.qkv_b, tab, tab + 3 * d, st_);
-        ln_fold_tables(dt_, e.fc1_w, 4 * d, d, e.ln2_w, e.ln2_b, e.fc1_b, tab + 6 * d, tab + 10 * d, st_);
-    }
-    lnf_ready_ = true;
 }
 
 void Engine::run_encoder(int B) {
@@ -881,9 +811,6 @@ void Engine::run_encoder(int B) {
     g.bias = conv2_b_;
     g.C = x_; g.ldc = d; g.sC = (int64_t)T * d;
     g.pos = enc_pos_;
-    if (lnf_on_) {  // LayerNorm fold: also layer 0's LN1 operand x o gamma and the row partials
-        g.lnf_g = enc_[0].ln1_w; g.lnf_xg = xn_; g.lnf_part = lnf_part_;
-    }
     gemm_nt(dt_, EPI_BIAS_GELU_POS, g, B, st_);
     // The layers run per window group, each group's rows (whole windows: every kernel below is
     // row-local or per window) on its own stream, so one group's kernels fill the CUs the other's
@@ -1003,25 +930,6 @@ float* Engine::enqueue_layers(DecGroup& g, int E, int Tq) {
     const int xs = vw ? (vw_merge ? 1 : 8) : mapped ? 1 : xsplit_;
     const int ks = dt_ == DT_BF16 ? 128 : 64;
     hipStream_t st = g.st;
-    if (Tq == 1 && pd_active_ && R <= 8) {
-        // every layer in one persistent launch (k_pdec.hip), bitwise this chain's result; it leaves
-        // the head's operands where the chain does: x (here dx2) + fc2's two pending slabs
-        PdArgs p{};
-        p.layers = pd_layers_; p.L = dm_.n_dec;
-        p.d = d; p.H = H; p.R = R; p.ctx = ctx; p.T_enc = T; p.B_layout = E;
-        p.ckv = (const char*)ckv_ + (mapped ? 0 : (int64_t)g.b0 * H * 4096) * esz_;
-        p.cross_layer = cross_layer;
-        p.kvrow = mapped ? g.kvrow : nullptr;
-        p.skv = g.skv; p.self_layer = self_layer;
-        p.x = g.dx; p.xo = g.dx2; p.pend = g.pend; p.ds = g.ds; p.gran = g.gran; p.ctl = g.pctl;
-        p.stamps = pd_stamps_;  // SPT_PD_STAMP (allocated with the engine), else null
-        p.force_giveup = pd_force_giveup_;
-        pdec_launch(p, st);
-        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-        HIP_CHECK(hipStreamIsCapturing(st, &cap));
-        if (cap == hipStreamCaptureStatusNone) cs_.pd_passes++;  // replays of a captured pass count where launched
-        return g.dx2;
-    }
     float* xc = g.dx;   // current residual rows (dec_embed / dec_finalize wrote this pass's input here)
     float* xo = g.dx2;  // the other buffer
     int np = 0;         // pending slabs in g.pend
@@ -1213,9 +1121,6 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
     }
     const int unit = std::max(1, S), nU = B / unit;
     if (Bg > max_rows_) throw std::runtime_error("batch exceeds the decoder's rows per pass");
-    // one-token passes of up to 8 rows in one group run the persistent pass (it needs every CU: two
-    // groups' passes on two streams would each hold part of the chip)
-    pd_active_ = pd_able_ && pd_env_ && !pd_fallback_ && G == 1 && Bg <= 8;
     const int cmax = std::max(1, std::min(4, max_rows_ / Bg));
     const int Tq_head = Bg * Tq > max_rows_ ? 1 : Tq;
     if (P > ctx / 2 + 1) throw std::runtime_error("prompt prefix longer than n_text_ctx / 2 + 1");
@@ -1296,10 +1201,6 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         fill_f32(g.out_t1, (int64_t)g.B * out_cap, -INFINITY, g.st);
         fill_f32(g.out_t2, (int64_t)g.B * out_cap, -INFINITY, g.st);
         dec_reset(g.ds, g.arrive, g.st);
-        if (pd_active_) {  // the persistent pass's control words and granules start each call at zero
-            HIP_CHECK(hipMemsetAsync(g.pctl, 0, 16, g.st));
-            HIP_CHECK(hipMemsetAsync(g.gran, 0, (size_t)pdec_granules(g.B, dm_.d, dm_.n_head) * 8, g.st));
-        }
         if (rq.full)  // WHISPER_DECODER_INIT: seek_delta starts at a whole window (3000 frames)
             HIP_CHECK(hipMemcpyAsync(g.ts_state, ts_init_.data() + (size_t)g.b0 * 4, g.B * 16, hipMemcpyHostToDevice,
                                      g.st));
@@ -1331,10 +1232,8 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         for (DecGroup* g : act) {
             HIP_CHECK(hipMemcpyAsync(first.data() + (size_t)g->b0 * out_cap, g->out_tok, (size_t)g->B * out_cap * 4,
                                      hipMemcpyDeviceToHost, g->st));
-            if (pd_active_) HIP_CHECK(hipMemcpyAsync(&pd_err_host_, g->pctl + 2, 4, hipMemcpyDeviceToHost, g->st));
             HIP_CHECK(hipStreamSynchronize(g->st));
         }
-        if (pd_active_ && pd_err_host_) throw PdGaveUp();  // decode() re-runs the call on the chain
         for (int b = 0; b < B; ++b) {
             const int v = rq.lang_tok[b];
             lang[b] = v >= 0 ? v : first[(size_t)(-v - 1) * out_cap];
@@ -1380,7 +1279,6 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
     if (rq.beam_k > 0) {  // beam search continues step by step from the host (beam_next)
         tm_.n_decode_passes = 1;
         for (DecGroup* g : act) {
-            if (pd_active_) HIP_CHECK(hipMemcpyAsync(&pd_err_host_, g->pctl + 2, 4, hipMemcpyDeviceToHost, g->st));
             HIP_CHECK(hipEventRecord(g->ev, g->st));
             HIP_CHECK(hipStreamWaitEvent(st_, g->ev, 0));
         }
@@ -1408,7 +1306,6 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
             // into the cross-attention grid (the map itself is read from g->kvrow)
             GraphKey key{g->B, E, g->b0, out_cap, rq.n_forced, rq.flags, rq.full};
             key.share = S;
-            key.pd = pd_active_;
             auto it = g->graphs.find(key);
             if (it == g->graphs.end()) {
                 hipGraph_t graph;
@@ -1427,7 +1324,6 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         for (int s = 1; s < rq.n_steps; ++s) {
             for (size_t i = 0; i < act.size(); ++i) HIP_CHECK(hipGraphLaunch(ex[i], act[i]->st));
             ++passes;
-            if (pd_active_) cs_.pd_passes += (int)act.size();
             if (early_exit && (s % 16) == 0) {
                 bool all = true;
                 for (DecGroup* g : act) {
@@ -1448,20 +1344,8 @@ void Engine::run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1
         if (ts_state_out && rq.full)
             HIP_CHECK(hipMemcpyAsync(ts_state_out + (size_t)g->b0 * 4, g->ts_state, (size_t)g->B * 16,
                                      hipMemcpyDeviceToHost, g->st));
-        if (pd_active_) HIP_CHECK(hipMemcpyAsync(&pd_err_host_, g->pctl + 2, 4, hipMemcpyDeviceToHost, g->st));
         HIP_CHECK(hipEventRecord(g->ev, g->st));
         HIP_CHECK(hipStreamWaitEvent(st_, g->ev, 0));
-    }
-}
-
-void Engine::dump_pd_stamps() {
-    int ncu = 0;
-    HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev_));
-    std::vector<unsigned long long> h((size_t)ncu * kPdStampMax * kPdStampRec);
-    HIP_CHECK(hipMemcpy(h.data(), pd_stamps_, h.size() * 8, hipMemcpyDeviceToHost));
-    if (FILE* f = fopen(pd_stamp_path_.c_str(), "wb")) {
-        fwrite(h.data(), 8, h.size(), f);
-        fclose(f);
     }
 }
 
@@ -1470,40 +1354,10 @@ void Engine::decode(int B, const DecodeRequest& rq, int* tokens, float* top1, fl
     select();
     require_weights();
     HIP_CHECK(hipEventRecord(ev_[6], st_));  // the decode groups wait for the encoded windows here
-    pd_err_host_ = 0;
-    bool gave_up = false;
-    const int pd0 = cs_.pd_passes;
-    try {
-        run_decode(B, rq, tokens, top1, top2, lang_out, ts_state_out);
-    } catch (const PdGaveUp&) {
-        gave_up = true;
-    }
+    run_decode(B, rq, tokens, top1, top2, lang_out, ts_state_out);
     HIP_CHECK(hipEventRecord(ev_[7], st_));
     HIP_CHECK(hipStreamSynchronize(st_));
     HIP_CHECK(hipGetLastError());
-    if (pd_stamps_ && pd_active_) dump_pd_stamps();
-    if (gave_up || (pd_active_ && pd_err_host_ != 0)) {
-        // the persistent pass could not hold every CU (another context's or process's kernels ran
-        // beside it) and gave up: the whole call again on the launch chain (re-runs are idempotent:
-        // outputs, state and caches are reset or rewritten)
-        fprintf(stderr, "[spt] persistent decoder pass gave up (code %u); re-running the call on the launch chain\n",
-                pd_err_host_);
-        for (DecGroup& g : groups_) HIP_CHECK(hipStreamSynchronize(g.st));
-        pd_fallback_ = true;
-        cs_.pd_fallbacks++;
-        cs_.pd_passes = pd0;  // the failed attempt's passes re-run on the chain
-        try {
-            HIP_CHECK(hipEventRecord(ev_[6], st_));
-            run_decode(B, rq, tokens, top1, top2, lang_out, ts_state_out);
-            HIP_CHECK(hipEventRecord(ev_[7], st_));
-            HIP_CHECK(hipStreamSynchronize(st_));
-        } catch (...) {
-            pd_fallback_ = false;
-            throw;
-        }
-        pd_fallback_ = false;
-        pd_active_ = false;
-    }
     tm_.batch = B;
     cs_.engine_calls++;
     cs_.decoder_passes += tm_.n_decode_passes;
@@ -1653,48 +1507,28 @@ void Engine::beam_next(const int* src, const int* tokens, const int* rowstate, i
         enqueue_head(g, 1, beam_rq_, beam_rq_.n_steps, x, suppress_, (beam_rq_.flags & 1u) != 0);
     };
     static const bool no_graph = getenv("SPT_NO_GRAPH") != nullptr;
-    // the step's head advances the decoder state (DecState) even when the persistent pass in front of
-    // it gave up: keep the starting state so the re-run starts where this step did
-    if (pd_active_) HIP_CHECK(hipMemcpyAsync(g.ds_save, g.ds, sizeof(DecState), hipMemcpyDeviceToDevice, g.st));
-    for (;;) {
-        const int pd0 = cs_.pd_passes;  // an eager persistent launch counts itself; set below either way
-        HIP_CHECK(hipEventRecord(ev_[8], g.st));
-        if (no_graph) {
+    HIP_CHECK(hipEventRecord(ev_[8], g.st));
+    if (no_graph) {
+        beam_pass();
+    } else {
+        // n_forced = -beam_k marks a beam-step graph (a real n_forced is >= 0)
+        GraphKey key{B, enc_E_, side, beam_rq_.n_steps, -beam_rq_.beam_k, beam_rq_.flags, beam_rq_.full};  // b0: cache side
+        key.share = g.share;
+        auto it = g.graphs.find(key);
+        if (it == g.graphs.end()) {
+            hipGraph_t graph;
+            HIP_CHECK(hipStreamBeginCapture(g.st, hipStreamCaptureModeThreadLocal));
             beam_pass();
-        } else {
-            // n_forced = -beam_k marks a beam-step graph (a real n_forced is >= 0)
-            GraphKey key{B, enc_E_, side, beam_rq_.n_steps, -beam_rq_.beam_k, beam_rq_.flags, beam_rq_.full};  // b0: cache side
-            key.share = g.share;
-            key.pd = pd_active_;
-            auto it = g.graphs.find(key);
-            if (it == g.graphs.end()) {
-                hipGraph_t graph;
-                HIP_CHECK(hipStreamBeginCapture(g.st, hipStreamCaptureModeThreadLocal));
-                beam_pass();
-                HIP_CHECK(hipStreamEndCapture(g.st, &graph));
-                hipGraphExec_t exec;
-                HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
-                HIP_CHECK(hipGraphDestroy(graph));
-                it = g.graphs.emplace(key, exec).first;
-            }
-            HIP_CHECK(hipGraphLaunch(it->second, g.st));
+            HIP_CHECK(hipStreamEndCapture(g.st, &graph));
+            hipGraphExec_t exec;
+            HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+            HIP_CHECK(hipGraphDestroy(graph));
+            it = g.graphs.emplace(key, exec).first;
         }
-        HIP_CHECK(hipEventRecord(ev_[9], g.st));
-        pd_err_host_ = 0;
-        if (pd_active_) HIP_CHECK(hipMemcpyAsync(&pd_err_host_, g.pctl + 2, 4, hipMemcpyDeviceToHost, g.st));
-        read_cands(B, out);  // synchronises g.st
-        // a persistent step counts once it is known not to have given up (a step re-run
-        // on the chain was counted as persistent too)
-        cs_.pd_passes = pd0 + (pd_active_ && pd_err_host_ == 0 ? 1 : 0);
-        if (!pd_active_ || pd_err_host_ == 0) break;
-        // the persistent pass gave up (decode()): this step again, and the rest of the search, on
-        // the launch chain (the step is idempotent: the gather, the appends and the candidates are
-        // rewritten from the same inputs)
-        fprintf(stderr, "[spt] persistent decoder pass gave up in a beam step (code %u); launch chain\n", pd_err_host_);
-        pd_active_ = false;
-        cs_.pd_fallbacks++;
-        HIP_CHECK(hipMemcpyAsync(g.ds, g.ds_save, sizeof(DecState), hipMemcpyDeviceToDevice, g.st));
+        HIP_CHECK(hipGraphLaunch(it->second, g.st));
     }
+    HIP_CHECK(hipEventRecord(ev_[9], g.st));
+    read_cands(B, out);  // synchronises g.st
     beam_side_ ^= 1;
     float ms = 0.0f;
     HIP_CHECK(hipEventElapsedTime(&ms, ev_[8], ev_[9]));
@@ -1724,7 +1558,6 @@ void Engine::debug_mel(const float* pcm_host, int n, int seek, float* out_host) 
 void Engine::debug_encode(const float* mel_host, float* out_host) {
     select();
     require_weights();
-    ensure_lnf_tables();
     const int nm = dm_.n_mels, d = dm_.d, T = dm_.n_audio_ctx;
     std::vector<char> img((size_t)MEL_ROWS * cp_ * esz_, 0);
     for (int t = 0; t < 3000; ++t)
@@ -1815,12 +1648,10 @@ double Engine::probe(int kind, int iters, double* work, int* is_flops) {
             break;
         }
         case 4: {
-            ensure_lnf_tables();
-            launch = [&] {
+                    launch = [&] {
                 GemmArgs a{};
                 a.A = xn_; a.lda = d; a.W = enc_[0].fc1_w; a.ldw = d; a.M = B * T; a.N = 4 * d; a.K = d;
                 a.bias = enc_[0].fc1_b; a.C = ff_; a.ldc = 4 * d;
-                if (lnf_on_) { a.lnf_in = lnf_part_; a.lnf_gw = lnf_tab_ + 6 * d; a.lnf_bw = lnf_tab_ + 10 * d; }
                 gemm_nt(dt_, EPI_BIAS_GELU, a, 1, st_);
             };
             *work = 2.0 * B * T * 4.0 * d * d;
@@ -1840,7 +1671,7 @@ double Engine::probe(int kind, int iters, double* work, int* is_flops) {
     }
     launch();  // warm
     static const bool insitu = getenv("SPT_PROBE_INSITU") && atoi(getenv("SPT_PROBE_INSITU")) != 0;
-    if (kind <= 3 && !pd_active_ && insitu) {
+    if (kind <= 3 && insitu) {
         // decoder kernels in situ (SPT_PROBE_INSITU=1): eager one-token passes over the last call's
         // rows, with events around the probed kernel of every layer (cross-attention,
         // self-attention, fc1) or around the logits launch after the layers.  Each pair also holds
@@ -1920,8 +1751,7 @@ double Engine::probe(int kind, int iters, double* work, int* is_flops) {
         // 10 % below its rocprofv3 average, r5's producer-then-kernel pairs with a host wait
         // between them 8 % below.  The residual rows x grow by one layer per run: the probe runs
         // after the timed calls, and every call recomputes them.
-        ensure_lnf_tables();
-        if ((int)probe_ev_.size() < 2 * iters) {
+            if ((int)probe_ev_.size() < 2 * iters) {
             for (int i = (int)probe_ev_.size(); i < 2 * iters; ++i) {
                 hipEvent_t ev;
                 HIP_CHECK(hipEventCreate(&ev));

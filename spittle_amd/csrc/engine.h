@@ -65,12 +65,10 @@ struct Timings {
 // and beam step), summed; reset by the C ABI at the start of each spt_transcribe* call
 struct CallStats {
     int engine_calls = 0, decoder_passes = 0, beam_steps = 0, encoder_windows = 0;
-    int pd_passes = 0;     // decoder passes run as the persistent launch
-    int pd_fallbacks = 0;  // calls re-run on the launch chain after the persistent pass gave up
+    int pd_passes = 0;     // ABI 12 counters of the persistent decoder pass (deleted in round 6): always 0
+    int pd_fallbacks = 0;
     double device_ms = 0, encoder_ms = 0, decode_ms = 0;
 };
-
-struct PdGaveUp {};  // the persistent decoder pass gave up inside run_decode (decode() re-runs the call)
 
 class Engine {
 public:
@@ -153,9 +151,7 @@ private:
         uint32_t flags;
         bool full;
         int share = 0;  // rows per window (0: identity rows, no window map)
-        bool pd = false;  // the layers run as the persistent pass (k_pdec.hip)
         bool operator<(const GraphKey& o) const {
-            if (pd != o.pd) return pd < o.pd;
             if (full != o.full) return full < o.full;
             if (B != o.B) return B < o.B;
             if (share != o.share) return share < o.share;
@@ -181,7 +177,6 @@ private:
         int *tok_in = nullptr, *out_tok = nullptr, *done = nullptr, *forced = nullptr;
         float *out_t1 = nullptr, *out_t2 = nullptr;
         DecState* ds = nullptr;
-        DecState* ds_save = nullptr;  // beam_next: the step's starting state (a persistent step that gave up re-runs from it)
         float* dx2 = nullptr;         // second residual buffer (ping-pong with dx)
         float* pend = nullptr;        // pending partial slabs [kMaxPend][R][d]
         float* xpart = nullptr;       // cross-attention chunk partials [R][H][<=4][66]
@@ -193,9 +188,6 @@ private:
         int *cand_id = nullptr, *beam_tid = nullptr;
         float* cand_lp = nullptr;
         int* kvrow = nullptr;         // [B] encoded window of each row (window map)
-        unsigned* pctl = nullptr;     // persistent pass: [kPdCtlWords] census / exits / error / launch
-        unsigned long long* gran = nullptr;  // persistent pass: granule arena (pdec_granules words)
-        int64_t gran_bytes = 0;
         int share = 0;                // rows per window of this call (0: identity, no map)
         std::map<GraphKey, hipGraphExec_t> graphs;
         std::vector<int> host_tok;    // host sources of the call's token uploads
@@ -215,11 +207,6 @@ private:
     void run_encoder(int B);
     void enc_layer(int l, int Bg, int64_t r0, hipStream_t s, int probe = 0, hipEvent_t e0 = nullptr,
                    hipEvent_t e1 = nullptr);
-    void ensure_lnf_tables();
-    // the encoder's LayerNorm fold: on unless SPT_LN_FOLD=0 (or the width does not fit)
-    bool lnf_on_ = false, lnf_ready_ = false;
-    float* lnf_tab_ = nullptr;      // [n_enc][qkv gw 3d | qkv bw 3d | fc1 gw 4d | fc1 bw 4d]
-    float2* lnf_part_ = nullptr;    // workspace: [B * T][d / 32] row partials
     void enqueue_encoder(int B);  // run_encoder, replayed from a per-B graph after the first call
     void run_cross_kv(int B);
     void run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1, float* top2, int* lang_out,
@@ -229,22 +216,6 @@ private:
     float* enqueue_layers(DecGroup& g, int E, int Tq);
     void enqueue_head(DecGroup& g, int Tq, const DecodeRequest& rq, int out_cap, float* xc, const uint32_t* sup,
                       bool blank);
-
-    // the persistent decoder pass (k_pdec.hip): one launch for every layer of a one-token pass of at
-    // most 8 rows in one decode group, bitwise the launch chain but measured 1.35-1.82x slower
-    // (DESIGN.md 4.1f): opt-in, SPT_PERSISTENT=1.
-    bool pd_able_ = false;       // this model / dtype / batch geometry can run it
-    bool pd_env_ = false;        // SPT_PERSISTENT=1
-    bool pd_active_ = false;     // this call's one-token passes run it (set per run_decode)
-    bool pd_fallback_ = false;   // re-running a call whose persistent pass gave up (the chain instead)
-    PdLayer* pd_layers_ = nullptr;  // device copy of the decoder layers' pointers
-    unsigned pd_err_host_ = 0;      // the last call's error word (read back with the tokens)
-    // SPT_PD_STAMP=<file>: per-unit stage stamps of every persistent pass (k_pdec.hip), the last
-    // pass of each decode call written to <file> (u64 [CUs][kPdStampMax][kPdStampRec])
-    unsigned long long* pd_stamps_ = nullptr;
-    int pd_force_giveup_ = -1;  // SPT_PD_FORCE_GIVEUP=<launch index>: test hook for the give-up path
-    std::string pd_stamp_path_;
-    void dump_pd_stamps();
 
     ModelDims dm_;
     int dt_, dev_, max_batch_;

@@ -109,129 +109,6 @@ __device__ __forceinline__ void epi_store(const GemmArgs& g, int bz, int row, co
     }
 }
 
-// the f32 value epi_store writes for the f32-output epilogues that feed a LayerNorm (producers of
-// the LayerNorm fold): the same operations in the same order
-template <int EPI>
-__device__ __forceinline__ float epi_value(const GemmArgs& g, const EpiCol& e, float acc, float y) {
-#pragma clang fp contract(off)
-    const float v = acc + e.bv;
-    if constexpr (EPI == EPI_BIAS_GELU_POS) return gelu_tanh(v) + y;
-    else return y + g.alpha * v;
-}
-
-// ---- LayerNorm fold (GemmArgs lnf_*) ------------------------------------------
-// Producer: every 32-column group of a row gets {sum, sum of squared deviations from the group mean}
-// in one canonical order -- each quad of 4 consecutive columns as (c0 + c1) + (c2 + c3), then
-// pairwise over the quads (q ^ 1, q ^ 2, q ^ 4) -- whichever lanes hold the columns (float addition
-// commutes, so both partners of a butterfly step hold the same bits), so every tile shape writes the
-// same partials.  Consumer: the row's groups merged in group order.
-template <int EPI> constexpr bool lnf_producer() { return EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU_POS; }
-template <int EPI> constexpr bool lnf_consumer() { return EPI == EPI_BIAS || EPI == EPI_BIAS_GELU; }
-// the kernels' epilogue template argument: the GemmArgs epilogue, | EPI_LNF for its LayerNorm-fold
-// form (a separate instantiation: the plain kernels stay exactly as they were)
-constexpr int EPI_LNF = 16;
-constexpr int epi_base(int e) { return e & (EPI_LNF - 1); }
-constexpr int kLnfMaxG = 40;  // groups per row: d <= 1280
-
-// the value of lane ^ X (X = 1, 2, 4, 8; within a 16-lane DPP row) by DPP moves: VALU-side, so the
-// epilogues' LDS staging traffic (in-order with ds_bpermute) does not wait behind the butterflies
-template <int X>
-__device__ __forceinline__ float xor_dpp(float v) {
-    const int i = __builtin_bit_cast(int, v);
-    if constexpr (X == 1) return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, i, 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
-    else if constexpr (X == 2) return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, i, 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
-    else if constexpr (X == 8) return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, i, 0x128, 0xF, 0xF, false));  // row_ror 8
-    else {  // lanes 0-3 of each 8 take lane + 4 (row_ror 12), lanes 4-7 take lane - 4 (row_ror 4)
-        const int up = __builtin_amdgcn_update_dpp(0, i, 0x12C, 0xF, 0xF, false);
-        const int dn = __builtin_amdgcn_update_dpp(0, i, 0x124, 0xF, 0xF, false);
-        return __builtin_bit_cast(float, (__lane_id() & 4) ? dn : up);
-    }
-}
-__device__ __forceinline__ uint32_t xor1_dpp_u(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
-}
-
-// the 8 quads of a group in 8 lanes (quad index = lane bits 0..2): {sum, M2}, the same in every lane
-__device__ __forceinline__ float2 lnf_group8(float4 o) {
-#pragma clang fp contract(off)
-    float s = (o.x + o.y) + (o.z + o.w);
-    s = s + xor_dpp<1>(s);
-    s = s + xor_dpp<2>(s);
-    s = s + xor_dpp<4>(s);
-    const float mean = s * (1.0f / kLnfGroup);
-    const float a = o.x - mean, b = o.y - mean, c = o.z - mean, e = o.w - mean;
-    const float a2 = a * a, b2 = b * b, c2 = c * c, e2 = e * e;
-    float m = (a2 + b2) + (c2 + e2);
-    m = m + xor_dpp<1>(m);
-    m = m + xor_dpp<2>(m);
-    m = m + xor_dpp<4>(m);
-    return make_float2(s, m);
-}
-// MFMA-layout form: one column per lane (lane bits 0..1 = column within the quad, 2..3 = quad bits 0..1)
-// and the two fragments lo / hi of the group (quad bit 2) in registers
-__device__ __forceinline__ float2 lnf_group16(float lo, float hi) {
-#pragma clang fp contract(off)
-    float s0 = lo + xor_dpp<1>(lo), s1 = hi + xor_dpp<1>(hi);
-    s0 = s0 + xor_dpp<2>(s0); s1 = s1 + xor_dpp<2>(s1);
-    s0 = s0 + xor_dpp<4>(s0); s1 = s1 + xor_dpp<4>(s1);
-    s0 = s0 + xor_dpp<8>(s0); s1 = s1 + xor_dpp<8>(s1);
-    const float s = s0 + s1;
-    const float mean = s * (1.0f / kLnfGroup);
-    const float a = lo - mean, b = hi - mean;
-    float m0 = a * a, m1 = b * b;
-    m0 = m0 + xor_dpp<1>(m0); m1 = m1 + xor_dpp<1>(m1);
-    m0 = m0 + xor_dpp<2>(m0); m1 = m1 + xor_dpp<2>(m1);
-    m0 = m0 + xor_dpp<4>(m0); m1 = m1 + xor_dpp<4>(m1);
-    m0 = m0 + xor_dpp<8>(m0); m1 = m1 + xor_dpp<8>(m1);
-    return make_float2(s, m0 + m1);
-}
-__device__ __forceinline__ size_t lnf_part_index(const GemmArgs& g, int bz, int row, int col) {
-    return ((size_t)bz * g.M + row) * (size_t)(g.N / kLnfGroup) + col / kLnfGroup;
-}
-// consumer: {mean, rstd} of an A row from its G = K / 32 partials, by 4 lanes (4 r + q): lane q
-// holds groups [q G / 4, (q + 1) G / 4) (lnf_load, issued ahead of the first DMA) and sums them in
-// order; the 4 quarter sums combine as (q0 + q1) + (q2 + q3) -- one fixed order in every tile shape
-constexpr int kLnfQ = kLnfMaxG / 4;  // groups per quarter, at most
-__device__ __forceinline__ void lnf_load(const float2* part_row, int K, int q, float2 (&v)[kLnfQ]) {
-    const int gq = K / kLnfGroup / 4;
-#pragma unroll
-    for (int i = 0; i < kLnfQ; ++i) v[i] = part_row[q * gq + min(i, gq - 1)];
-}
-__device__ __forceinline__ float2 lnf_merge(const float2 (&v)[kLnfQ], int K) {
-#pragma clang fp contract(off)
-    const int gq = K / kLnfGroup / 4;
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < kLnfQ; ++i)
-        if (i < gq) s = s + v[i].x;
-    s = s + xor_dpp<1>(s);
-    s = s + xor_dpp<2>(s);
-    const float mean = s / (float)K;
-    float m2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < kLnfQ; ++i)
-        if (i < gq) {
-            const float dm = v[i].x * (1.0f / kLnfGroup) - mean;
-            float t = dm * dm;
-            t = t * (float)kLnfGroup;
-            m2 = m2 + v[i].y;
-            m2 = m2 + t;
-        }
-    m2 = m2 + xor_dpp<1>(m2);
-    m2 = m2 + xor_dpp<2>(m2);
-    return make_float2(mean, 1.0f / sqrtf(m2 / (float)K + 1e-5f));
-}
-// consumer output element before the activation: (acc - mean gw) rstd + bw, as two explicit FMAs
-// (the same bits in every tile shape)
-__device__ __forceinline__ float lnf_apply(float acc, float2 mr, float gw, float bw) {
-    return __builtin_fmaf(__builtin_fmaf(-mr.x, gw, acc), mr.y, bw);
-}
-template <typename T> __device__ __forceinline__ uint32_t lnf_pack2(float a, float b);
-template <> __device__ __forceinline__ uint32_t lnf_pack2<bf16>(float a, float b) { return pack_bf2(a, b); }
-template <> __device__ __forceinline__ uint32_t lnf_pack2<f16>(float a, float b) {
-    return (uint32_t)__builtin_bit_cast(unsigned short, (f16)a) | ((uint32_t)__builtin_bit_cast(unsigned short, (f16)b) << 16);
-}
-
 // ST-slot LDS ring (ST x 32 KiB, dynamic for ST > 2): ST - 1 K-slabs in flight while one is
 // computed.  The 16-slab GEMMs of a Parakeet streaming pass (M = 832, K = 1024) and Whisper's
 // smaller shapes give about one workgroup per CU and no other wave to cover a slab's load
@@ -239,10 +116,8 @@ template <> __device__ __forceinline__ uint32_t lnf_pack2<f16>(float a, float b)
 // BMT = 64 halves the tile's rows (each wave 32 x 64 of C), BNT = 64 its columns: at M = 832 a
 // 128 x 128 tile gives at most one workgroup per CU, so one wave per SIMD with every LDS read and
 // DMA wait of a k-step exposed.  Every C element is the same MFMA chain in every tile shape.
-template <typename T, int EPIX, int ST, int BMT = BM, int BNT = BN>
+template <typename T, int EPI, int ST, int BMT = BM, int BNT = BN>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256, 1) put the accumulators in AGPRs + ~90 copies per k-step
-    constexpr int EPI = epi_base(EPIX);
-    constexpr bool LNF = EPIX != EPI;
     static_assert((BMT == 64 || BMT == 128) && (BNT == 64 || BNT == 128), "tile shape");
     static_assert(ST == 2 || (BMT == 128 && BNT == 128), "deeper rings: 128 x 128 only");
     constexpr int MI = BMT / 32;      // 16-row A fragments per wave
@@ -301,28 +176,11 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256,
     const int nkt = Kc * (int)sizeof(T) / SLAB;
     const int fr = lane & 15, fq = lane >> 4;
 
-    // LayerNorm fold, consumer: {mean, rstd} of the tile's A rows into LDS behind the ring (the
-    // partials are loaded ahead of the first slab's DMA, merged after it is issued)
-    constexpr int STAT_OFF = ST * (BMT + BNT) * SLAB;
-    constexpr int LNF_P = BMT / 64;  // rows per thread (4 lanes per row)
-    constexpr bool lnf_c = LNF && lnf_consumer<EPI>();
-    float2 lv[LNF_P][kLnfQ];
-    if (lnf_c)
-#pragma unroll
-        for (int p = 0; p < LNF_P; ++p)
-            lnf_load(g.lnf_in + ((size_t)bz * g.M + min(m0 + 64 * p + (tid >> 2), g.M - 1)) * (g.K / kLnfGroup), g.K,
-                     tid & 3, lv[p]);
 
     // prologue: slabs 0 .. ST - 2.  Every iteration issues exactly one slab (past the end: the last
     // slab again, into a free slot), so each wave's vmcnt counts the same instructions everywhere.
 #pragma unroll
     for (int p = 0; p < ST - 1; ++p) stage(p, min(p, nkt - 1));
-    if (lnf_c)
-#pragma unroll
-        for (int p = 0; p < LNF_P; ++p) {
-            const float2 mr = lnf_merge(lv[p], g.K);
-            if (!(tid & 3)) *(float2*)(smem + STAT_OFF + (64 * p + (tid >> 2)) * 8) = mr;
-        }
     for (int kt = 0; kt < nkt; ++kt) {
         const int cur = kt % ST;
         // slab kt landed (8 DMA instructions per slab and wave; ST - 2 younger slabs may fly on),
@@ -403,40 +261,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256,
                 for (int r = 0; r < 4; ++r)
                     y[i][j][r] = epi_y<EPI>(g, bz, min(m0 + wm * (BMT / 2) + 16 * i + 4 * fq + r, g.M - 1), ec[j]);
     }
-    // LayerNorm fold operands: the next LayerNorm's gamma of this lane's columns (producer), the
-    // fold tables of its columns (consumer)
-    constexpr bool lnf_p = LNF && lnf_producer<EPI>();
-    float lg[NJ], lgw[NJ], lbw[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-        lg[j] = lnf_p ? g.lnf_g[ec[j].col] : 0.f;
-        lgw[j] = lnf_c ? g.lnf_gw[ec[j].col] : 0.f;
-        lbw[j] = lnf_c ? g.lnf_bw[ec[j].col] : 0.f;
-    }
     epi_loads_landed();
-    if constexpr (lnf_c) {
-        {
-            float2 mrv[MI][4];
-#pragma unroll
-            for (int i = 0; i < MI; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) mrv[i][r] = *(const float2*)(smem + STAT_OFF + (wm * (BMT / 2) + 16 * i + 4 * fq + r) * 8);
-#pragma unroll
-            for (int i = 0; i < MI; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int rl = wm * (BMT / 2) + 16 * i + 4 * fq + r, row = m0 + rl;
-                    const float2 mr = mrv[i][r];
-#pragma unroll
-                    for (int j = 0; j < NJ; ++j) {
-                        float v = lnf_apply(acc[i][j][r], mr, lgw[j], lbw[j]);
-                        if constexpr (EPI == EPI_BIAS_GELU) v = gelu_tanh(v);
-                        if (row < g.M) ((T*)g.C + (size_t)bz * g.sC)[(size_t)row * g.ldc + ec[j].col] = from_f<T>(v);
-                    }
-                }
-            return;
-        }
-    }
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
@@ -446,40 +271,6 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256,
                 const int row = m0 + wm * (BMT / 2) + 16 * i + 4 * fq + r;
                 if (row < g.M) epi_store<T, EPI>(g, bz, row, ec[j], acc[i][j][r], y[epi_reads_y<EPI>() ? i : 0][j][r]);
             }
-    if constexpr (lnf_p) {
-        {
-            // x o gamma (model dtype; lane pairs fr, fr ^ 1 store two adjacent columns) and the
-            // partials of each 32-column group (fragments 2 jp, 2 jp + 1)
-            T* xg = (T*)g.lnf_xg + (size_t)bz * g.sC;
-#pragma unroll
-            for (int i = 0; i < MI; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = m0 + wm * (BMT / 2) + 16 * i + 4 * fq + r;
-#pragma unroll
-                    for (int jp = 0; jp < NJ / 2; ++jp) {
-                        float o[2];
-#pragma unroll
-                        for (int h = 0; h < 2; ++h) {
-                            const int j = 2 * jp + h;
-                            o[h] = epi_value<EPI>(g, ec[j], acc[i][j][r], y[i][j][r]);
-                            const float xv = o[h] * lg[j];
-                            if constexpr (sizeof(T) == 4) {
-                                const float nb = xor_dpp<1>(xv);
-                                if (!(fr & 1) && row < g.M)
-                                    *(float2*)(xg + (size_t)row * g.ldc + ec[j].col) = make_float2(xv, nb);
-                            } else {
-                                const float nb = xor_dpp<1>(xv);
-                                if (!(fr & 1) && row < g.M)
-                                    *(uint32_t*)(xg + (size_t)row * g.ldc + ec[j].col) = lnf_pack2<T>(xv, nb);
-                            }
-                        }
-                        const float2 st = lnf_group16(o[0], o[1]);
-                        if (fr == 0 && row < g.M) g.lnf_part[lnf_part_index(g, bz, row, ec[2 * jp].col)] = st;
-                    }
-                }
-        }
-    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -506,8 +297,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {  // (256,
 constexpr int G2_BM = 256, G2_BN = 256, G2_ROW = 128;  // G2_ROW: bytes of K per row per K-tile
 constexpr int G2_BUF = 2 * 256 * G2_ROW;               // one buffer: A + W
 constexpr int G2_LDS = 2 * G2_BUF;                     // 128 KiB
-constexpr int G2_STAT = 8 * 128 * (128 + 16) > G2_LDS ? 8 * 128 * (128 + 16) : G2_LDS;  // + epilogue staging
-constexpr int G2_LDS_ALL = G2_STAT + 256 * 8;  // + the LayerNorm fold's {mean, rstd} of the tile's rows
+constexpr int G2_LDS_ALL = 8 * 128 * (128 + 16) > G2_LDS ? 8 * 128 * (128 + 16) : G2_LDS;  // + epilogue staging
 
 // STG: the wave groups wr = 0 (waves 0-3) and wr = 1 (waves 4-7; each SIMD holds one wave of each)
 // run one phase apart -- group 1 passes one extra barrier first, group 0 one extra at the end --
@@ -521,10 +311,8 @@ constexpr int G2_LDS_ALL = G2_STAT + 256 * 8;  // + the LayerNorm fold's {mean, 
 // other multiplies.  The restaging and wait rules above hold unchanged (a read completes before its
 // phase's MFMAs; a half-tile is restaged >= 2 phases after its last read and read >= 2 phases after
 // every wave's wait for it), and the MFMA order per accumulator is the same: bitwise equal results.
-template <int EPIX, bool F16, bool STG = false, bool PP = false>
+template <int EPI, bool F16, bool STG = false, bool PP = false>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
-    constexpr int EPI = epi_base(EPIX);
-    constexpr bool LNF = EPIX != EPI;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wr = wid >> 2, wc = wid & 3;
@@ -624,25 +412,9 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
 #define G2_BARRIER() asm volatile("s_barrier" ::: "memory")
 #define G2_VMWAIT() asm volatile("s_waitcnt vmcnt(10)" ::: "memory")
 
-    // LayerNorm fold, consumer: {mean, rstd} of the tile's 256 A rows into LDS after the epilogue's
-    // staging region (partials loaded ahead of the prologue's DMA, merged after it is issued)
-    constexpr bool lnf_c = LNF && lnf_consumer<EPI>();
-    float2 lv[2][kLnfQ];  // rows tid / 4 and 128 + tid / 4, quarter tid % 4
-    if (lnf_c)
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-            lnf_load(g.lnf_in + ((size_t)bz * g.M + min(m0 + 128 * p + (tid >> 2), g.M - 1)) * (g.K / kLnfGroup), g.K,
-                     tid & 3, lv[p]);
-
     // prologue: K-tile 0 whole, K-tile 1 but its A1 (issued by K-tile 0's P1)
     stageA(0, 0, 0); stageW(0, 0, 0); stageW(0, 0, 1); stageA(0, 0, 1);
     stageA(1, 1, 0); stageW(1, 1, 0); stageW(1, 1, 1);
-    if (lnf_c)
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            const float2 mr = lnf_merge(lv[p], g.K);
-            if (!(tid & 3)) *(float2*)(smem + G2_STAT + (128 * p + (tid >> 2)) * 8) = mr;
-        }
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     G2_BARRIER();
     if constexpr (STG) {
@@ -726,26 +498,9 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
     constexpr int CPR = 64 * ESZ / 16;         // 16-byte chunks per row (8 or 16)
     constexpr int RPI = 64 / CPR;              // rows per wave-instruction (8 or 4)
     char* wreg = smem + wid * (PR * RS);
-    float bv[4], lgw[4], lbw[4];
+    float bv[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        bv[j] = g.bias ? g.bias[n0 + wc * 64 + 16 * j + fr] : 0.0f;
-        lgw[j] = lnf_c ? g.lnf_gw[n0 + wc * 64 + 16 * j + fr] : 0.0f;
-        lbw[j] = lnf_c ? g.lnf_bw[n0 + wc * 64 + 16 * j + fr] : 0.0f;
-    }
-    // LayerNorm fold, consumer: {mean, rstd} of this lane's 32 accumulator rows, read from LDS once
-    // (inside the staging loop each read waited behind the staging writes before it)
-    float2 mrv[lnf_c ? 8 : 1][4];
-    if constexpr (lnf_c) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) mrv[i][r] = *(const float2*)(smem + G2_STAT + (wr * 128 + 16 * i + 4 * fq + r) * 8);
-    }
-    // LayerNorm fold, producer: the next LayerNorm's gamma of this lane's 4 columns (16-byte chunk ch)
-    constexpr bool lnf_p = LNF && lnf_producer<EPI>();
-    float4 lg = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (lnf_p) lg = *(const float4*)(g.lnf_g + n0 + wc * 64 + (lane % CPR) * (16 / ESZ));
+    for (int j = 0; j < 4; ++j) bv[j] = g.bias ? g.bias[n0 + wc * 64 + 16 * j + fr] : 0.0f;
 #pragma unroll
     for (int pass = 0; pass < 128 / PR; ++pass) {
         const int ch = lane % CPR, rsub = lane / CPR;
@@ -774,11 +529,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int rl = 16 * ii + 4 * fq + r, cl = 16 * j + fr;
-                    float v;
-                    if constexpr (lnf_c)
-                        v = lnf_apply(acc[i][j][r], mrv[lnf_c ? i : 0][r], lgw[j], lbw[j]);
-                    else
-                        v = acc[i][j][r] + bv[j];
+                    float v = acc[i][j][r] + bv[j];
                     if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_POS) v = gelu_tanh(v);
                     if constexpr (EPI == EPI_BIAS_SWISH) v = swish(v);
                     if constexpr (EPI == EPI_BIAS_RELU) v = fmaxf(v, 0.0f);
@@ -795,8 +546,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
             const int rl = it * RPI + rsub;
             const int row = m0 + wr * 128 + pass * PR + rl;
             const uint4 v = *(const uint4*)(wreg + rl * RS + ch * 16);
-            if (!lnf_p && row >= g.M) continue;  // (fold producers: lanes of every row shuffle below)
-            const bool rv = row < g.M;
+            if (row >= g.M) continue;
             const int col = n0 + wc * 64 + ch * (16 / ESZ);
             if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_SWISH || EPI == EPI_BIAS_RELU) {
                 *(uint4*)((bf16*)g.C + (size_t)bz * g.sC + (size_t)row * g.ldc + col) = v;
@@ -815,20 +565,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmArgs g) {
                 if constexpr (YIN) y = ypre[it];
                 else y = make_float4(0.f, 0.f, 0.f, 0.f);
                 o.x += y.x; o.y += y.y; o.z += y.z; o.w += y.w;
-                if (rv) *(float4*)cp = o;
-                if constexpr (lnf_p) {
-                    {
-                        // x o gamma, 8 columns per even lane (16-byte stores), and the partials of the
-                        // lane's 32-column group (lanes ch & ~7 .. + 7)
-                        typedef typename std::conditional<F16, f16, bf16>::type T;
-                        const uint32_t p0 = lnf_pack2<T>(o.x * lg.x, o.y * lg.y), p1 = lnf_pack2<T>(o.z * lg.z, o.w * lg.w);
-                        const uint32_t q0 = xor1_dpp_u(p0), q1 = xor1_dpp_u(p1);
-                        if (rv && !(ch & 1))
-                            *(uint4*)((T*)g.lnf_xg + (size_t)bz * g.sC + (size_t)row * g.ldc + col) = make_uint4(p0, p1, q0, q1);
-                        const float2 st = lnf_group8(o);
-                        if (rv && !(ch & 7)) g.lnf_part[lnf_part_index(g, bz, row, col)] = st;
-                    }
-                }
+                *(float4*)cp = o;
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -953,7 +690,7 @@ void launch_t_st(const GemmArgs& g0, int batch, hipStream_t st) {
     static const int nmajor = getenv("SPT_GEMM_NT_RASTER") ? atoi(getenv("SPT_GEMM_NT_RASTER")) : 0;
     GemmArgs g = g0;
     g.nmajor = nmajor;
-    constexpr int lds = ST * 2 * BM * SLAB + BM * 8;  // + the LayerNorm fold's row statistics
+    constexpr int lds = ST * 2 * BM * SLAB;
     if (lds > 64 * 1024) ensure_lds_attr((const void*)gemm_nt_kernel<T, EPI, ST>, lds);
     dim3 grid(cdiv(g.M, BM) * (g.N / BN), g.ksplit, batch);
     hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, ST>), grid, dim3(256), lds, st, g);
@@ -965,7 +702,7 @@ void launch_small(const GemmArgs& g0, int batch, hipStream_t st) {  // 64 x 128 
     GemmArgs g = g0;
     g.nmajor = nmajor;
     dim3 grid(cdiv(g.M, BMT) * (g.N / BNT), g.ksplit, batch);
-    hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, 2, BMT, BNT>), grid, dim3(256), 2 * (BMT + BNT) * SLAB + BMT * 8, st, g);
+    hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, 2, BMT, BNT>), grid, dim3(256), 2 * (BMT + BNT) * SLAB, st, g);
 }
 
 template <typename T, int EPI>
@@ -987,12 +724,12 @@ void prepare_epi() {
     ensure_lds_attr((const void*)gemm256_kernel<EPI, true, true>, G2_LDS_ALL);
     ensure_lds_attr((const void*)gemm256_kernel<EPI, false, true, true>, G2_LDS_ALL);
     ensure_lds_attr((const void*)gemm256_kernel<EPI, true, true, true>, G2_LDS_ALL);
-    ensure_lds_attr((const void*)gemm_nt_kernel<bf16, EPI, 3>, 3 * 2 * BM * SLAB + BM * 8);
-    ensure_lds_attr((const void*)gemm_nt_kernel<f16, EPI, 3>, 3 * 2 * BM * SLAB + BM * 8);
-    ensure_lds_attr((const void*)gemm_nt_kernel<float, EPI, 3>, 3 * 2 * BM * SLAB + BM * 8);
-    ensure_lds_attr((const void*)gemm_nt_kernel<bf16, EPI, kNtStages>, kNtStages * 2 * BM * SLAB + BM * 8);
-    ensure_lds_attr((const void*)gemm_nt_kernel<f16, EPI, kNtStages>, kNtStages * 2 * BM * SLAB + BM * 8);
-    ensure_lds_attr((const void*)gemm_nt_kernel<float, EPI, kNtStages>, kNtStages * 2 * BM * SLAB + BM * 8);
+    ensure_lds_attr((const void*)gemm_nt_kernel<bf16, EPI, 3>, 3 * 2 * BM * SLAB);
+    ensure_lds_attr((const void*)gemm_nt_kernel<f16, EPI, 3>, 3 * 2 * BM * SLAB);
+    ensure_lds_attr((const void*)gemm_nt_kernel<float, EPI, 3>, 3 * 2 * BM * SLAB);
+    ensure_lds_attr((const void*)gemm_nt_kernel<bf16, EPI, kNtStages>, kNtStages * 2 * BM * SLAB);
+    ensure_lds_attr((const void*)gemm_nt_kernel<f16, EPI, kNtStages>, kNtStages * 2 * BM * SLAB);
+    ensure_lds_attr((const void*)gemm_nt_kernel<float, EPI, kNtStages>, kNtStages * 2 * BM * SLAB);
 }
 
 }  // namespace
@@ -1009,10 +746,6 @@ void ensure_lds_attr(const void* kernel, int bytes) {
 }
 
 void gemm_prepare() {
-    prepare_epi<EPI_BIAS | EPI_LNF>();
-    prepare_epi<EPI_BIAS_GELU | EPI_LNF>();
-    prepare_epi<EPI_BIAS_GELU_POS | EPI_LNF>();
-    prepare_epi<EPI_BIAS_RESID | EPI_LNF>();
     prepare_epi<EPI_BIAS>();
     prepare_epi<EPI_BIAS_GELU>();
     prepare_epi<EPI_BIAS_GELU_POS>();
@@ -1028,16 +761,6 @@ void gemm_nt(int dtype, int epi, const GemmArgs& g, int batch, hipStream_t st) {
 
 void gemm_nt_variant(int dtype, int epi, const GemmArgs& g, int batch, int variant, hipStream_t st) {
     const int esz = dtype == DT_F32 ? 4 : 2;
-    // the LayerNorm fold's kernels (kernels.h GemmArgs lnf_*)
-    const bool lnf_cons = g.lnf_in && (epi == EPI_BIAS || epi == EPI_BIAS_GELU);
-    const bool lnf_prod = g.lnf_g && (epi == EPI_BIAS_RESID || epi == EPI_BIAS_GELU_POS);
-    if (lnf_cons || lnf_prod) {
-        if (variant == 3 || g.ksplit != 1 || (lnf_cons && (g.K > 40 * kLnfGroup || g.K % (4 * kLnfGroup))) ||
-            (lnf_prod && (g.N > 40 * kLnfGroup || g.N % 64)))
-            throw std::runtime_error("gemm_nt: LayerNorm fold needs a tile kernel, no split-K, a consumer K <= 1280 "
-                                     "with K % 128 == 0, a producer N <= 1280 with N % 64 == 0");
-        epi |= EPI_LNF;
-    }
     if (g.ksplit < 1 || g.K % g.ksplit || (g.ksplit > 1 && epi != EPI_PARTIAL))
         throw std::runtime_error("gemm_nt: split-K needs EPI_PARTIAL and K % ksplit == 0");
     if (variant != 3 && (g.N % (variant == 5 ? 64 : BN) != 0 || (g.K / g.ksplit * esz) % SLAB != 0 || g.M <= 0))
@@ -1054,10 +777,6 @@ void gemm_nt_variant(int dtype, int epi, const GemmArgs& g, int batch, int varia
         case EPI_BIAS_RELU: launch_t<T, EPI_BIAS_RELU>(g, batch, variant, st); return; \
         case EPI_BIAS_F32: launch_t<T, EPI_BIAS_F32>(g, batch, variant, st); return; \
         case EPI_PARTIAL: launch_t<T, EPI_PARTIAL>(g, batch, variant, st); return; \
-        case EPI_BIAS | EPI_LNF: launch_t<T, EPI_BIAS | EPI_LNF>(g, batch, variant, st); return; \
-        case EPI_BIAS_GELU | EPI_LNF: launch_t<T, EPI_BIAS_GELU | EPI_LNF>(g, batch, variant, st); return; \
-        case EPI_BIAS_GELU_POS | EPI_LNF: launch_t<T, EPI_BIAS_GELU_POS | EPI_LNF>(g, batch, variant, st); return; \
-        case EPI_BIAS_RESID | EPI_LNF: launch_t<T, EPI_BIAS_RESID | EPI_LNF>(g, batch, variant, st); return; \
     }
 #define SPT_GEMM256_CASES(F)                                                       \
     switch (epi) {                                                                 \
@@ -1070,10 +789,6 @@ void gemm_nt_variant(int dtype, int epi, const GemmArgs& g, int batch, int varia
         case EPI_BIAS_RELU: launch_256<EPI_BIAS_RELU, F>(g, batch, st); return;    \
         case EPI_BIAS_F32: launch_256<EPI_BIAS_F32, F>(g, batch, st); return;      \
         case EPI_PARTIAL: launch_256<EPI_PARTIAL, F>(g, batch, st); return;        \
-        case EPI_BIAS | EPI_LNF: launch_256<EPI_BIAS | EPI_LNF, F>(g, batch, st); return; \
-        case EPI_BIAS_GELU | EPI_LNF: launch_256<EPI_BIAS_GELU | EPI_LNF, F>(g, batch, st); return; \
-        case EPI_BIAS_GELU_POS | EPI_LNF: launch_256<EPI_BIAS_GELU_POS | EPI_LNF, F>(g, batch, st); return; \
-        case EPI_BIAS_RESID | EPI_LNF: launch_256<EPI_BIAS_RESID | EPI_LNF, F>(g, batch, st); return; \
     }
 #define SPT_GEMM_SKINNY_CASES(F)                                                   \
     switch (epi) {                                                                 \

@@ -320,32 +320,6 @@ void ln_dispatch(const float* x, int M, int d, const float* w, const float* b, T
     }
 }
 
-// LayerNorm-fold tables of a consumer GEMM (GemmArgs lnf_gw / lnf_bw): one wave per output row n,
-// lane-strided f32 sums over K, then the wave's fixed reduction tree (deterministic)
-template <typename T>
-__global__ __launch_bounds__(256) void ln_fold_tables_kernel(const T* __restrict__ W, int N, int K,
-                                                             const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                             const float* __restrict__ b, float* __restrict__ gw,
-                                                             float* __restrict__ bw) {
-#pragma clang fp contract(off)
-    const int lane = threadIdx.x & 63;
-    const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (n >= N) return;
-    const T* w = W + (size_t)n * K;
-    float sg = 0.f, sb = 0.f;
-    for (int c = lane; c < K; c += 64) {
-        const float v = to_f<T>(w[c]);
-        sg += v * gamma[c];
-        sb += v * beta[c];
-    }
-    sg = wave_sum(sg);
-    sb = wave_sum(sb);
-    if (lane == 0) {
-        gw[n] = sg;
-        bw[n] = (b ? b[n] : 0.f) + sb;
-    }
-}
-
 template <typename T>
 __global__ void to_f32_kernel(const T* __restrict__ s, float* __restrict__ d, int64_t n) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -378,18 +352,6 @@ void layernorm_pend2(int dtype2, const float* x, int M, int d, const float* slab
     if (dtype2 == DT_BF16) ln_pend2_dispatch<bf16>(x, M, d, slab, ks, slab_stride, pbias, alpha, w, b, y, w2, b2, (bf16*)y2, st);
     else if (dtype2 == DT_F16) ln_pend2_dispatch<f16>(x, M, d, slab, ks, slab_stride, pbias, alpha, w, b, y, w2, b2, (f16*)y2, st);
     else ln_pend2_dispatch<float>(x, M, d, slab, ks, slab_stride, pbias, alpha, w, b, y, w2, b2, (float*)y2, st);
-    SPT_LAUNCH_CHECK();
-}
-
-void ln_fold_tables(int dtype, const void* W, int N, int K, const float* gamma, const float* beta, const float* b,
-                    float* gw, float* bw, hipStream_t st) {
-    const dim3 grid((N + 3) / 4);
-    if (dtype == DT_BF16)
-        hipLaunchKernelGGL(ln_fold_tables_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)W, N, K, gamma, beta, b, gw, bw);
-    else if (dtype == DT_F16)
-        hipLaunchKernelGGL(ln_fold_tables_kernel<f16>, grid, dim3(256), 0, st, (const f16*)W, N, K, gamma, beta, b, gw, bw);
-    else
-        hipLaunchKernelGGL(ln_fold_tables_kernel<float>, grid, dim3(256), 0, st, (const float*)W, N, K, gamma, beta, b, gw, bw);
     SPT_LAUNCH_CHECK();
 }
 

@@ -37,20 +37,7 @@ struct GemmArgs {
     float alpha = 1.0f;                   // EPI_BIAS_RESID / EPI_BIAS_F32 scale
     int ksplit = 1; int64_t c_split = 0;  // EPI_PARTIAL: K split over grid.y, slab stride (elements)
     int nmajor = 0;                       // 128 x 128 tile: raster tiles N-major (set by the launcher)
-    // LayerNorm fold (encoder, r6).  A producer (EPI_BIAS_RESID / EPI_BIAS_GELU_POS,
-    // f32 rows x) with lnf_g set also writes lnf_xg = x o lnf_g in the model dtype (same addressing
-    // as C) and, per row and 32-column group, lnf_part = {sum, sum of squared deviations from the
-    // group's mean} (canonical pairwise order, the same bits in every tile shape).  A consumer
-    // (EPI_BIAS / EPI_BIAS_GELU over A = lnf_xg) with lnf_in set merges the row's groups in order into
-    // mean and rstd and writes (acc - mean gw[n]) rstd + bw[n] (then GELU): LN(x) W^T + b, with
-    // gw = W gamma and bw = b + W beta precomputed (ln_fold_tables); g.bias is not read.
-    const float* lnf_g = nullptr; void* lnf_xg = nullptr; float2* lnf_part = nullptr;
-    const float2* lnf_in = nullptr; const float* lnf_gw = nullptr; const float* lnf_bw = nullptr;
 };
-constexpr int kLnfGroup = 32;  // columns per LayerNorm-fold partial
-// gw[n] = sum_c gamma_c W[n][c], bw[n] = b[n] + sum_c beta_c W[n][c] (f32, fixed order), W [N][K] of dtype
-void ln_fold_tables(int dtype, const void* W, int N, int K, const float* gamma, const float* beta, const float* b,
-                    float* gw, float* bw, hipStream_t st);
 void gemm_nt(int dtype, int epi, const GemmArgs& g, int batch, hipStream_t st);
 // variant 0: automatic (bf16 N % 256 == 0 -> 256 x 256 tile); 1: 128 x 128 tile; 2: prefer 256 x 256;
 // 3: skinny (M <= 64, 16-bit dtypes: 16 columns per workgroup, the weight stream spread over the grid)
@@ -214,56 +201,6 @@ struct FinalizeArgs {
 void dec_finalize(int dtype, const FinalizeArgs& a, int B, hipStream_t st);
 void dec_reset(DecState* ds, unsigned* arrive, hipStream_t st);
 
-// ------------------------------------------------------------------ persistent decoder pass (k_pdec.hip)
-// Every decoder layer of a one-token pass (Tq = 1, bf16) in ONE launch of one 512-thread workgroup
-// per CU: the eight per-layer stages of enqueue_layers (LN1+QKV, self-attention, self-out, LN2 +
-// cross-Q, cross-attention in 8 key chunks, their merge, cross-out, LN3+fc1, fc2) run as units
-// spread over the workgroups, each handing its output to the next stage as data-tagged 8-byte
-// granules.  Every unit repeats the per-stage kernels' arithmetic operation for operation (the
-// same K chains of each GEMV and their summation order, AttnWave's online softmax, attn_merge):
-// the pass is bitwise the launch chain's.
-struct PdLayer {
-    const float *ln1_w, *ln1_b; const void* qkv_w; const float* qkv_b;
-    const void* so_w; const float* so_b;
-    const float *ln2_w, *ln2_b; const void* cq_w; const float* cq_b;
-    const void* co_w; const float* co_b;
-    const float *ln3_w, *ln3_b; const void* fc1_w; const float* fc1_b;
-    const void* fc2_w; const float* fc2_b;
-};
-constexpr int kPdStages = 9;   // A B C D E E2 F G H
-struct PdArgs {
-    const PdLayer* layers; int L;            // device array [L]
-    int d, H, R, ctx, T_enc, B_layout;
-    const void* ckv; int64_t cross_layer;     // cross K/V (kv_offset layout, B_layout windows); at the
-                                              // group's first window when kvrow is null
-    const int* kvrow;                         // [R] window of each row, or null (row b -> window b)
-    void* skv; int64_t self_layer;            // self K/V, per layer [2][R][H][ctx][64]
-    const float* x;                           // [R][d] layer-0 input rows (kept: a failed pass re-runs)
-    float* xo;                                // [R][d] on return the last layer's cross-out residual
-    float* pend;                              // [2][R][d]: on return the last fc2's two K-split partials
-    const DecState* ds;
-    unsigned long long* gran;                 // granule arena: pdec_granules() words, zeroed per call
-    unsigned* ctl;                            // [4] census, exits, error, launch index (zeroed per call)
-    int force_giveup;                         // test hook (SPT_PD_FORCE_GIVEUP): the launch of this
-                                              // index within a call gives up (-1: never)
-    unsigned long long* stamps;               // diagnostics (SPT_PD_STAMP): per workgroup kPdStampMax
-                                              // records of kPdStampRec s_memrealtime words, or null
-    // geometry (pdec_launch fills it)
-    int nwg, e_vw, nss, U;
-    int n[kPdStages], pre[kPdStages], ks[kPdStages];
-    int64_t go[12];                           // granule buffer offsets
-};
-int64_t pdec_granules(int R, int d, int H);
-constexpr int kPdCtlWords = 4;
-// per-unit stage stamps (100 MHz s_memrealtime) of one pass, record = {meta = l | s << 8 | u << 16,
-// gather start, gather wave 0 inputs ready, compute after barrier A, compute weights landed, gather
-// after barrier B, compute done, publish landed, compute after issuing the next unit's prefetch,
-// compute after barrier B}
-constexpr int kPdStampRec = 10, kPdStampMax = 512;
-// empty string if the persistent pass can run this geometry, else why not
-std::string pdec_unsupported(int dtype, int d, int H, int R, int ctx, int T_enc);
-void pdec_launch(PdArgs a, hipStream_t st);
-void pdec_prepare();  // kernel attributes (outside stream capture)
 
 
 // whisper_full decoding parameters of one call (device memory: read by graph-captured launches)
