@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 for C in FETCH_SIZE WRITE_SIZE; do
   SPT_NO_GRAPH=1 timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d gpurun_out/pmc_${TAG}_$C -o run -- \
-     python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-app-latency --no-probe --no-turbo --no-parakeet --decode-steps 8 \
+     python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-app-latency --no-probe --no-turbo --no-parakeet --no-c2 --decode-steps 8 \
      > gpurun_out/pmc_${TAG}_$C.log 2>&1 || { echo "pmc $C failed"; exit 1; }
 done
 python3 scripts/pmc_parse.py ${TAG} > gpurun_out/pmc_${TAG}_parsed.txt && cp profiles/pmc_*.json gpurun_out/ && \
