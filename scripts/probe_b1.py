@@ -1,6 +1,7 @@
-"""GPU box, profiling: the app's B = 1 call shape on large-v3 bf16 (one 30 s window, greedy fast
-path, 128 tokens), three timed calls after a capture call.  Run under rocprofv3 --kernel-trace
---stats once with SPT_PERSISTENT=0 (the launch chain) and once with 1 (the persistent pass)."""
+"""GPU box, profiling / A/B: the app's B = 1 call shape on large-v3 bf16 (one 30 s window, greedy fast
+path, 128 tokens; B1_BATCH = 8: the C3 batch), three timed calls after a capture call.
+B1_DUMP=<file.npz>: the last call's tokens / top-1 / top-2 logits, for bitwise comparisons across
+switches read at engine creation."""
 import json
 import os
 import sys
@@ -36,7 +37,13 @@ for _ in range(3):
     run()
 t = e.timings()
 cs = e.call_stats()
-print(json.dumps({"persistent": os.environ.get("SPT_PERSISTENT", "0"), "decode_ms": t["decode_ms"],
-                  "passes": t["n_decode_passes"], "pass_ms": t["decode_ms"] / t["n_decode_passes"],
+print(json.dumps({"decode_ms": t["decode_ms"], "passes": t["n_decode_passes"], "pass_ms": t["decode_ms"] / t["n_decode_passes"],
                   "pd_passes": cs["pd_passes"], "pd_fallbacks": cs["pd_fallbacks"]}))
+if os.environ.get("B1_DUMP"):
+    import numpy as np
+
+    r = run()
+    rs = [r] if nb == 1 else r
+    np.savez(os.environ["B1_DUMP"], tokens=np.array([x.tokens for x in rs]), top1=np.array([x.top1 for x in rs]),
+             top2=np.array([x.top2 for x in rs]))
 e.unload_model()
