@@ -1744,14 +1744,14 @@ double Engine::probe(int kind, int iters, double* work, int* is_flops) {
     }
     if (kind == 4 || kind == 5) {
         // encoder kernels inside the encoder's own sequence: `iters` back-to-back runs of encoder
-        // layer 0's launches on the last call's buffers (enc_layer: q/k/v, attention, out, fc1,
-        // fc2, with the LayerNorms folded or, SPT_LN_FOLD=0, in front of q/k/v and fc1), with an event pair around the probed kernel of each run and one
-        // host wait at the end, so the kernel follows its producer, on a chip as busy (and as hot)
+        // layer 0's launches on the last call's buffers (enc_layer: LN1, q/k/v, attention, out, LN2,
+        // fc1, fc2), with an event pair around the probed kernel of each run and one host wait at the
+        // end, so the kernel follows its producer, on a chip as busy (and as hot)
         // as inside the encoder.  r4's back-to-back repeats of the kernel alone read the attention
         // 10 % below its rocprofv3 average, r5's producer-then-kernel pairs with a host wait
         // between them 8 % below.  The residual rows x grow by one layer per run: the probe runs
         // after the timed calls, and every call recomputes them.
-            if ((int)probe_ev_.size() < 2 * iters) {
+        if ((int)probe_ev_.size() < 2 * iters) {
             for (int i = (int)probe_ev_.size(); i < 2 * iters; ++i) {
                 hipEvent_t ev;
                 HIP_CHECK(hipEventCreate(&ev));
