@@ -363,6 +363,8 @@ def test_one_encoder_run_per_window_with_fallback(tiny):
     assert r.n_fallbacks == 5 * r.n_windows
     assert cs["encoder_windows"] == r.n_windows, cs
     assert cs["engine_calls"] >= 6 * r.n_windows, cs
+    # ABI 12's persistent-pass counters stay in the struct for layout; the pass was deleted in r6
+    assert cs["pd_passes"] == 0 and cs["pd_fallbacks"] == 0, cs
 
 
 @pytest.mark.parametrize("vw", ["0", "3"])
