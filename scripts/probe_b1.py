@@ -7,6 +7,8 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if os.environ.get("B1_PKG"):  # import spittle_amd from another build (A/B between builds on one box)
+    sys.path.insert(0, os.path.abspath(os.environ["B1_PKG"]))
 
 if os.environ.get("B1_TORCH"):  # initialise HIP through torch first (its bundled runtime), as bench.py does
     import torch  # noqa: E402

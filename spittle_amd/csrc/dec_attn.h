@@ -147,6 +147,37 @@ struct AttnWave {
             blk += NW;
         }
     }
+    // run() with the wave's first block (blk) already in ring slot 0: loaded before n_keys was known
+    // (self-attention: before the decoder position arrives), clamped to the cache's rows instead of
+    // n_keys - 1.  The keys past n_keys are masked in process() either way (p = 0 against finite
+    // cache rows), so the result is run()'s.
+    template <int MAXB>
+    __device__ __forceinline__ void run_pre(int blk, int nblk, const float (&qv)[NQ][8], const int (&lim)[NQ], int Tq) {
+        if (blk >= nblk) return;
+        const int cnt = (nblk - 1 - blk) / NW + 1;
+        const int mine = blk + (cnt - 1) * NW;
+        if (MAXB <= 8 && cnt <= MAXB) {
+#pragma unroll
+            for (int d = 1; d < PF - 1 && d < MAXB; ++d) load_blk(kc_[d], vc_[d], min(blk + d * NW, mine));
+#pragma unroll
+            for (int i = 0; i < (MAXB <= 8 ? MAXB : 1); ++i) {
+                if (i >= cnt) break;
+                if (i + PF - 1 < (MAXB <= 8 ? MAXB : 1))
+                    load_blk(kc_[(i + PF - 1) % PF], vc_[(i + PF - 1) % PF], min(blk + (i + PF - 1) * NW, mine));
+                process(kc_[i % PF], vc_[i % PF], (blk + i * NW) * KB, qv, lim, Tq);
+            }
+            return;
+        }
+        while (blk < nblk) {
+            load_blk(kc_[1], vc_[1], min(blk + NW, mine));
+            process(kc_[0], vc_[0], blk * KB, qv, lim, Tq);
+            blk += NW;
+            if (blk >= nblk) break;
+            load_blk(kc_[0], vc_[0], min(blk + NW, mine));
+            process(kc_[1], vc_[1], blk * KB, qv, lim, Tq);
+            blk += NW;
+        }
+    }
     // sum l and o over the 8 key slots of the wave (m is wave-uniform) into LDS
     __device__ __forceinline__ void to_lds(float (*s_m)[NQ], float (*s_l)[NQ], float (*s_o)[NQ][64], int wid,
                                            int lane) {

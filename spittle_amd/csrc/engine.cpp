@@ -1453,6 +1453,9 @@ void Engine::beam_begin(int B, const DecodeRequest& rq, BeamCands* out, int* lan
             kvtmp_ = nullptr;
             throw std::runtime_error("out of device memory for the beam search scratch");
         }
+        // finite from the start: the self-attention reads a wave's first key block before it knows
+        // the position (rows past it are masked, p = 0, and must not hold NaN / Inf bit patterns)
+        HIP_CHECK(hipMemset(kvtmp_, 0, bytes));
     }
     beam_rq_ = rq;
     beam_B_ = B;

@@ -599,11 +599,15 @@ __global__ __launch_bounds__(64 * AW) void self_attn_kernel(const T* __restrict_
     __shared__ float s_o[AW][NQ][64];
     const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane & 7;
+    AttnWave<T, NQ, NIX> aw;
+    // the wave's first key block is fetched before the position is known (every cache row is
+    // readable): the K/V stream no longer waits behind the DecState round trip (run_pre)
+    aw.init(kv + (((size_t)0 * B + b) * H + h) * (size_t)ctx * 64 + 8 * g,
+            kv + (((size_t)1 * B + b) * H + h) * (size_t)ctx * 64 + 8 * g, ctx, lane);
+    aw.load_blk(aw.kc_[0], aw.vc_[0], wid);
     const int pos0 = ds->pos0;
     const int n_keys = pos0 + Tq;
-    AttnWave<T, NQ, NIX> aw;
-    aw.init(kv + (((size_t)0 * B + b) * H + h) * (size_t)ctx * 64 + 8 * g,
-            kv + (((size_t)1 * B + b) * H + h) * (size_t)ctx * 64 + 8 * g, n_keys, lane);
+    aw.n_keys = n_keys;
     float qv[NQ][8];
     int lim[NQ];
 #pragma unroll
@@ -614,7 +618,7 @@ __global__ __launch_bounds__(64 * AW) void self_attn_kernel(const T* __restrict_
         for (int e = 0; e < 8; ++e) qv[t][e] = to_f<T>(qr[e]) * kLog2Scale;
         lim[t] = pos0 + tt + 1;
     }
-    aw.template run<(448 / AttnWave<T, NQ, NIX>::KB + 1 + AW - 1) / AW>(wid, cdiv(n_keys, AttnWave<T, NQ, NIX>::KB), qv, lim, Tq);
+    aw.template run_pre<(448 / AttnWave<T, NQ, NIX>::KB + 1 + AW - 1) / AW>(wid, cdiv(n_keys, AttnWave<T, NQ, NIX>::KB), qv, lim, Tq);
     aw.to_lds(s_m, s_l, s_o, wid, lane);
     __syncthreads();
     if (tid < 64 * Tq) {
