@@ -825,11 +825,14 @@ __global__ __launch_bounds__(FIN_T) void finalize_kernel(FinalizeArgs a) {
     const float* pp = a.pos + (size_t)pn * a.d;
     for (int i = tid; i < a.d; i += FIN_T) a.x[(size_t)b * a.d + i] = to_f<T>(e[i]) + pp[i];
     if (tid == 0) {
-        const unsigned prev = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        // relaxed: every block's reads of the step state were consumed before it arrives, and the next
+        // kernel sees the last arriver's plain stores across the launch boundary (an acq_rel RMW cost
+        // an L2 write-back and invalidate in every block's tail)
+        const unsigned prev = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (prev == (unsigned)gridDim.x - 1) {
             a.ds->pos0 = pos0 + a.Tq;
             a.ds->step = step + 1;
-            __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
