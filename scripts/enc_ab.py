@@ -17,8 +17,8 @@ from spittle_amd import WhisperEngine, WhisperInferenceParams, WhisperModelParam
 from spittle_amd.synth import synth_audio  # noqa: E402
 
 nb = int(os.environ.get("ENC_AB_B", "8"))  # windows per call (1: the app's single-window call)
-e = WhisperEngine(WhisperModelParams(dtype="bf16", max_batch=nb))
-e.load_model("synthetic:large-v3")
+e = WhisperEngine(WhisperModelParams(dtype=os.environ.get("ENC_AB_DTYPE", "bf16"), max_batch=nb))
+e.load_model(os.environ.get("ENC_AB_MODEL", "synthetic:large-v3"))
 xs = [synth_audio(i) for i in range(nb)]
 p = WhisperInferenceParams(language="en", no_timestamps=True, temperature_inc=0.0, ignore_eot=True, max_new_tokens=4)
 for _ in range(2):

@@ -1,25 +1,19 @@
-"""GPU box, developer A/B: encoder output of one large-v3 bf16 window (debug_encode) saved to
-gpurun_out/enc_<tag>.npy, plus the encoder probe times, for bitwise comparison between builds /
-environment switches."""
-import json
+"""GPU box: the encoder output of one seeded window (debug_encode) saved to an .npz, for bitwise
+comparisons across switches read at engine creation.  usage: enc_dump.py MODEL DTYPE OUT.npz"""
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import numpy as np
-import torch
+import numpy as np  # noqa: E402
 
-torch.cuda.init()
-from spittle_amd import WhisperEngine, WhisperInferenceParams, WhisperModelParams
-from spittle_amd.synth import synth_audio
+from spittle_amd import WhisperEngine, WhisperModelParams  # noqa: E402
+from spittle_amd.synth import synth_audio  # noqa: E402
 
-tag = sys.argv[1]
-e = WhisperEngine(WhisperModelParams(dtype="bf16", max_batch=8))
-e.load_model("synthetic:large-v3")
-mel = e.debug_mel(synth_audio(0))
+model, dtype, out = sys.argv[1], sys.argv[2], sys.argv[3]
+e = WhisperEngine(WhisperModelParams(dtype=dtype, max_batch=1))
+e.load_model(model)
+mel = e.debug_mel(synth_audio(5))
 enc = e.debug_encode(mel)
-np.save(f"gpurun_out/enc_{tag}.npy", enc)
-p = WhisperInferenceParams(language="en", no_timestamps=True, temperature_inc=0.0, ignore_eot=True, max_new_tokens=4)
-e.transcribe_batch([synth_audio(i) for i in range(8)], p)
-print(json.dumps({"tag": tag, "enc_sum": float(np.abs(enc).sum()), "enc_fc1_gemm": e.probe("enc_fc1_gemm", 20),
-                  "enc_attn": e.probe("enc_attn", 20)}))
+np.savez(out, enc=enc)
+print(out, enc.shape, float(np.abs(enc).max()))
+e.unload_model()
