@@ -523,6 +523,9 @@ void gemv_attr_all() {
         gemv_attr<T, MODE, ASRC, 1, 10, 2, 2, true>();
         gemv_attr<T, MODE, ASRC, 2, 10, 2, 2, true>();
         gemv_attr<T, MODE, ASRC, 4, 10, 2, 2, true>();
+        gemv_attr<T, MODE, ASRC, 1, 12, 1, 1, true>();
+        gemv_attr<T, MODE, ASRC, 2, 12, 1, 1, true>();
+        gemv_attr<T, MODE, ASRC, 4, 12, 1, 1, true>();
     }
 #undef SPT_ATTR
 }
@@ -558,6 +561,13 @@ void gemv_launch_rg(const GemvArgs& a, hipStream_t st) {
             if (exact_ln && nss == 10) {
                 if (a.N >= ct2_min) gemv_launch_cfg<T, MODE, ASRC, RG, 10, 2, 2, true>(a, st);
                 else gemv_launch_cfg<T, MODE, ASRC, RG, 10, 1, 1, true>(a, st);
+                return;
+            }
+            // K = 12 super-steps (Whisper-small's d = 768 in f32, the C2 decoder): 12 waves, one exact
+            // super-step each (experiment; SPT_GV_EXACT12=0: the 8-wave shape)
+            static const bool exact12 = !getenv("SPT_GV_EXACT12") || atoi(getenv("SPT_GV_EXACT12")) != 0;
+            if (exact_ln && exact12 && nss == 12) {
+                gemv_launch_cfg<T, MODE, ASRC, RG, 12, 1, 1, true>(a, st);
                 return;
             }
             if (a.N >= 4096 && nss <= 24) {
