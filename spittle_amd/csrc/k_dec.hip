@@ -513,6 +513,9 @@ void gemv_attr_all() {
         SPT_ATTR(8, 8, 4)
     } else if constexpr (ASRC == A_DIRECT || is_attn(ASRC)) {
         SPT_GV_CONFIGS(SPT_ATTR)
+        gemv_attr<T, MODE, ASRC, 1, 12, 1, 1, true>();
+        gemv_attr<T, MODE, ASRC, 2, 12, 1, 1, true>();
+        gemv_attr<T, MODE, ASRC, 4, 12, 1, 1, true>();
     } else {
         SPT_ATTR(4, 1, 2)
         SPT_ATTR(8, 1, 2)
@@ -572,6 +575,17 @@ void gemv_launch_rg(const GemvArgs& a, hipStream_t st) {
             }
             if (a.N >= 4096 && nss <= 24) {
                 gemv_launch_cfg<T, MODE, ASRC, RG, 8, 2, 3>(a, st);
+                return;
+            }
+        }
+        // the directly-read / attention-merge GEMVs of 12 super-steps (C2's self-out and cross-out) on
+        // the same exact 12-wave split (r6ac: pass 0.623 -> 0.618 ms; SPT_GV_EXACT12_DIRECT=0: 8 waves).
+        // A_DIRECT and A_ATTN keep one geometry, so the merged-partials projection stays bitwise the
+        // merge kernel's
+        static const bool exact12_direct = !getenv("SPT_GV_EXACT12_DIRECT") || atoi(getenv("SPT_GV_EXACT12_DIRECT")) != 0;
+        if constexpr (!is_ln(ASRC)) {
+            if (exact12_direct && nss == 12) {
+                gemv_launch_cfg<T, MODE, ASRC, RG, 12, 1, 1, true>(a, st);
                 return;
             }
         }
