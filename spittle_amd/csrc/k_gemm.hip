@@ -812,13 +812,16 @@ void gemm_nt_variant(int dtype, int epi, const GemmArgs& g, int batch, int varia
     // f32 (Whisper-small C2: one 30 s window gives 72-288 128 x 128 tiles on 256 CUs) takes the 64-row
     // tiles, like the 16-bit types (r6, profiles/r6/exp_f32_small_tiles.txt: C2 encoder 7.11 -> 5.42 ms);
     // SPT_GEMM_F32_SMALL=0 keeps the 128 x 128 tile
-    static const bool f32_small = !getenv("SPT_GEMM_F32_SMALL") || atoi(getenv("SPT_GEMM_F32_SMALL")) != 0;
+    // (read per launch, like the switches of launch_256: eager runs such as debug_encode pick it up)
+    const char* f32s_env = getenv("SPT_GEMM_F32_SMALL");
+    const bool f32_small = !f32s_env || atoi(f32s_env) != 0;
     if (variant == 0 && !force128 && dtype == DT_F32 && f32_small) {
         const int64_t t128 = (int64_t)cdiv(g.M, BM) * (g.N / BN) * g.ksplit * batch;
         const int64_t t64 = (int64_t)cdiv(g.M, 64) * (g.N / BN) * g.ksplit * batch;
         // below four rounds of 128 x 128 tiles (r6aa: at 256, Whisper-small's fc1 kept 288 of them,
         // 1.125 rounds; SPT_GEMM_F32_T128MIN moves the threshold)
-        static const int t128_min = getenv("SPT_GEMM_F32_T128MIN") ? atoi(getenv("SPT_GEMM_F32_T128MIN")) : 1024;
+        const char* t128_env = getenv("SPT_GEMM_F32_T128MIN");
+        const int t128_min = t128_env ? atoi(t128_env) : 1024;
         if (t128 < t128_min && g.N % 64 == 0) variant = (t64 >= 512 && g.N % BN == 0) ? 4 : 5;
     }
     if (variant == 0 && !force128 && dtype != DT_F32) {
