@@ -772,6 +772,7 @@ void Engine::enc_layer(int l, int Bg, int64_t r0, hipStream_t s, int probe, hipE
     layernorm(dt_, x, M, d, e.ln1_w, e.ln1_b, xn, s);
     g.A = xn; g.lda = d; g.W = e.qkv_w; g.ldw = d; g.M = M; g.N = 3 * d; g.K = d; g.bias = e.qkv_b;
     g.C = qkv; g.ldc = 3 * d;
+    g.groups = enc_groups_cur_;
     gemm_nt(dt_, EPI_BIAS, g, 1, s);
     if (probe == 5) HIP_CHECK(hipEventRecord(e0, s));
     enc_attention(dt_, qkv, Bg, T, H, ao, s);
@@ -779,17 +780,20 @@ void Engine::enc_layer(int l, int Bg, int64_t r0, hipStream_t s, int probe, hipE
     g = GemmArgs{};
     g.A = ao; g.lda = d; g.W = e.o_w; g.ldw = d; g.M = M; g.N = d; g.K = d; g.bias = e.o_b;
     g.C = x; g.ldc = d;
+    g.groups = enc_groups_cur_;
     gemm_nt(dt_, EPI_BIAS_RESID, g, 1, s);
     layernorm(dt_, x, M, d, e.ln2_w, e.ln2_b, xn, s);
     g = GemmArgs{};
     g.A = xn; g.lda = d; g.W = e.fc1_w; g.ldw = d; g.M = M; g.N = 4 * d; g.K = d; g.bias = e.fc1_b;
     g.C = ff; g.ldc = 4 * d;
     if (probe == 4) HIP_CHECK(hipEventRecord(e0, s));
+    g.groups = enc_groups_cur_;
     gemm_nt(dt_, EPI_BIAS_GELU, g, 1, s);
     if (probe == 4) HIP_CHECK(hipEventRecord(e1, s));
     g = GemmArgs{};
     g.A = ff; g.lda = 4 * d; g.W = e.fc2_w; g.ldw = 4 * d; g.M = M; g.N = d; g.K = 4 * d; g.bias = e.fc2_b;
     g.C = x; g.ldc = d;
+    g.groups = enc_groups_cur_;
     gemm_nt(dt_, EPI_BIAS_RESID, g, 1, s);
 }
 
@@ -827,6 +831,7 @@ void Engine::run_encoder(int B) {
         for (int i = 1; i < G; ++i) HIP_CHECK(hipStreamWaitEvent(stream_of(i), enc_ev_[0], 0));
     }
     auto rows = [&](void* base, int64_t row, int64_t ld, int es) { return (char*)base + row * ld * es; };
+    enc_groups_cur_ = G;  // the layers' GEMMs of the G groups run side by side (tile choice)
     for (int l = 0; l < dm_.n_enc; ++l)
         for (int i = 0; i < G; ++i)  // layer l of every group before layer l + 1 of any
             enc_layer(l, b0[i + 1] - b0[i], (int64_t)b0[i] * T, stream_of(i));
@@ -1761,6 +1766,7 @@ double Engine::probe(int kind, int iters, double* work, int* is_flops) {
                 probe_ev_.push_back(ev);
             }
         }
+        enc_groups_cur_ = 1;  // one full-batch launch per kernel
         for (int i = 0; i < iters; ++i) enc_layer(0, B, 0, st_, kind, probe_ev_[2 * i], probe_ev_[2 * i + 1]);
         HIP_CHECK(hipStreamSynchronize(st_));
         double tot = 0.0;

@@ -207,6 +207,7 @@ private:
     void run_encoder(int B);
     void enc_layer(int l, int Bg, int64_t r0, hipStream_t s, int probe = 0, hipEvent_t e0 = nullptr,
                    hipEvent_t e1 = nullptr);
+    int enc_groups_cur_ = 1;  // window groups of the encoder run being enqueued (GemmArgs::groups)
     void enqueue_encoder(int B);  // run_encoder, replayed from a per-B graph after the first call
     void run_cross_kv(int B);
     void run_decode(int B, const DecodeRequest& rq, int* tokens, float* top1, float* top2, int* lang_out,

@@ -832,7 +832,14 @@ void gemm_nt_variant(int dtype, int epi, const GemmArgs& g, int batch, int varia
         const int64_t t256 = (int64_t)cdiv(g.M, G2_BM) * (g.N / G2_BN) * g.ksplit * batch;
         const int64_t t128 = (int64_t)cdiv(g.M, BM) * (g.N / BN) * g.ksplit * batch;
         const int64_t t64 = (int64_t)cdiv(g.M, 64) * (g.N / BN) * g.ksplit * batch;
-        if (g.N % G2_BN != 0 || t256 < 96) variant = t128 >= 256 ? 1 : t64 >= 512 ? 4 : 5;
+        // r6: also below half a round of 256 x 256 tiles counted over the launches that run together (the
+        // encoder's window groups, g.groups): one 30 s window's fc1 (120 tiles, alone) is 4.5 % faster
+        // on the 128 x 128 tile, while two groups' 120-tile out / fc2 launches side by side are not
+        // (profiles/r6/exp_bf16_tile_thresholds.txt); SPT_GEMM_BF16_T256G moves that bound (0: off)
+        const char* t256g_env = getenv("SPT_GEMM_BF16_T256G");
+        const int t256g = t256g_env ? atoi(t256g_env) : 128;
+        if (g.N % G2_BN != 0 || t256 < 96 || t256 * std::max(1, g.groups) < t256g)
+            variant = t128 >= 256 ? 1 : t64 >= 512 ? 4 : 5;
     }
     const bool use256 = variant == 2 || (variant == 0 && !force128);
     const bool fits32 = (int64_t)g.M * g.lda < (1ll << 31) && (int64_t)g.N * g.ldw < (1ll << 31);

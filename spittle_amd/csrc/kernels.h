@@ -37,6 +37,7 @@ struct GemmArgs {
     float alpha = 1.0f;                   // EPI_BIAS_RESID / EPI_BIAS_F32 scale
     int ksplit = 1; int64_t c_split = 0;  // EPI_PARTIAL: K split over grid.y, slab stride (elements)
     int nmajor = 0;                       // 128 x 128 tile: raster tiles N-major (set by the launcher)
+    int groups = 1;                       // launches of this shape running concurrently (encoder window groups)
 };
 void gemm_nt(int dtype, int epi, const GemmArgs& g, int batch, hipStream_t st);
 // variant 0: automatic (bf16 N % 256 == 0 -> 256 x 256 tile); 1: 128 x 128 tile; 2: prefer 256 x 256;
