@@ -938,10 +938,9 @@ float* Engine::enqueue_layers(DecGroup& g, int E, int Tq) {
     float* xc = g.dx;   // current residual rows (dec_embed / dec_finalize wrote this pass's input here)
     float* xo = g.dx2;  // the other buffer
     int np = 0;         // pending slabs in g.pend
+    pend_fold_ = !getenv("SPT_DEC_XFOLD") || atoi(getenv("SPT_DEC_XFOLD")) != 0;
     auto ln_input = [&](GemvArgs& a) {  // LayerNorm prologue over xc + the pending slabs
-        a.A = xc;
-        for (int p = 0; p < kMaxPend; ++p) a.pend[p] = p < np ? g.pend + (int64_t)p * R * d : zero_;
-        a.n_pend = np;
+        ln_source(a, xc, g.pend, np, (int64_t)R * d);
         a.x_out = np > 0 ? xo : nullptr;
     };
     auto consumed = [&] {
@@ -955,6 +954,7 @@ float* Engine::enqueue_layers(DecGroup& g, int E, int Tq) {
     auto partial = [&](GemvArgs& a, int split) {  // a K-split projection producing pending slabs
         a.C = g.pend; a.ldc = d; a.c_split = (int64_t)R * d;
         a.ksplit = split;
+        a.p_resid = pend_fold_ ? xc : nullptr;
         if (a.K / ks < split) throw std::runtime_error("decoder projection too narrow for its K split");
         np = split;
     };
@@ -1021,6 +1021,15 @@ float* Engine::enqueue_layers(DecGroup& g, int E, int Tq) {
     return xc;
 }
 
+void Engine::ln_source(GemvArgs& a, float* xc, float* pend, int np, int64_t slab) const {
+    // x + p0 + p1 + ...; with the residual folded into slab 0 the sum starts at slab 0 (the same
+    // additions in the same order: bitwise the same rows)
+    const int f = np > 0 && pend_fold_ ? 1 : 0;
+    a.A = f ? pend : xc;
+    for (int p = 0; p < kMaxPend; ++p) a.pend[p] = p < np - f ? pend + (int64_t)(p + f) * slab : zero_;
+    a.n_pend = np - f;
+}
+
 // Final LayerNorm of each sequence's last row + logits (suppression mask `sup`, the step-0
 // blank rule when `blank`) + top-2 partials, then argmax / record / next embedding / advance.
 void Engine::enqueue_head(DecGroup& g, int Tq, const DecodeRequest& rq, int out_cap, float* xc,
@@ -1032,9 +1041,7 @@ void Engine::enqueue_head(DecGroup& g, int Tq, const DecodeRequest& rq, int out_
     GemvArgs a{};
     // final LayerNorm of the last token of each sequence (x + fc2's pending slabs); the
     // combined rows are not needed
-    a.A = xc;
-    for (int p = 0; p < kMaxPend; ++p) a.pend[p] = p < fc2_split_ ? g.pend + (int64_t)p * R * d : zero_;
-    a.n_pend = fc2_split_;
+    ln_source(a, xc, g.pend, fc2_split_, (int64_t)R * d);
     a.lda = Tq * d; a.a_row0 = (Tq - 1) * d; a.ln_w = lnf_w_; a.ln_b = lnf_b_; a.R = B;
     a.W = tok_emb_; a.N = dm_.n_vocab; a.K = d; a.C = g.logits; a.ldc = dm_.n_vocab; a.st = g.ds;
     a.suppress = sup;
@@ -1712,9 +1719,8 @@ double Engine::probe(int kind, int iters, double* work, int* is_flops) {
             probe_kind_ = -1;
             if (kind == 2) {
                 GemvArgs a{};
-                a.A = x; a.lda = d; a.ln_w = lnf_w_; a.ln_b = lnf_b_; a.R = Bg;
-                for (int p = 0; p < kMaxPend; ++p) a.pend[p] = p < fc2_split_ ? g.pend + (int64_t)p * Bg * d : zero_;
-                a.n_pend = fc2_split_;
+                ln_source(a, x, g.pend, fc2_split_, (int64_t)Bg * d);
+                a.lda = d; a.ln_w = lnf_w_; a.ln_b = lnf_b_; a.R = Bg;
                 a.W = tok_emb_; a.N = V; a.K = d; a.C = g.logits; a.ldc = V; a.st = g.ds;
                 a.suppress = suppress_; a.blank0 = a.blank1 = -1; a.part = g.part; a.n_tiles = (V + 15) / 16;
                 HIP_CHECK(hipEventRecord(probe_ev_[0], g.st));

@@ -224,6 +224,12 @@ private:
     int esz_;     // bytes per weight / activation element
     int cp_;      // padded mel channels (conv1 K = 3 * cp_)
     static constexpr int fc2_split_ = 2;  // K split of the fc2 projection (pending slabs)
+    // fc2's first split adds the residual into its slab, so the next LayerNorm prologue reads
+    // slab 0 + the other slabs instead of x + all of them (SPT_DEC_XFOLD=0: off; read when a pass
+    // is captured, by enqueue_layers, and used by the head that follows it)
+    bool pend_fold_ = true;
+    // the LayerNorm source over the residual xc and np pending slabs at pend (slab stride `slab`)
+    void ln_source(GemvArgs& a, float* xc, float* pend, int np, int64_t slab) const;
     int xsplit_ = 1;  // cross-attention key chunks per (b, h) (merged by the output projection)
     int n_groups_ = 1;
     int max_rows_ = 64;  // decoder rows per pass (gemv_max_image_rows); larger batches use more groups  // SPT_DECODE_GROUPS=2 splits the batch over two streams

@@ -117,7 +117,7 @@ __device__ __forceinline__ F load_w(const F* p) {
 //             workgroup (0, 0) also writes the combined rows to x_out;
 //   A_ATTN    the cross-attention output merged from its S key-chunk partials
 //             [R][H][S][66] = {o[64], m, l} (rows of this workgroup's K range), staged in LDS.
-// kernel-side A source codes: A_DIRECT, LN_SRC(np) = A_LN with np pending slabs (0, 2, 4), or
+// kernel-side A source codes: A_DIRECT, LN_SRC(np) = A_LN with np pending slabs (0, 1, 2, 4), or
 // ATTN_SRC(s) = A_ATTN combining s cross-attention key chunks
 constexpr int LN_SRC(int np) { return 16 + np; }
 constexpr bool is_ln(int asrc) { return asrc >= 16 && asrc < 32; }
@@ -206,13 +206,17 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
         if (ep_lane && a.bias && kz == 0) bias_pre = a.bias[n_ep];
     }
     float resid_pre[RG][4];
-    if constexpr (MODE == GV_BIAS_RESID) {
+    // GV_PARTIAL with p_resid: split 0 adds the residual rows into its slab, so the consumer's
+    // prologue sums one slab fewer (x + p0 is formed here instead of there: the same operation)
+    const float* resid = MODE == GV_BIAS_RESID ? (const float*)a.C
+                         : MODE == GV_PARTIAL && kz == 0 ? a.p_resid : nullptr;
+    if constexpr (MODE == GV_BIAS_RESID || MODE == GV_PARTIAL) {
 #pragma unroll
         for (int g = 0; g < RG; ++g)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = g * 16 + 4 * fq + r;
-                resid_pre[g][r] = (ep_lane && row < a.R) ? ((const float*)a.C)[(size_t)row * a.ldc + n_ep] : 0.f;
+                resid_pre[g][r] = (resid && ep_lane && row < a.R) ? resid[(size_t)row * a.ldc + n_ep] : 0.f;
             }
     }
     int st_pre = 0;  // decoder step state: GV_QKV_CACHE appends at pos0, GV_LOGITS reads step
@@ -437,7 +441,7 @@ __global__ __launch_bounds__(64 * NWV) void gemv_kernel(GemvArgs a) {
             } else if constexpr (MODE == GV_BIAS_GELU) {
                 ((T*)a.C)[(size_t)row * a.ldc + n] = from_f<T>(gelu_tanh(y));
             } else if constexpr (MODE == GV_PARTIAL) {
-                ((float*)a.C + (size_t)kz * a.c_split)[(size_t)row * a.ldc + n] = y;
+                ((float*)a.C + (size_t)kz * a.c_split)[(size_t)row * a.ldc + n] = resid ? resid_pre[g][r] + y : y;
             } else if constexpr (MODE == GV_BIAS_RESID) {
                 ((float*)a.C)[(size_t)row * a.ldc + n] = resid_pre[g][r] + y;
             } else if constexpr (MODE == GV_QKV_CACHE) {
@@ -486,12 +490,14 @@ void gemv_launch_cfg(const GemvArgs& a, hipStream_t st) {
 // the (mode, A source) pairs the decoder uses
 #define SPT_GV_PAIRS(X)                 \
     X(GV_QKV_CACHE, LN_SRC(0))          \
+    X(GV_QKV_CACHE, LN_SRC(1))          \
     X(GV_QKV_CACHE, LN_SRC(2))          \
     X(GV_QKV_CACHE, LN_SRC(4))          \
     X(GV_BIAS, LN_SRC(0))               \
     X(GV_BIAS, LN_SRC(2))               \
     X(GV_BIAS_GELU, LN_SRC(0))          \
     X(GV_LOGITS, LN_SRC(0))             \
+    X(GV_LOGITS, LN_SRC(1))             \
     X(GV_LOGITS, LN_SRC(2))             \
     X(GV_LOGITS, LN_SRC(4))             \
     X(GV_PARTIAL, A_DIRECT)             \
@@ -896,8 +902,9 @@ void gemv(int dtype, int mode, int asrc, const GemvArgs& a_in, hipStream_t st) {
         throw std::runtime_error("gemv: A image exceeds the LDS budget");
     if (asrc == A_LN && (a.K > 1536 || !a.ln_w || !a.ln_b))
         throw std::runtime_error("gemv: LayerNorm prologue needs K <= 1536 and LN parameters");
-    if (asrc == A_LN && a.n_pend != 0 && a.n_pend != 2 && a.n_pend != 4)
-        throw std::runtime_error("gemv: pending slab count must be 0, 2 or 4");
+    if (asrc == A_LN && (a.n_pend < 0 || a.n_pend > 4 || a.n_pend == 3))
+        throw std::runtime_error("gemv: pending slab count must be 0, 1, 2 or 4");
+    if (a.p_resid && mode != GV_PARTIAL) throw std::runtime_error("gemv: residual rows into slab 0 need partial outputs");
     if (asrc == A_LN)
         for (int p = 0; p < 4; ++p)
             if (!a.pend[p]) throw std::runtime_error("gemv: LayerNorm prologue needs 4 pending slabs (zero slab if none)");

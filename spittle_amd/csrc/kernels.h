@@ -132,7 +132,7 @@ struct GemvArgs {
     // A rows: row i at A + (i * lda + a_row0); A_DIRECT: dtype activations; A_LN: f32 residual rows
     const void* A; int lda; int a_row0;
     const float* ln_w; const float* ln_b; // A_LN: LayerNorm of x + pend[0] + .. + pend[3]
-    const float* pend[4]; int n_pend;     // A_LN: pending partial slabs (same layout as A): n_pend = 0, 2 or 4
+    const float* pend[4]; int n_pend;     // A_LN: pending partial slabs (same layout as A): n_pend = 0, 1, 2 or 4
     float* x_out;                         // A_LN: combined rows written here by workgroup (0, 0) (or nullptr)
     const float* apart; int a_splits, a_heads;  // A_ATTN: cross-attention chunk partials [R][H][S][66] (S = 2..4, 8)
     int R;                                // rows (<= 64)
@@ -140,6 +140,7 @@ struct GemvArgs {
     const float* bias;
     void* C; int ldc;                     // output rows (GV_BIAS*, GV_LOGITS, GV_PARTIAL; GV_BIAS_RESID: f32 C += ...)
     int ksplit; int64_t c_split;          // GV_PARTIAL: K split over workgroups, slab s at C + s * c_split (f32)
+    const float* p_resid;                 // GV_PARTIAL (or nullptr): f32 rows [R][ldc] added into slab 0
     // GV_QKV_CACHE: q -> C, k/v -> cache [2][B][H][ctx][64] at position pos0 + t (row = b*Tq + t)
     void* cache; int cache_B, cache_H, cache_ctx, Tq;
     const DecState* st;

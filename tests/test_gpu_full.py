@@ -393,6 +393,28 @@ def test_cross_attention_strategies_bitwise(tiny, kind, vw, monkeypatch):
         assert np.array_equal(np.asarray(a.top1), np.asarray(b.top1))
 
 
+@pytest.mark.parametrize("kind", ["greedy", "beam5"])
+def test_fc2_residual_fold_bitwise(tiny, kind, monkeypatch):
+    """fc2's first K split adds the residual into its slab (r6), so the next LayerNorm prologue sums
+    slab 0 + slab 1 instead of x + slab 0 + slab 1: the same additions in the same order, so the
+    result is bitwise that of the unfolded passes (SPT_DEC_XFOLD=0, a new engine's captures)."""
+    from spittle_amd import WhisperEngine, WhisperModelParams
+    e, _ = tiny
+    xs = [O.synth_audio(89, 12 * 16000), O.synth_audio(90, 35 * 16000)]
+    kw = dict(beam_size=5, max_new_tokens=10) if kind == "beam5" else dict(max_new_tokens=24)
+    ref = e.transcribe_batch(xs, _params(**kw))
+    monkeypatch.setenv("SPT_DEC_XFOLD", "0")
+    e2 = WhisperEngine(WhisperModelParams(dtype="f32", max_batch=8, seed=SEED))
+    try:
+        e2.load_model("synthetic:tiny.en")
+        got = e2.transcribe_batch(xs, _params(**kw))
+    finally:
+        e2.unload_model()
+    for a, b in zip(ref, got):
+        assert a.tokens == b.tokens and a.text == b.text
+        assert np.array_equal(np.asarray(a.top1), np.asarray(b.top1))
+
+
 @pytest.mark.parametrize("kind", ["beam5", "fallback_best_of5"])
 def test_shared_window_bitwise_equal_to_copies(tiny, kind, monkeypatch):
     """The decoders of one utterance (beam 5, best_of 5) read one shared encoded window; the

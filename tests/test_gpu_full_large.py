@@ -174,6 +174,24 @@ def test_large_v3_beam5_cross_attention_strategies_bitwise(large, vw, monkeypatc
     assert a.tokens == b.tokens and np.array_equal(np.asarray(a.top1), np.asarray(b.top1))
 
 
+def test_large_v3_fc2_residual_fold_bitwise(large, monkeypatch):
+    """Greedy and beam 5 at large-v3 width in bf16: fc2's residual fold into slab 0 (default)
+    gives bitwise the unfolded passes' result (SPT_DEC_XFOLD=0, a new engine's captures)."""
+    from spittle_amd import WhisperEngine, WhisperModelParams
+    e, _ = large
+    x = _audio(20, 194)
+    a = [e.transcribe_samples(x, _params(max_new_tokens=24)), e.transcribe_samples(x, _params(beam_size=5, max_new_tokens=12))]
+    monkeypatch.setenv("SPT_DEC_XFOLD", "0")
+    e2 = WhisperEngine(WhisperModelParams(dtype="bf16", max_batch=8, seed=SEED))
+    try:
+        e2.load_model(SPEC)
+        b = [e2.transcribe_samples(x, _params(max_new_tokens=24)), e2.transcribe_samples(x, _params(beam_size=5, max_new_tokens=12))]
+    finally:
+        e2.unload_model()
+    for ra, rb in zip(a, b):
+        assert ra.tokens == rb.tokens and np.array_equal(np.asarray(ra.top1), np.asarray(rb.top1))
+
+
 def test_large_v3_beam5_dedup_batch_geometry():
     """Beam 5 at large-v3 width in bf16 (38 rows per pass): the same utterance alone, beside 1, 3
     and 6 others (one engine call of 10, 20, 35 rows) and in a call of 9 utterances split over two
