@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <stdexcept>
 
 #include "common.h"
@@ -168,6 +169,9 @@ void ParakeetEngine::release() {
     if (win_) (void)hipFree(win_);
     if (basis_) (void)hipFree(basis_);
     if (fbT_) (void)hipFree(fbT_);
+    if (pin_) (void)hipHostFree(pin_);
+    pin_ = nullptr;
+    pin_cap_ = 0;
     warena_ = aarena_ = nullptr;
     scratch_ = win_ = basis_ = fbT_ = nullptr;
     if (st_) (void)hipStreamDestroy(st_);
@@ -788,16 +792,49 @@ void ParakeetEngine::transcribe_host(const float* const* pcm, const int* n, int 
                                      std::vector<PkUtt>* out) {
     if (B < 1 || B > max_batch_) throw std::runtime_error("batch must be in [1, max_batch]");
     select();
-    HIP_CHECK(hipEventRecord(ev_[4], st_));
+    int nmax = 0;
     for (int b = 0; b < B; ++b) {
         if (n[b] < 0 || n[b] > max_samples_) throw std::runtime_error("utterance length out of range");
-        if (n[b]) HIP_CHECK(hipMemcpyAsync(pcm_ + (size_t)b * max_samples_, pcm[b], (size_t)n[b] * 4, hipMemcpyHostToDevice, st_));
+        if (n[b] > 0 && !pcm[b]) throw std::runtime_error("null pcm");
+        nmax = std::max(nmax, n[b]);
+    }
+    // Many short windows (C5: 64 x 1 s) paid a pageable copy each (0.68 ms for 4 MB): windows of
+    // up to 4 s are gathered into pinned rows of nmax samples and sent by one 2D copy (the tail of
+    // a shorter row is never read: the front end stops at n[b]).  Longer windows keep the pageable
+    // copies (8 x 30 s: the host gather cost more than it saved).  SPT_PK_PINNED=0: never, 2: always.
+    // h2d_ms = the host gather + the copy on the stream.
+    const int pin_env = getenv("SPT_PK_PINNED") ? atoi(getenv("SPT_PK_PINNED")) : 1;
+    const bool pinned = pin_env == 2 || (pin_env != 0 && nmax <= 4 * 16000);
+    double gather_ms = 0.0;
+    if (pinned && nmax > 0) {
+        const size_t need = (size_t)B * nmax;
+        if (need > pin_cap_) {
+            if (pin_) HIP_CHECK(hipHostFree(pin_));
+            pin_ = nullptr;
+            pin_cap_ = 0;
+            HIP_CHECK(hipHostMalloc((void**)&pin_, need * 4, hipHostMallocDefault));
+            pin_cap_ = need;
+        }
+        // the previous call's copy out of pin_ has completed (calls end by reading their results
+        // back on st_; this also covers one that threw part way)
+        HIP_CHECK(hipStreamSynchronize(st_));
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int b = 0; b < B; ++b)
+            if (n[b]) memcpy(pin_ + (size_t)b * nmax, pcm[b], (size_t)n[b] * 4);
+        gather_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        HIP_CHECK(hipEventRecord(ev_[4], st_));
+        HIP_CHECK(hipMemcpy2DAsync(pcm_, (size_t)max_samples_ * 4, pin_, (size_t)nmax * 4, (size_t)nmax * 4, B,
+                                   hipMemcpyHostToDevice, st_));
+    } else {
+        HIP_CHECK(hipEventRecord(ev_[4], st_));
+        for (int b = 0; b < B; ++b)
+            if (n[b]) HIP_CHECK(hipMemcpyAsync(pcm_ + (size_t)b * max_samples_, pcm[b], (size_t)n[b] * 4, hipMemcpyHostToDevice, st_));
     }
     HIP_CHECK(hipEventRecord(ev_[5], st_));
     transcribe_device(pcm_, max_samples_, n, B, max_symbols, out);
     float ms;
     HIP_CHECK(hipEventElapsedTime(&ms, ev_[4], ev_[5]));
-    tm_.h2d_ms = ms;
+    tm_.h2d_ms = ms + gather_ms;
 }
 
 void ParakeetEngine::debug_mel(const float* pcm_host, int n, float* out_host) {

@@ -156,6 +156,9 @@ private:
     char* aarena_ = nullptr;
     int64_t abytes_ = 0;
     float* pcm_ = nullptr;
+    // pinned host staging of transcribe_host's PCM: one DMA instead of a pageable copy per window
+    float* pin_ = nullptr;
+    size_t pin_cap_ = 0;  // floats
     int *nsamp_ = nullptr, *lens_ = nullptr;
     float *frames_ = nullptr, *spec_ = nullptr, *mel_ = nullptr;
     void *y1_ = nullptr, *y2a_ = nullptr, *y2_ = nullptr, *y3a_ = nullptr, *y3_ = nullptr;

@@ -151,6 +151,24 @@ def test_fp16_batch_is_bitwise_invariant(small16):
         assert list(rs.tokens) == list(rbi.tokens) and np.array_equal(rs.top1, rbi.top1)
 
 
+def test_pinned_staging_bitwise(small16, monkeypatch):
+    """transcribe_host gathers short windows into pinned rows of the batch's longest length and sends
+    them with one 2D copy (r6); the per-window pageable copies (SPT_PK_PINNED=0) give bitwise the
+    same result.  A short batch first, then a longer ragged one (the staging buffer grows, and the
+    rows' tails past each window's length hold stale samples the front end must not read)."""
+    e, _ = small16
+    short = [synth_audio(60 + i, 8000) for i in range(3)]
+    ragged = [synth_audio(70 + i, n) for i, n in enumerate([16000 * 2, 7777, 16000 + 160 * 5, 400, 12345])]
+    monkeypatch.setenv("SPT_PK_PINNED", "2")  # every batch (by default only windows up to 4 s)
+    got = [e.transcribe_batch(short, _tok_params()), e.transcribe_batch(ragged, _tok_params())]
+    monkeypatch.setenv("SPT_PK_PINNED", "0")
+    ref = [e.transcribe_batch(short, _tok_params()), e.transcribe_batch(ragged, _tok_params())]
+    for g, r in zip(got, ref):
+        for a, b in zip(g, r):
+            assert list(a.tokens) == list(b.tokens) and list(a.frames) == list(b.frames)
+            assert np.array_equal(a.top1, b.top1)
+
+
 def test_long_utterance_is_decoded_whole():
     """A recording longer than the context's max_seconds is decoded in one pass (the reference's
     ParakeetEngine::transcribe_samples takes the whole buffer): the workspace grows to its length,
