@@ -172,6 +172,12 @@ void ParakeetEngine::release() {
     if (pin_) (void)hipHostFree(pin_);
     pin_ = nullptr;
     pin_cap_ = 0;
+    if (hst_pin_) (void)hipHostFree(hst_pin_);
+    hst_pin_ = nullptr;
+    hst_cap_ = 0;
+    if (res_pin_) (void)hipHostFree(res_pin_);
+    res_pin_ = nullptr;
+    res_cap_ = 0;
     warena_ = aarena_ = nullptr;
     scratch_ = win_ = basis_ = fbT_ = nullptr;
     if (st_) (void)hipStreamDestroy(st_);
@@ -723,37 +729,60 @@ void ParakeetEngine::run_decode(int B, int T3p, int max_symbols, std::vector<PkU
     }
     // every joint evaluation advances a frame or emits one of <= max_symbols tokens of it
     const int max_steps = T3p * (max_symbols + 1) + kStepsPerGraph;
-    hstate_.resize(B);
+    // read-backs into pinned memory: the state after every graph, then only the emitted prefix of
+    // each output row (r6: four whole [B][cap] pageable copies -- 6 MB at B = 64 -- cost the C5
+    // call more host time than its decoder's GPU time)
+    if (B > hst_cap_) {
+        if (hst_pin_) HIP_CHECK(hipHostFree(hst_pin_));
+        hst_pin_ = nullptr;
+        hst_cap_ = 0;
+        HIP_CHECK(hipHostMalloc((void**)&hst_pin_, (size_t)B * sizeof(PkState), hipHostMallocDefault));
+        hst_cap_ = B;
+    }
     int steps = 0;
     while (true) {
         if (no_graph) for (int s = 0; s < kStepsPerGraph; ++s) enqueue_step(B, max_symbols, cap_, s & 1);
         else HIP_CHECK(hipGraphLaunch(it->second, st_));
         steps += kStepsPerGraph;
-        HIP_CHECK(hipMemcpyAsync(hstate_.data(), state_, B * sizeof(PkState), hipMemcpyDeviceToHost, st_));
+        HIP_CHECK(hipMemcpyAsync(hst_pin_, state_, B * sizeof(PkState), hipMemcpyDeviceToHost, st_));
         HIP_CHECK(hipStreamSynchronize(st_));
         bool all = true;
-        for (int b = 0; b < B; ++b) all = all && hstate_[b].done;
+        for (int b = 0; b < B; ++b) all = all && hst_pin_[b].done;
         if (all) break;
         if (steps > max_steps) throw std::runtime_error("TDT decoding did not finish (internal error)");
     }
+    hstate_.assign(hst_pin_, hst_pin_ + B);
     tm_.n_steps = steps;
     HIP_CHECK(hipEventRecord(ev_[3], st_));
-    std::vector<int> tok((size_t)B * cap_), fr((size_t)B * cap_);
-    std::vector<float> t1((size_t)B * cap_), t2((size_t)B * cap_);
-    HIP_CHECK(hipMemcpyAsync(tok.data(), out_tok_, tok.size() * 4, hipMemcpyDeviceToHost, st_));
-    HIP_CHECK(hipMemcpyAsync(fr.data(), out_frame_, fr.size() * 4, hipMemcpyDeviceToHost, st_));
-    HIP_CHECK(hipMemcpyAsync(t1.data(), out_t1_, t1.size() * 4, hipMemcpyDeviceToHost, st_));
-    HIP_CHECK(hipMemcpyAsync(t2.data(), out_t2_, t2.size() * 4, hipMemcpyDeviceToHost, st_));
-    HIP_CHECK(hipStreamSynchronize(st_));
+    int nmo = 0;  // the longest emitted row
+    for (int b = 0; b < B; ++b) nmo = std::max(nmo, std::min(hstate_[b].n_out, cap_));
     out->assign(B, PkUtt{});
+    if (nmo == 0) return;
+    const size_t per = (size_t)B * nmo;  // one output's trimmed rows
+    if (4 * per > res_cap_) {
+        if (res_pin_) HIP_CHECK(hipHostFree(res_pin_));
+        res_pin_ = nullptr;
+        res_cap_ = 0;
+        HIP_CHECK(hipHostMalloc((void**)&res_pin_, 4 * per * 4, hipHostMallocDefault));
+        res_cap_ = 4 * per;
+    }
+    const void* src[4] = {out_tok_, out_frame_, out_t1_, out_t2_};
+    for (int k = 0; k < 4; ++k)
+        HIP_CHECK(hipMemcpy2DAsync(res_pin_ + k * per, (size_t)nmo * 4, src[k], (size_t)cap_ * 4, (size_t)nmo * 4, B,
+                                   hipMemcpyDeviceToHost, st_));
+    HIP_CHECK(hipStreamSynchronize(st_));
+    const int* tok = res_pin_;
+    const int* fr = res_pin_ + per;
+    const float* t1 = (const float*)(res_pin_ + 2 * per);
+    const float* t2 = (const float*)(res_pin_ + 3 * per);
     for (int b = 0; b < B; ++b) {
         const int n = std::min(hstate_[b].n_out, cap_);
         PkUtt& u = (*out)[b];
-        const size_t o = (size_t)b * cap_;
-        u.tok.assign(tok.begin() + o, tok.begin() + o + n);
-        u.frame.assign(fr.begin() + o, fr.begin() + o + n);
-        u.top1.assign(t1.begin() + o, t1.begin() + o + n);
-        u.top2.assign(t2.begin() + o, t2.begin() + o + n);
+        const size_t o = (size_t)b * nmo;
+        u.tok.assign(tok + o, tok + o + n);
+        u.frame.assign(fr + o, fr + o + n);
+        u.top1.assign(t1 + o, t1 + o + n);
+        u.top2.assign(t2 + o, t2 + o + n);
     }
 }
 

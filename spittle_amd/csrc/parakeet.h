@@ -159,6 +159,11 @@ private:
     // pinned host staging of transcribe_host's PCM: one DMA instead of a pageable copy per window
     float* pin_ = nullptr;
     size_t pin_cap_ = 0;  // floats
+    // pinned read-back of the decode state and of the emitted tokens (rows trimmed to the longest)
+    PkState* hst_pin_ = nullptr;
+    int hst_cap_ = 0;
+    int* res_pin_ = nullptr;
+    size_t res_cap_ = 0;  // 4-byte elements
     int *nsamp_ = nullptr, *lens_ = nullptr;
     float *frames_ = nullptr, *spec_ = nullptr, *mel_ = nullptr;
     void *y1_ = nullptr, *y2a_ = nullptr, *y2_ = nullptr, *y3a_ = nullptr, *y3_ = nullptr;
